@@ -82,6 +82,101 @@ int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,
                          const double* d_gate_xyz, double gate,
                          int32_t* d_pairs, int32_t* d_count, void* stream);
 
+
+/* ------------------------------------------------------------------------
+ * Bundle adjustment (BAL model) — replaces the reference's BAL block
+ * /root/reference/BundleAdjustment.py:287-402 (rotate / project / objective /
+ * bundle_adjustment_sparsity / least_squares TRF) with Levenberg-Marquardt on
+ * the normal equations: analytic 2x12 Jacobian per observation, f64 MFMA Gram
+ * [J_c | r | u]^T [J_c | r | u] per camera, point-block Schur complement,
+ * Cholesky of the reduced camera system.
+ *
+ * Camera layout per row: [r0 r1 r2 t0 t1 t2 f k1 k2] (BundleAdjustment.py:324).
+ * ---------------------------------------------------------------------- */
+
+/* objective() residuals (BundleAdjustment.py:331-369) in the caller's
+ * observation order: d_resid [n_obs][2] (= the reference's ravel order).
+ * Indices must be in range (checked by the host wrapper). */
+int slam_ba_residual(const double* d_cams, const double* d_pts, const int32_t* d_cam_idx,
+                     const int32_t* d_pt_idx, const double* d_qs, int n_obs,
+                     double* d_resid, void* stream);
+
+/* Per-observation residual and Jacobian (clamped like objective()):
+ * d_jac [n_obs][2][12] columns [w0 w1 w2 t0 t1 t2 f k1 k2 | X0 X1 X2]. */
+int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d_cam_idx,
+                     const int32_t* d_pt_idx, const double* d_qs, int n_obs,
+                     double* d_resid, double* d_jac, void* stream);
+
+/* LM state slots (doubles in slam_ba_problem.state). */
+#define SLAM_BA_ST_LAMBDA 0
+#define SLAM_BA_ST_NU 1
+#define SLAM_BA_ST_COST 2      /* 0.5*|r|^2 at the live parameters           */
+#define SLAM_BA_ST_COST_NEW 3  /* 0.5*|r|^2 at the last trial step            */
+#define SLAM_BA_ST_PRED 4      /* predicted reduction of the last trial step   */
+#define SLAM_BA_ST_RHO 5
+#define SLAM_BA_ST_ACCEPTED 6  /* 1 if the last trial step was accepted        */
+#define SLAM_BA_ST_CUR 7       /* which of the two parameter buffers is live   */
+#define SLAM_BA_ST_ITERS 8
+#define SLAM_BA_ST_NACCEPT 9
+#define SLAM_BA_ST_PRED_CAM 10
+#define SLAM_BA_ST_CHOL_FAIL 11
+#define SLAM_BA_ST_SLOTS 16
+
+/* Everything the LM iteration touches; all pointers are device pointers.
+ * Built by the host planner (slam355/ba.py): observations sorted by
+ * (point, camera); index tables are fixed for the life of a problem. */
+typedef struct slam_ba_problem {
+  int32_t n_cams, n_pts, n_obs;
+  int32_t n_cam_chunks;  /* camera-Gram work items                          */
+  int32_t n_blocks;      /* upper camera-pair blocks of S with >= 1 obs pair */
+  int32_t n_pair_chunks; /* Schur work items                                 */
+  int32_t n_pairs;
+  int32_t reserved;
+  double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
+  double* pts[2];               /* [P][3]                                      */
+  const int32_t* obs_cam;       /* [O] (sorted by point, then camera)          */
+  const int32_t* obs_pt;        /* [O]                                         */
+  const double* obs_q;          /* [O][2]                                      */
+  const int32_t* pt_ptr;        /* [P+1] CSR point -> obs                      */
+  const int32_t* cam_obs;       /* [O] obs ids grouped by camera               */
+  const int32_t* cam_chunks;    /* [n_cam_chunks][3] (cam, begin, end) in cam_obs */
+  const int32_t* cam_chunk_ptr; /* [C+1] chunk range of each camera            */
+  const int32_t* pair_o;        /* [n_pairs][2] (o1 in c1, o2 in c2), by block */
+  const int32_t* pair_chunks;   /* [n_pair_chunks][3] (block, begin, end)      */
+  const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2)                    */
+  const int32_t* block_chunk_ptr; /* [n_blocks+1]                              */
+  double* rec;                  /* [O][2][16] Jc(9) r u Jp(3) 0 0              */
+  double* wy;                   /* [O][54] W = Jc^T Jp (9x3), Y = W V*^-1       */
+  double* ptdata;               /* [P][12] e(3) g(3) diagV(3) -                 */
+  double* cam_part;             /* [n_cam_chunks][256] Gram partials           */
+  double* pair_part;            /* [n_pair_chunks][81] Schur partials          */
+  double* sys;                  /* S[(9C)^2] b[9C] g[9C] diagU[9C] cost[C]     */
+  double* chol;                 /* [(9C)^2] factor workspace (9C > 120 only)   */
+  double* delta_c;              /* [9C]                                        */
+  double* red_part;             /* [slam_ba_red_slots(P, O)]                   */
+  double* small;                /* [4] trial |r|^2, sum pred_p (all-reduced)   */
+  double* state;                /* [SLAM_BA_ST_SLOTS]                          */
+} slam_ba_problem;
+
+/* Number of doubles red_part needs for a problem of P points and O obs. */
+int slam_ba_red_slots(int n_pts, int n_obs);
+/* Doubles in the all-reduced system buffer: (9C)^2 + 27C + C. */
+long long slam_ba_sys_len(int n_cams);
+
+/* Phase 1 (per rank): linearise at the live parameters and build this
+ * rank's share of the reduced camera system into prob->sys. */
+int slam_ba_build_system(const slam_ba_problem* prob, void* stream);
+/* Phase 2 (after sys is summed over ranks): damp, Cholesky-solve for the
+ * camera step, back-substitute the point step, evaluate the trial cost
+ * partial sums into prob->small. */
+int slam_ba_solve_step(const slam_ba_problem* prob, void* stream);
+/* Phase 3 (after small is summed over ranks): LM accept/reject, lambda update. */
+int slam_ba_decide(const slam_ba_problem* prob, void* stream);
+/* Single-rank convenience: n_iter x (phase 1, 2, 3) with no host sync. */
+int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream);
+/* Reset the LM state: lambda0, nu = 2, cur = 0, counters = 0. */
+int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

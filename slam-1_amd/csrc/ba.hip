@@ -1,0 +1,698 @@
+// Levenberg-Marquardt bundle adjustment (BAL model) for gfx950.
+//
+// Replaces the reference's BAL block (/root/reference/BundleAdjustment.py:287-402:
+// rotate, project, objective with its two >5000 px clamps, the 2x12 sparsity
+// and scipy least_squares TRF) with LM on the normal equations, all state on
+// the device so a fixed number of iterations runs with no host round trip.
+//
+// One LM iteration = 10 launches:
+//   k_linearize     obs    -> rec[o] = [Jc(9) r u Jp(3) 0 0] per residual row
+//   k_points        point  -> V*_p, e_p = V*^-1 g_p, W_o = Jc^T Jp, Y_o = W_o V*^-1,
+//                             u_o = Jp e_p (written into rec column 10)
+//   k_cam_gram      chunk  -> f64 MFMA Gram  G = M^T M, M = [Jc | r | u] (2 rows/obs)
+//   k_pair_partials chunk  -> sum over obs pairs of Y_o1 W_o2^T (Schur terms)
+//   k_assemble      block  -> S = blockdiag(U) - sum(Y W^T), b = -Jc^T r - Jc^T u, ...
+//   (all-reduce of sys over ranks happens here for multi-GPU)
+//   k_solve         1 WG   -> damp, Cholesky, camera step, pred_cam, trial cameras
+//   k_backsub       point  -> point step, trial points, pred_p partials
+//   k_trial_cost    obs    -> |r(x+delta)|^2 partials
+//   k_reduce_small  1 WG   -> small = {sum r^2, sum pred_p}
+//   (all-reduce of small over ranks)
+//   k_decide        1 lane -> rho, accept/reject, lambda update, buffer swap
+#include "common.hpp"
+
+#include <cmath>
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr double kClamp = 5000.0;
+constexpr double kDiagMin = 1e-6, kDiagMax = 1e32;
+constexpr double kLamMin = 1e-16, kLamMax = 1e32;
+constexpr int kRecW = 16;  // doubles per residual row in rec
+constexpr int kBS = 256;   // block size of the element-wise kernels
+
+// ---------------------------------------------------------------- projection
+// Residual (proj - q) of BundleAdjustment.py:317-337 with the operation order
+// of the numpy code, and optionally its analytic 2x12 Jacobian.
+template <bool JAC>
+__device__ __forceinline__ void reproject(const double* __restrict__ cam,
+                                          const double* __restrict__ X,
+                                          const double* __restrict__ q, double r[2],
+                                          double J[2][12]) {
+  const double w0 = cam[0], w1 = cam[1], w2 = cam[2];
+  const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0;  // nan_to_num(w / 0) == 0  (:292-293)
+  if (th > 0.0) {
+    v0 = w0 / th;
+    v1 = w1 / th;
+    v2 = w2 / th;
+  }
+  const double X0 = X[0], X1 = X[1], X2 = X[2];
+  const double c = cos(th), s = sin(th);
+  const double dot = X0 * v0 + X1 * v1 + X2 * v2;
+  const double cx0 = v1 * X2 - v2 * X1;
+  const double cx1 = v2 * X0 - v0 * X2;
+  const double cx2 = v0 * X1 - v1 * X0;
+  const double omc = 1.0 - c;
+  const double dk = dot * omc;
+  const double RX0 = c * X0 + s * cx0 + dk * v0;
+  const double RX1 = c * X1 + s * cx1 + dk * v1;
+  const double RX2 = c * X2 + s * cx2 + dk * v2;
+  const double P0 = RX0 + cam[3], P1 = RX1 + cam[4], P2 = RX2 + cam[5];
+  const double p0 = -P0 / P2, p1 = -P1 / P2;
+  const double f = cam[6], k1 = cam[7], k2 = cam[8];
+  const double n = p0 * p0 + p1 * p1;
+  const double rad = 1.0 + k1 * n + k2 * (n * n);
+  const double sc = rad * f;
+  r[0] = p0 * sc - q[0];
+  r[1] = p1 * sc - q[1];
+  if constexpr (JAC) {
+    // R = c I + s [v]x + (1-c) v v^T
+    double R[3][3];
+    R[0][0] = c + omc * v0 * v0; R[0][1] = -s * v2 + omc * v0 * v1; R[0][2] = s * v1 + omc * v0 * v2;
+    R[1][0] = s * v2 + omc * v1 * v0; R[1][1] = c + omc * v1 * v1; R[1][2] = -s * v0 + omc * v1 * v2;
+    R[2][0] = -s * v1 + omc * v2 * v0; R[2][1] = s * v0 + omc * v2 * v1; R[2][2] = c + omc * v2 * v2;
+    // dRX/dw: Gallego & Yezzi: -R [X]x (w w^T + (R^T - I)[w]x) / |w|^2 ; -[RX]x at w = 0
+    double dR[3][3];
+    const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+    if (th2 < 1e-24) {
+      dR[0][0] = 0.0;  dR[0][1] = RX2;  dR[0][2] = -RX1;
+      dR[1][0] = -RX2; dR[1][1] = 0.0;  dR[1][2] = RX0;
+      dR[2][0] = RX1;  dR[2][1] = -RX0; dR[2][2] = 0.0;
+    } else {
+      const double W[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
+      const double w[3] = {w0, w1, w2};
+      double A[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) {
+          double acc = w[i] * w[k];
+          for (int j = 0; j < 3; ++j) acc += R[j][i] * W[j][k];
+          A[i][k] = acc - W[i][k];
+        }
+      const double Xs[3][3] = {{0.0, -X2, X1}, {X2, 0.0, -X0}, {-X1, X0, 0.0}};
+      double B[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          B[i][k] = Xs[i][0] * A[0][k] + Xs[i][1] * A[1][k] + Xs[i][2] * A[2][k];
+      const double inv = -1.0 / th2;
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          dR[i][k] = (R[i][0] * B[0][k] + R[i][1] * B[1][k] + R[i][2] * B[2][k]) * inv;
+    }
+    // dp/dP
+    const double iz = 1.0 / P2;
+    const double dpP[2][3] = {{-iz, 0.0, P0 * iz * iz}, {0.0, -iz, P1 * iz * iz}};
+    // dproj/dp = sc I + 2 f (k1 + 2 k2 n) p p^T
+    const double g2 = 2.0 * f * (k1 + 2.0 * k2 * n);
+    const double Dp[2][2] = {{sc + g2 * p0 * p0, g2 * p0 * p1}, {g2 * p1 * p0, sc + g2 * p1 * p1}};
+    double D[2][3];
+    for (int a = 0; a < 2; ++a)
+      for (int k = 0; k < 3; ++k) D[a][k] = Dp[a][0] * dpP[0][k] + Dp[a][1] * dpP[1][k];
+    const double pp[2] = {p0, p1};
+    for (int a = 0; a < 2; ++a) {
+      for (int k = 0; k < 3; ++k) {
+        J[a][k] = D[a][0] * dR[0][k] + D[a][1] * dR[1][k] + D[a][2] * dR[2][k];
+        J[a][3 + k] = D[a][k];
+        J[a][9 + k] = D[a][0] * R[0][k] + D[a][1] * R[1][k] + D[a][2] * R[2][k];
+      }
+      J[a][6] = pp[a] * rad;
+      J[a][7] = pp[a] * (f * n);
+      J[a][8] = pp[a] * (f * n * n);
+    }
+  }
+}
+
+// The two clamps of BundleAdjustment.py:339-350 (x first, then y on the
+// rescaled row), with the chain rule applied to J when JAC.
+template <bool JAC>
+__device__ __forceinline__ void clamp_rows(double r[2], double J[2][12]) {
+#pragma unroll
+  for (int comp = 0; comp < 2; ++comp) {
+    const double rc = r[comp];
+    if (fabs(rc) > kClamp) {
+      const double arc = fabs(rc);
+      const double half = comp == 0 ? 613.0 : 185.0;
+      if constexpr (JAC) {
+        const double a = (half * 2.0) / arc;
+        double Jc[12];
+        for (int k = 0; k < 12; ++k) Jc[k] = J[comp][k];
+        for (int row = 0; row < 2; ++row) {
+          const double ratio = r[row] / rc;
+          for (int k = 0; k < 12; ++k) J[row][k] = a * (J[row][k] - ratio * Jc[k]);
+        }
+      }
+      r[0] = r[0] / arc * half * 2.0;
+      r[1] = r[1] / arc * half * 2.0;
+    }
+  }
+}
+
+__device__ __forceinline__ double block_sum(double v, double* lds) {
+  // deterministic: fixed shuffle tree then fixed LDS order
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) s += lds[w];
+  }
+  __syncthreads();
+  return s;  // valid on thread 0
+}
+
+// ---------------------------------------------------------------- standalone
+__global__ __launch_bounds__(kBS) void k_residual(const double* __restrict__ cams,
+                                                  const double* __restrict__ pts,
+                                                  const int32_t* __restrict__ ci,
+                                                  const int32_t* __restrict__ pi,
+                                                  const double* __restrict__ qs, int n_obs,
+                                                  double* __restrict__ resid,
+                                                  double* __restrict__ jac) {
+  const int o = blockIdx.x * kBS + threadIdx.x;
+  if (o >= n_obs) return;
+  double r[2], J[2][12];
+  if (jac) {
+    reproject<true>(cams + 9 * ci[o], pts + 3 * pi[o], qs + 2 * o, r, J);
+    clamp_rows<true>(r, J);
+    for (int a = 0; a < 2; ++a)
+      for (int k = 0; k < 12; ++k) jac[(size_t)o * 24 + a * 12 + k] = J[a][k];
+  } else {
+    reproject<false>(cams + 9 * ci[o], pts + 3 * pi[o], qs + 2 * o, r, J);
+    clamp_rows<false>(r, J);
+  }
+  resid[2 * o] = r[0];
+  resid[2 * o + 1] = r[1];
+}
+
+// ---------------------------------------------------------------- LM kernels
+__device__ __forceinline__ int cur_of(const double* state) {
+  return state[SLAM_BA_ST_CUR] != 0.0 ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kBS) void k_linearize(slam_ba_problem p) {
+  const int o = blockIdx.x * kBS + threadIdx.x;
+  if (o >= p.n_obs) return;
+  const int cur = cur_of(p.state);
+  double r[2], J[2][12];
+  reproject<true>(p.cams[cur] + 9 * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o], p.obs_q + 2 * o,
+                  r, J);
+  clamp_rows<true>(r, J);
+  double* rec = p.rec + (size_t)o * 2 * kRecW;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    double* row = rec + a * kRecW;
+    for (int k = 0; k < 9; ++k) row[k] = J[a][k];
+    row[9] = r[a];
+    row[10] = 0.0;
+    row[11] = J[a][9];
+    row[12] = J[a][10];
+    row[13] = J[a][11];
+    row[14] = 0.0;
+    row[15] = 0.0;
+  }
+}
+
+__device__ __forceinline__ double clampd(double d) { return fmin(fmax(d, kDiagMin), kDiagMax); }
+
+__global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
+  const int pt = blockIdx.x * kBS + threadIdx.x;
+  if (pt >= p.n_pts) return;
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  const int b = p.pt_ptr[pt], e = p.pt_ptr[pt + 1];
+  double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  for (int o = b; o < e; ++o) {
+    const double* rec = p.rec + (size_t)o * 2 * kRecW;
+    for (int a = 0; a < 2; ++a) {
+      const double* row = rec + a * kRecW;
+      const double j0 = row[11], j1 = row[12], j2 = row[13], rr = row[9];
+      V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
+      V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
+      g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
+    }
+  }
+  const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
+  const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
+  const double a01 = V01, a02 = V02, a12 = V12;
+  // inverse of the symmetric 3x3 by cofactors
+  const double c00 = a11 * a22 - a12 * a12;
+  const double c01 = a02 * a12 - a01 * a22;
+  const double c02 = a01 * a12 - a02 * a11;
+  const double c11 = a00 * a22 - a02 * a02;
+  const double c12 = a01 * a02 - a00 * a12;
+  const double c22 = a00 * a11 - a01 * a01;
+  const double det = a00 * c00 + a01 * c01 + a02 * c02;
+  const double id = det != 0.0 ? 1.0 / det : 0.0;
+  const double Vi[3][3] = {{c00 * id, c01 * id, c02 * id},
+                           {c01 * id, c11 * id, c12 * id},
+                           {c02 * id, c12 * id, c22 * id}};
+  const double e0 = Vi[0][0] * g0 + Vi[0][1] * g1 + Vi[0][2] * g2;
+  const double e1 = Vi[1][0] * g0 + Vi[1][1] * g1 + Vi[1][2] * g2;
+  const double e2 = Vi[2][0] * g0 + Vi[2][1] * g1 + Vi[2][2] * g2;
+  double* pd = p.ptdata + (size_t)pt * 12;
+  pd[0] = e0; pd[1] = e1; pd[2] = e2;
+  pd[3] = g0; pd[4] = g1; pd[5] = g2;
+  pd[6] = d0; pd[7] = d1; pd[8] = d2;
+  for (int o = b; o < e; ++o) {
+    double* rec = p.rec + (size_t)o * 2 * kRecW;
+    double W[9][3];
+    for (int i = 0; i < 9; ++i) {
+      const double a0 = rec[i], a1 = rec[kRecW + i];
+      for (int c = 0; c < 3; ++c) W[i][c] = a0 * rec[11 + c] + a1 * rec[kRecW + 11 + c];
+    }
+    double* wy = p.wy + (size_t)o * 54;
+    for (int i = 0; i < 9; ++i) {
+      for (int c = 0; c < 3; ++c) wy[i * 3 + c] = W[i][c];
+      for (int c = 0; c < 3; ++c)
+        wy[27 + i * 3 + c] = W[i][0] * Vi[0][c] + W[i][1] * Vi[1][c] + W[i][2] * Vi[2][c];
+    }
+    for (int a = 0; a < 2; ++a) {
+      double* row = rec + a * kRecW;
+      row[10] = row[11] * e0 + row[12] * e1 + row[13] * e2;
+    }
+  }
+}
+
+// f64 MFMA Gram of M = [Jc | r | u | Jp | 0 0] over one chunk of a camera's
+// observations: G = M^T M.  v_mfma_f64_16x16x4_f64: lane l holds
+// A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; with A = M^T, B = M both are
+// the same element M[k][l&15], so every lane loads one double per MFMA and one
+// MFMA consumes 4 residual rows = 2 observations.
+constexpr int kGramWG = 256;
+__global__ __launch_bounds__(kGramWG) void k_cam_gram(slam_ba_problem p) {
+  __shared__ double red[4][256];
+  const int ch = blockIdx.x;
+  const int beg = p.cam_chunks[3 * ch + 1], end = p.cam_chunks[3 * ch + 2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int krow = lane >> 4, col = lane & 15;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  // each MFMA step covers 2 observations; the 4 waves interleave steps
+  for (int s = beg + 2 * wid; s < end; s += 8) {
+    const int oi = s + (krow >> 1);
+    double v = 0.0;
+    if (oi < end) {
+      const int o = p.cam_obs[oi];
+      v = p.rec[(size_t)o * 2 * kRecW + (krow & 1) * kRecW + col];
+    }
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+  }
+  // D layout (f64): col = lane&15, row = (lane>>4) + 4*reg
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][(krow + 4 * r) * 16 + col] = acc[r];
+  __syncthreads();
+  const int t = threadIdx.x;
+  p.cam_part[(size_t)ch * 256 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
+// Schur terms: sum over the chunk's obs pairs of Y_o1 (9x3) W_o2^T (3x9).
+constexpr int kPairChunk = 64;
+constexpr int kPairWG = 256;
+__global__ __launch_bounds__(kPairWG) void k_pair_partials(slam_ba_problem p) {
+  __shared__ double sy[kPairChunk][27];
+  __shared__ double sw[kPairChunk][27];
+  __shared__ double red[3][81];
+  const int ch = blockIdx.x;
+  const int beg = p.pair_chunks[3 * ch + 1], end = p.pair_chunks[3 * ch + 2];
+  const int n = end - beg;
+  for (int i = threadIdx.x; i < n * 27; i += kPairWG) {
+    const int k = i / 27, e = i - k * 27;
+    const int o1 = p.pair_o[2 * (beg + k)], o2 = p.pair_o[2 * (beg + k) + 1];
+    sy[k][e] = p.wy[(size_t)o1 * 54 + 27 + e];
+    sw[k][e] = p.wy[(size_t)o2 * 54 + e];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < 243) {
+    const int g = t / 81, ent = t - g * 81, i = ent / 9, j = ent - i * 9;
+    double acc = 0.0;
+    for (int k = g; k < n; k += 3)
+      acc += sy[k][3 * i] * sw[k][3 * j] + sy[k][3 * i + 1] * sw[k][3 * j + 1] +
+             sy[k][3 * i + 2] * sw[k][3 * j + 2];
+    red[g][ent] = acc;
+  }
+  __syncthreads();
+  if (t < 81) p.pair_part[(size_t)ch * 81 + t] = (red[0][t] + red[1][t]) + red[2][t];
+}
+
+// One workgroup per upper block (c1 <= c2): S block = [U_c] - sum(Y W^T).
+__global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
+  __shared__ double G[256];
+  const int blk = blockIdx.x;
+  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
+  const int C9 = 9 * p.n_cams;
+  double* S = p.sys;
+  double* bvec = S + (size_t)C9 * C9;
+  double* gvec = bvec + C9;
+  double* diagU = gvec + C9;
+  double* costc = diagU + C9;
+  const int t = threadIdx.x;
+  if (c1 == c2) {
+    double acc = 0.0;
+    for (int ch = p.cam_chunk_ptr[c1]; ch < p.cam_chunk_ptr[c1 + 1]; ++ch)
+      acc += p.cam_part[(size_t)ch * 256 + t];
+    G[t] = acc;
+  }
+  __syncthreads();
+  if (t < 81) {
+    double acc = 0.0;
+    for (int ch = p.block_chunk_ptr[blk]; ch < p.block_chunk_ptr[blk + 1]; ++ch)
+      acc += p.pair_part[(size_t)ch * 81 + t];
+    const int i = t / 9, j = t - i * 9;
+    if (c1 == c2) {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = G[i * 16 + j] - acc;
+    } else {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = -acc;
+      S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = -acc;
+    }
+  }
+  if (c1 == c2 && t < 9) {
+    // G row i: [.. U .. | col 9 = Jc^T r | col 10 = Jc^T u]
+    gvec[9 * c1 + t] = -G[t * 16 + 9];
+    bvec[9 * c1 + t] = -G[t * 16 + 9] - G[t * 16 + 10];
+    diagU[9 * c1 + t] = G[t * 16 + t];
+  }
+  if (c1 == c2 && t == 0) costc[c1] = G[9 * 16 + 9];
+}
+
+// ---------------------------------------------------------------- solve
+constexpr int kSolveWG = 1024;
+constexpr int kLdsMaxN = 120;  // 120*120*8 = 115 KB of LDS
+constexpr int kSolveHdr = 32;  // doubles of LDS header in k_solve
+
+// Right-looking Cholesky (lower) of the n x n matrix A (row stride ld) in
+// place, then solve A x = b (b overwritten with x).  Returns false if not SPD.
+__device__ bool chol_solve(double* A, int n, int ld, double* b, int* fail) {
+  const int t = threadIdx.x;
+  for (int k = 0; k < n; ++k) {
+    if (t == 0) {
+      const double akk = A[(size_t)k * ld + k];
+      if (!(akk > 0.0) || !isfinite(akk)) *fail = 1;
+      A[(size_t)k * ld + k] = sqrt(fmax(akk, 1e-300));
+    }
+    __syncthreads();
+    if (*fail) return false;
+    const double dk = A[(size_t)k * ld + k];
+    for (int i = k + 1 + t; i < n; i += kSolveWG) A[(size_t)i * ld + k] /= dk;
+    __syncthreads();
+    const int m = n - k - 1;
+    for (int idx = t; idx < m * m; idx += kSolveWG) {
+      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
+      if (j <= i) A[(size_t)i * ld + j] -= A[(size_t)i * ld + k] * A[(size_t)j * ld + k];
+    }
+    __syncthreads();
+  }
+  // forward: L y = b
+  for (int k = 0; k < n; ++k) {
+    if (t == 0) b[k] /= A[(size_t)k * ld + k];
+    __syncthreads();
+    const double yk = b[k];
+    for (int i = k + 1 + t; i < n; i += kSolveWG) b[i] -= A[(size_t)i * ld + k] * yk;
+    __syncthreads();
+  }
+  // backward: L^T x = y
+  for (int k = n - 1; k >= 0; --k) {
+    if (t == 0) b[k] /= A[(size_t)k * ld + k];
+    __syncthreads();
+    const double xk = b[k];
+    for (int i = t; i < k; i += kSolveWG) b[i] -= A[(size_t)k * ld + i] * xk;
+    __syncthreads();
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
+  // All LDS in the dynamic region (16-byte aligned base, Guideline 17):
+  // [0,16) block_sum scratch, [16] fail flag, [32, ...) A then x when in LDS.
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* red = lds;
+  int* fail_p = reinterpret_cast<int*>(lds + 16);
+  const int C9 = 9 * p.n_cams;
+  const double* S = p.sys;
+  const double* bvec = S + (size_t)C9 * C9;
+  const double* gvec = bvec + C9;
+  const double* diagU = gvec + C9;
+  const double* costc = diagU + C9;
+  double* state = p.state;
+  const double lam = state[SLAM_BA_ST_LAMBDA];
+  const int t = threadIdx.x;
+  const bool in_lds = C9 <= kLdsMaxN;
+  double* A = in_lds ? lds + kSolveHdr : p.chol;
+  double* x = in_lds ? lds + kSolveHdr + (size_t)C9 * C9 : p.delta_c;
+  if (t == 0) *fail_p = 0;
+  for (int idx = t; idx < C9 * C9; idx += kSolveWG) {
+    const int i = idx / C9, j = idx - i * C9;
+    double a = S[idx];
+    if (i == j) a += lam * clampd(diagU[i]);
+    A[idx] = a;
+  }
+  for (int i = t; i < C9; i += kSolveWG) x[i] = bvec[i];
+  __syncthreads();
+  const bool ok = chol_solve(A, C9, C9, x, fail_p);
+  const int cur = cur_of(state);
+  double pc = 0.0;
+  for (int i = t; i < C9; i += kSolveWG) {
+    const double d = ok ? x[i] : 0.0;
+    p.delta_c[i] = d;
+    p.cams[1 - cur][i] = p.cams[cur][i] + d;
+    pc += d * (lam * clampd(diagU[i]) * d + gvec[i]);
+  }
+  pc = block_sum(pc, red);
+  if (t == 0) {
+    double cost = 0.0;
+    for (int c = 0; c < p.n_cams; ++c) cost += costc[c];
+    state[SLAM_BA_ST_COST] = 0.5 * cost;
+    state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
+    state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : 1.0;
+  }
+}
+
+__global__ __launch_bounds__(kBS) void k_backsub(slam_ba_problem p, double* __restrict__ part) {
+  __shared__ double red[kBS / 64];
+  const int pt = blockIdx.x * kBS + threadIdx.x;
+  const int cur = cur_of(p.state);
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  double pred = 0.0;
+  if (pt < p.n_pts) {
+    const double* pd = p.ptdata + (size_t)pt * 12;
+    double d0 = pd[0], d1 = pd[1], d2 = pd[2];
+    for (int o = p.pt_ptr[pt]; o < p.pt_ptr[pt + 1]; ++o) {
+      const double* Y = p.wy + (size_t)o * 54 + 27;
+      const double* dc = p.delta_c + 9 * p.obs_cam[o];
+      for (int i = 0; i < 9; ++i) {
+        d0 -= Y[3 * i] * dc[i];
+        d1 -= Y[3 * i + 1] * dc[i];
+        d2 -= Y[3 * i + 2] * dc[i];
+      }
+    }
+    const double* x = p.pts[cur] + 3 * pt;
+    double* xn = p.pts[1 - cur] + 3 * pt;
+    xn[0] = x[0] + d0;
+    xn[1] = x[1] + d1;
+    xn[2] = x[2] + d2;
+    pred = d0 * (lam * pd[6] * d0 + pd[3]) + d1 * (lam * pd[7] * d1 + pd[4]) +
+           d2 * (lam * pd[8] * d2 + pd[5]);
+    if (p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0) pred = 0.0;
+  }
+  const double s = block_sum(pred, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBS) void k_trial_cost(slam_ba_problem p, double* __restrict__ part) {
+  __shared__ double red[kBS / 64];
+  const int o = blockIdx.x * kBS + threadIdx.x;
+  const int nxt = 1 - cur_of(p.state);
+  double v = 0.0;
+  if (o < p.n_obs) {
+    double r[2], J[2][12];
+    reproject<false>(p.cams[nxt] + 9 * p.obs_cam[o], p.pts[nxt] + 3 * p.obs_pt[o],
+                     p.obs_q + 2 * o, r, J);
+    clamp_rows<false>(r, J);
+    v = r[0] * r[0] + r[1] * r[1];
+  }
+  const double s = block_sum(v, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+constexpr int kRedWG = 1024;
+__global__ __launch_bounds__(kRedWG) void k_reduce_small(const double* __restrict__ cost_part,
+                                                         int n_cost, const double* __restrict__ pred_part,
+                                                         int n_pred, double* __restrict__ small) {
+  __shared__ double red[kRedWG / 64];
+  double a = 0.0, b = 0.0;
+  for (int i = threadIdx.x; i < n_cost; i += kRedWG) a += cost_part[i];
+  for (int i = threadIdx.x; i < n_pred; i += kRedWG) b += pred_part[i];
+  a = block_sum(a, red);
+  b = block_sum(b, red);
+  if (threadIdx.x == 0) {
+    small[0] = a;
+    small[1] = b;
+  }
+}
+
+__global__ void k_decide(double* __restrict__ state, const double* __restrict__ small) {
+  if (threadIdx.x != 0) return;
+  const double cost = state[SLAM_BA_ST_COST];
+  const double cost_new = 0.5 * small[0];
+  const double pred = state[SLAM_BA_ST_PRED_CAM] + 0.5 * small[1];
+  const bool fail = state[SLAM_BA_ST_CHOL_FAIL] != 0.0;
+  const double rho = (!fail && pred > 0.0) ? (cost - cost_new) / pred : -1.0;
+  double lam = state[SLAM_BA_ST_LAMBDA], nu = state[SLAM_BA_ST_NU];
+  const bool acc = rho > 0.0 && isfinite(cost_new);
+  if (acc) {
+    const double t = 2.0 * rho - 1.0;
+    lam *= fmax(1.0 / 3.0, 1.0 - t * t * t);
+    lam = fmin(fmax(lam, kLamMin), kLamMax);
+    nu = 2.0;
+    state[SLAM_BA_ST_CUR] = state[SLAM_BA_ST_CUR] != 0.0 ? 0.0 : 1.0;
+    state[SLAM_BA_ST_COST] = cost_new;
+    state[SLAM_BA_ST_NACCEPT] += 1.0;
+  } else {
+    lam = fmin(lam * nu, kLamMax);
+    nu *= 2.0;
+  }
+  state[SLAM_BA_ST_LAMBDA] = lam;
+  state[SLAM_BA_ST_NU] = nu;
+  state[SLAM_BA_ST_COST_NEW] = cost_new;
+  state[SLAM_BA_ST_PRED] = pred;
+  state[SLAM_BA_ST_RHO] = rho;
+  state[SLAM_BA_ST_ACCEPTED] = acc ? 1.0 : 0.0;
+  state[SLAM_BA_ST_ITERS] += 1.0;
+}
+
+__global__ void k_reset(double* state, double lam0) {
+  const int t = threadIdx.x;
+  if (t < SLAM_BA_ST_SLOTS) state[t] = 0.0;
+  if (t == 0) {
+    state[SLAM_BA_ST_LAMBDA] = lam0;
+    state[SLAM_BA_ST_NU] = 2.0;
+  }
+}
+
+inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
+
+int check_problem(const slam_ba_problem* p) {
+  SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
+  SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->rec && p->wy && p->sys && p->state && p->small &&
+                   p->red_part && p->delta_c,
+               "slam_ba: null buffer");
+  SLAM_REQUIRE(9 * p->n_cams <= kLdsMaxN || p->chol != nullptr,
+               "slam_ba: chol workspace required for 9C > %d", kLdsMaxN);
+  return SLAM_OK;
+}
+
+}  // namespace
+
+extern "C" int slam_ba_red_slots(int n_pts, int n_obs) {
+  return nblk(n_obs, kBS) + nblk(n_pts, kBS) + 1;
+}
+
+extern "C" long long slam_ba_sys_len(int n_cams) {
+  const long long c9 = 9ll * n_cams;
+  return c9 * c9 + 3 * c9 + n_cams;
+}
+
+extern "C" int slam_ba_residual(const double* d_cams, const double* d_pts,
+                                const int32_t* d_cam_idx, const int32_t* d_pt_idx,
+                                const double* d_qs, int n_obs, double* d_resid, void* stream) {
+  SLAM_REQUIRE(n_obs >= 0, "slam_ba_residual: n_obs < 0");
+  if (n_obs == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_cams && d_pts && d_cam_idx && d_pt_idx && d_qs && d_resid,
+               "slam_ba_residual: null pointer");
+  k_residual<<<nblk(n_obs, kBS), kBS, 0, slam::as_stream(stream)>>>(
+      d_cams, d_pts, d_cam_idx, d_pt_idx, d_qs, n_obs, d_resid, nullptr);
+  SLAM_LAUNCHED("k_residual");
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_jacobian(const double* d_cams, const double* d_pts,
+                                const int32_t* d_cam_idx, const int32_t* d_pt_idx,
+                                const double* d_qs, int n_obs, double* d_resid, double* d_jac,
+                                void* stream) {
+  SLAM_REQUIRE(n_obs >= 0, "slam_ba_jacobian: n_obs < 0");
+  if (n_obs == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_cams && d_pts && d_cam_idx && d_pt_idx && d_qs && d_resid && d_jac,
+               "slam_ba_jacobian: null pointer");
+  k_residual<<<nblk(n_obs, kBS), kBS, 0, slam::as_stream(stream)>>>(
+      d_cams, d_pts, d_cam_idx, d_pt_idx, d_qs, n_obs, d_resid, d_jac);
+  SLAM_LAUNCHED("k_residual(jac)");
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream) {
+  if (int rc = check_problem(prob)) return rc;
+  k_reset<<<1, 64, 0, slam::as_stream(stream)>>>(prob->state, lambda0);
+  SLAM_LAUNCHED("k_reset");
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
+  if (int rc = check_problem(prob)) return rc;
+  const slam_ba_problem& p = *prob;
+  hipStream_t s = slam::as_stream(stream);
+  SLAM_HIP(hipMemsetAsync(p.sys, 0, sizeof(double) * slam_ba_sys_len(p.n_cams), s));
+  if (p.n_obs > 0) {
+    k_linearize<<<nblk(p.n_obs, kBS), kBS, 0, s>>>(p);
+    SLAM_LAUNCHED("k_linearize");
+  }
+  if (p.n_pts > 0) {
+    k_points<<<nblk(p.n_pts, kBS), kBS, 0, s>>>(p);
+    SLAM_LAUNCHED("k_points");
+  }
+  if (p.n_cam_chunks > 0) {
+    k_cam_gram<<<p.n_cam_chunks, kGramWG, 0, s>>>(p);
+    SLAM_LAUNCHED("k_cam_gram");
+  }
+  if (p.n_pair_chunks > 0) {
+    k_pair_partials<<<p.n_pair_chunks, kPairWG, 0, s>>>(p);
+    SLAM_LAUNCHED("k_pair_partials");
+  }
+  if (p.n_blocks > 0) {
+    k_assemble<<<p.n_blocks, kBS, 0, s>>>(p);
+    SLAM_LAUNCHED("k_assemble");
+  }
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_solve_step(const slam_ba_problem* prob, void* stream) {
+  if (int rc = check_problem(prob)) return rc;
+  const slam_ba_problem& p = *prob;
+  hipStream_t s = slam::as_stream(stream);
+  const int C9 = 9 * p.n_cams;
+  const size_t lds = sizeof(double) * (kSolveHdr + (C9 <= kLdsMaxN ? (size_t)C9 * C9 + C9 : 0));
+  k_solve<<<1, kSolveWG, lds, s>>>(p);
+  SLAM_LAUNCHED("k_solve");
+  const int nb_cost = nblk(p.n_obs, kBS), nb_pts = nblk(p.n_pts, kBS);
+  double* cost_part = p.red_part;
+  double* pred_part = p.red_part + nb_cost;
+  if (p.n_pts > 0) {
+    k_backsub<<<nb_pts, kBS, 0, s>>>(p, pred_part);
+    SLAM_LAUNCHED("k_backsub");
+  }
+  if (p.n_obs > 0) {
+    k_trial_cost<<<nb_cost, kBS, 0, s>>>(p, cost_part);
+    SLAM_LAUNCHED("k_trial_cost");
+  }
+  k_reduce_small<<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small);
+  SLAM_LAUNCHED("k_reduce_small");
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_decide(const slam_ba_problem* prob, void* stream) {
+  if (int rc = check_problem(prob)) return rc;
+  k_decide<<<1, 64, 0, slam::as_stream(stream)>>>(prob->state, prob->small);
+  SLAM_LAUNCHED("k_decide");
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream) {
+  for (int i = 0; i < n_iter; ++i) {
+    if (int rc = slam_ba_build_system(prob, stream)) return rc;
+    if (int rc = slam_ba_solve_step(prob, stream)) return rc;
+    if (int rc = slam_ba_decide(prob, stream)) return rc;
+  }
+  return SLAM_OK;
+}

@@ -19,6 +19,26 @@ c_size_t = ctypes.c_size_t
 c_p = ctypes.c_void_p
 c_uint64 = ctypes.c_uint64
 
+c_i32 = ctypes.c_int32
+
+
+class BAProblemStruct(ctypes.Structure):
+    """Mirror of `slam_ba_problem` (include/slam355.h)."""
+    _fields_ = [
+        ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_cam_chunks", c_i32),
+        ("n_blocks", c_i32), ("n_pair_chunks", c_i32), ("n_pairs", c_i32), ("reserved", c_i32),
+        ("cams", c_p * 2), ("pts", c_p * 2),
+        ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p),
+        ("cam_obs", c_p), ("cam_chunks", c_p), ("cam_chunk_ptr", c_p),
+        ("pair_o", c_p), ("pair_chunks", c_p), ("blocks", c_p), ("block_chunk_ptr", c_p),
+        ("rec", c_p), ("wy", c_p), ("ptdata", c_p), ("cam_part", c_p), ("pair_part", c_p),
+        ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
+        ("state", c_p),
+    ]
+
+
+_PROB = ctypes.POINTER(BAProblemStruct)
+
 # name -> argtypes (restype is int unless listed in _RESTYPE)
 SIGNATURES = {
     "slam_abi_version": [],
@@ -26,8 +46,17 @@ SIGNATURES = {
     "slam_device_count": [],
     "slam_hamming_knn2": [c_p, c_p, c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p],
     "slam_compact_matches": [c_p, c_p, c_p, c_int, c_int, c_p, c_double, c_p, c_p, c_p],
+    "slam_ba_residual": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p],
+    "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
+    "slam_ba_red_slots": [c_int, c_int],
+    "slam_ba_sys_len": [c_int],
+    "slam_ba_build_system": [_PROB, c_p],
+    "slam_ba_solve_step": [_PROB, c_p],
+    "slam_ba_decide": [_PROB, c_p],
+    "slam_ba_iterate": [_PROB, c_int, c_p],
+    "slam_ba_reset": [_PROB, c_double, c_p],
 }
-_RESTYPE = {"slam_last_error": ctypes.c_char_p}
+_RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong}
 
 
 class SlamError(RuntimeError):

@@ -1,0 +1,231 @@
+"""GPU Levenberg-Marquardt bundle adjustment (BAL model) — host planner + driver.
+
+The planner turns a reference-style BA problem (BundleAdjustment.py:331:
+params = [cams (C x 9), points (P x 3)], cam_idxs, Q_idxs, qs) into the index
+tables the HIP kernels in csrc/ba.hip consume, allocates the device buffers
+(torch tensors as HBM containers) and runs LM iterations with all state on the
+device.  Multi-GPU: each rank builds a BAProblem over ALL cameras and the
+observations of its own points; `step_distributed` all-reduces the reduced
+camera system (one RCCL all-reduce of ~(9C)^2 doubles) and two scalars per
+iteration.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import ptr, require_gpu, stream_ptr
+
+from ._lib import BAProblemStruct as _Prob
+
+ST = dict(LAMBDA=0, NU=1, COST=2, COST_NEW=3, PRED=4, RHO=5, ACCEPTED=6, CUR=7, ITERS=8,
+          NACCEPT=9, PRED_CAM=10, CHOL_FAIL=11)
+N_STATE = 16
+LDS_MAX_N = 120  # k_solve keeps S in LDS up to 9C <= 120
+
+
+def _check_indices(n_cams, n_pts, cam_idx, pt_idx, qs):
+    cam_idx = np.asarray(cam_idx).astype(np.int64).ravel()
+    pt_idx = np.asarray(pt_idx).astype(np.int64).ravel()
+    qs = np.asarray(qs, np.float64).reshape(-1, 2)
+    if not (len(cam_idx) == len(pt_idx) == len(qs)):
+        raise ValueError("cam_idxs, Q_idxs and qs must have the same length")
+    if len(cam_idx) and (cam_idx.min() < 0 or cam_idx.max() >= n_cams):
+        raise ValueError("camera index out of range")
+    if len(pt_idx) and (pt_idx.min() < 0 or pt_idx.max() >= n_pts):
+        raise ValueError("point index out of range")
+    return cam_idx, pt_idx, qs
+
+
+# ----------------------------------------------------------------------------- planner
+def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
+    """Index tables for the LM kernels (host numpy, once per problem structure)."""
+    O = len(cam_idx)
+    order = np.lexsort((cam_idx, pt_idx))  # by point, then camera
+    obs_cam = cam_idx[order].astype(np.int32)
+    obs_pt = pt_idx[order].astype(np.int32)
+    pt_ptr = np.zeros(n_pts + 1, np.int64)
+    np.cumsum(np.bincount(obs_pt, minlength=n_pts), out=pt_ptr[1:])
+    cam_obs = np.argsort(obs_cam, kind="stable").astype(np.int32)
+    cam_cnt = np.bincount(obs_cam, minlength=n_cams)
+    if (cam_cnt == 0).any():
+        raise ValueError(f"cameras without observations: {np.nonzero(cam_cnt == 0)[0][:8]}")
+    cam_ptr = np.concatenate([[0], np.cumsum(cam_cnt)])
+    chunks, cptr = [], [0]
+    for c in range(n_cams):
+        for b in range(cam_ptr[c], cam_ptr[c + 1], cam_chunk):
+            chunks.append((c, b, min(b + cam_chunk, cam_ptr[c + 1])))
+        cptr.append(len(chunks))
+    cam_chunks = np.asarray(chunks, np.int32).reshape(-1, 3)
+
+    # Schur pairs: per point, ordered obs pairs (i, j) with cam_i <= cam_j
+    cnt = np.diff(pt_ptr)
+    o1s, o2s = [], []
+    for n in np.unique(cnt):
+        if n == 0:
+            continue
+        pts_n = np.nonzero(cnt == n)[0]
+        base = pt_ptr[pts_n][:, None, None]
+        ii, jj = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
+        a = (base + ii[None]).reshape(len(pts_n), -1)
+        b = (base + jj[None]).reshape(len(pts_n), -1)
+        keep = obs_cam[a] <= obs_cam[b]
+        o1s.append(a[keep])
+        o2s.append(b[keep])
+    o1 = np.concatenate(o1s) if o1s else np.zeros(0, np.int64)
+    o2 = np.concatenate(o2s) if o2s else np.zeros(0, np.int64)
+    bid = obs_cam[o1].astype(np.int64) * n_cams + obs_cam[o2]
+    so = np.lexsort((o1, bid))
+    o1, o2, bid = o1[so], o2[so], bid[so]
+    ub, bstart = np.unique(bid, return_index=True)
+    bend = np.append(bstart[1:], len(bid))
+    blocks = np.stack([ub // n_cams, ub % n_cams], 1).astype(np.int32)
+    pchunks, bptr = [], [0]
+    for k in range(len(ub)):
+        for b in range(bstart[k], bend[k], pair_chunk):
+            pchunks.append((k, b, min(b + pair_chunk, bend[k])))
+        bptr.append(len(pchunks))
+    return dict(
+        order=order, obs_cam=obs_cam, obs_pt=obs_pt, pt_ptr=pt_ptr.astype(np.int32),
+        cam_obs=cam_obs, cam_chunks=cam_chunks, cam_chunk_ptr=np.asarray(cptr, np.int32),
+        pair_o=np.stack([o1, o2], 1).astype(np.int32),
+        pair_chunks=np.asarray(pchunks, np.int32).reshape(-1, 3), blocks=blocks,
+        block_chunk_ptr=np.asarray(bptr, np.int32), n_obs=O)
+
+
+class BAProblem:
+    """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
+
+    def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, cam_chunk=512,
+                 pair_chunk=64, stream=None):
+        dev = require_gpu()
+        cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
+        pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+        C, P = len(cams), len(pts)
+        cam_idx, pt_idx, qs = _check_indices(C, P, cam_idx, pt_idx, qs)
+        pl = plan(C, P, cam_idx, pt_idx, cam_chunk, pair_chunk)
+        self.plan = pl
+        self.C, self.P, self.O = C, P, pl["n_obs"]
+        self.stream = stream
+        T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        z = lambda n: torch.zeros(max(int(n), 1), dtype=torch.float64, device=dev)  # noqa: E731
+        self.t = t = {}
+        t["cams0"], t["cams1"] = T(cams), T(cams.copy())
+        t["pts0"], t["pts1"] = T(pts), T(pts.copy())
+        for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
+                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr"):
+            arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
+            t[k] = T(arr.astype(np.int32))
+        t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
+        O, C9 = self.O, 9 * C
+        t["rec"] = z(O * 32)
+        t["wy"] = z(O * 54)
+        t["ptdata"] = z(P * 12)
+        t["cam_part"] = z(len(pl["cam_chunks"]) * 256)
+        t["pair_part"] = z(len(pl["pair_chunks"]) * 81)
+        self.sys_len = int(_lib.lib.slam_ba_sys_len(C))
+        t["sys"] = z(self.sys_len)
+        t["chol"] = z(C9 * C9 if C9 > LDS_MAX_N else 1)
+        t["delta_c"] = z(C9)
+        t["red_part"] = z(_lib.lib.slam_ba_red_slots(P, O))
+        t["small"] = z(4)
+        t["state"] = z(N_STATE)
+        s = _Prob()
+        s.n_cams, s.n_pts, s.n_obs = C, P, O
+        s.n_cam_chunks = len(pl["cam_chunks"])
+        s.n_blocks = len(pl["blocks"])
+        s.n_pair_chunks = len(pl["pair_chunks"])
+        s.n_pairs = len(pl["pair_o"])
+        s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
+        s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
+        for k in ("obs_cam", "obs_pt", "obs_q", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
+                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "rec", "wy", "ptdata",
+                  "cam_part", "pair_part", "sys", "chol", "delta_c", "red_part", "small", "state"):
+            setattr(s, k, t[k].data_ptr())
+        self._s = s
+        self.reset(lam0)
+
+    # -- primitive phases -------------------------------------------------------
+    def _sp(self):
+        return stream_ptr(self.stream)
+
+    def reset(self, lam0=1e-4):
+        _lib.call("slam_ba_reset", ctypes.byref(self._s), float(lam0), self._sp())
+
+    def build_system(self):
+        _lib.call("slam_ba_build_system", ctypes.byref(self._s), self._sp())
+
+    def solve_step(self):
+        _lib.call("slam_ba_solve_step", ctypes.byref(self._s), self._sp())
+
+    def decide(self):
+        _lib.call("slam_ba_decide", ctypes.byref(self._s), self._sp())
+
+    def iterate(self, n: int = 1):
+        """n LM iterations, no host synchronisation (single rank)."""
+        _lib.call("slam_ba_iterate", ctypes.byref(self._s), int(n), self._sp())
+
+    def step_distributed(self, group=None):
+        """One LM iteration with RCCL all-reduce of the camera system (multi-rank)."""
+        import torch.distributed as dist
+
+        self.build_system()
+        dist.all_reduce(self.t["sys"], group=group)
+        self.solve_step()
+        dist.all_reduce(self.t["small"], group=group)
+        self.decide()
+
+    # -- host views ---------------------------------------------------------------
+    def state(self) -> dict:
+        s = self.t["state"].cpu().numpy()
+        return {k: float(s[v]) for k, v in ST.items()}
+
+    def params(self):
+        cur = int(self.t["state"][ST["CUR"]].item() != 0)
+        return (self.t[f"cams{cur}"].cpu().numpy().copy(), self.t[f"pts{cur}"].cpu().numpy().copy())
+
+    def cost(self) -> float:
+        return self.state()["COST"]
+
+    def solve(self, max_iters=100, ftol=1e-10, check_every=5):
+        """Iterate until the relative cost decrease of an accepted step is < ftol
+        or max_iters.  Returns the final state dict."""
+        done = 0
+        last = None
+        while done < max_iters:
+            k = min(check_every, max_iters - done)
+            self.iterate(k)
+            done += k
+            st = self.state()
+            c = st["COST"]
+            if last is not None and abs(last - c) <= ftol * max(c, 1e-300) and st["LAMBDA"] < 1e8:
+                break
+            last = c
+        return self.state()
+
+
+# ----------------------------------------------------------------------------- kernels
+def residuals(cams, pts, cam_idx, pt_idx, qs, *, jacobian=False):
+    """objective()-order residuals [O,2] (and Jacobians [O,2,12]) on the GPU."""
+    dev = require_gpu()
+    cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
+    pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+    cam_idx, pt_idx, qs = _check_indices(len(cams), len(pts), cam_idx, pt_idx, qs)
+    O = len(cam_idx)
+    if O == 0:
+        return (np.zeros((0, 2)), np.zeros((0, 2, 12))) if jacobian else np.zeros((0, 2))
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    tc, tp = T(cams), T(pts)
+    ti, tj, tq = T(cam_idx.astype(np.int32)), T(pt_idx.astype(np.int32)), T(qs)
+    r = torch.empty((O, 2), dtype=torch.float64, device=dev)
+    if jacobian:
+        J = torch.empty((O, 2, 12), dtype=torch.float64, device=dev)
+        _lib.call("slam_ba_jacobian", ptr(tc), ptr(tp), ptr(ti), ptr(tj), ptr(tq), O, ptr(r),
+                  ptr(J), stream_ptr())
+        return r.cpu().numpy(), J.cpu().numpy()
+    _lib.call("slam_ba_residual", ptr(tc), ptr(tp), ptr(ti), ptr(tj), ptr(tq), O, ptr(r),
+              stream_ptr())
+    return r.cpu().numpy()

@@ -1,0 +1,207 @@
+"""Bundle adjustment: oracle pinning against the reference's BAL block (CPU)
+and GPU parity of the HIP LM solver.
+
+Reference: /root/reference/BundleAdjustment.py:287-402 (BAL block, pinned by
+tests/golden/ba_golden.npz made from the reference's own code).
+Tolerances (float64):
+  residual kernel vs reference objective: |d| <= 1e-9 * max(1, |r|)
+  Jacobian kernel vs oracle analytic J:   |d| <= 1e-8 * max(1, |J|)
+  LM iterates GPU vs oracle:              cost rel 1e-9, params rel 1e-6 (first 8 iters)
+  converged cost vs reference least_squares (tight tol): <= ref * (1 + 1e-6)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import ba as oba
+
+
+@pytest.fixture(scope="module")
+def g(golden_dir):
+    return np.load(os.path.join(golden_dir, "ba_golden.npz"))
+
+
+def make_problem(seed, C, P, obs_per_pt, noise=0.5, f=716.8):
+    """Local-BA-shaped synthetic problem (tracks over consecutive keyframes)."""
+    from slam355.synthetic import ba_problem
+
+    return ba_problem(np.random.default_rng(seed), C, P, obs_per_pt, f=f, noise=noise)
+
+
+# ----------------------------------------------------------------------------- CPU
+def test_oracle_objective_equals_reference(g):
+    params = np.hstack((g["res_cams"].ravel(), g["res_pts"].ravel()))
+    r = oba.objective(params, 6, 300, g["res_cam_idx"], g["res_pt_idx"], g["res_qs"])
+    assert np.array_equal(r, g["res_out"])  # bit-exact: same numpy expression order
+    assert np.array_equal(oba.rotate(g["rot_in_pts"], g["rot_in_vecs"]), g["rot_out"])
+
+
+def test_oracle_sparsity_equals_reference(g):
+    rows, cols, shape = oba.sparsity_coo(6, 300, g["res_cam_idx"], g["res_pt_idx"])
+    assert np.array_equal(rows, g["sp_rows"]) and np.array_equal(cols, g["sp_cols"])
+    assert tuple(shape) == tuple(g["sp_shape"])
+
+
+def test_oracle_jacobian_vs_finite_differences(g):
+    cams, pts = g["res_cams"].copy(), g["res_pts"].copy()
+    ci, pi, qs = g["res_cam_idx"], g["res_pt_idx"], g["res_qs"]
+    r, J = oba.residual_and_jacobian(cams, pts, ci, pi, qs)
+    assert np.allclose(r.ravel(), g["res_out"], rtol=0, atol=1e-9)
+    clamped = [3, 5, 8]
+    zero_rot = int(np.nonzero(ci == 0)[0][0])
+    for o in clamped + [zero_rot, 17, 100, 999]:
+        c, p = ci[o], pi[o]
+        for k in range(12):
+            cp, cm, pp, pm = cams.copy(), cams.copy(), pts.copy(), pts.copy()
+            if k < 9:
+                h = 1e-6 * max(1.0, abs(cams[c, k]))
+                cp[c, k] += h
+                cm[c, k] -= h
+            else:
+                h = 1e-6 * max(1.0, abs(pts[p, k - 9]))
+                pp[p, k - 9] += h
+                pm[p, k - 9] -= h
+            sl = slice(o, o + 1)
+            fd = (oba.residual_and_jacobian(cp, pp, ci[sl], pi[sl], qs[sl])[0] -
+                  oba.residual_and_jacobian(cm, pm, ci[sl], pi[sl], qs[sl])[0])[0] / (2 * h)
+            assert np.allclose(fd, J[o, :, k], rtol=1e-5, atol=1e-5 * max(1, np.abs(J[o]).max()))
+
+
+def test_oracle_lm_reaches_reference_optimum(g):
+    cams, pts, hist = oba.lm_solve(g["sol_cams0"], g["sol_pts0"], g["sol_cam_idx"],
+                                   g["sol_pt_idx"], g["sol_qs"], iters=40)
+    ref_tight = float(g["sol_tight_cost"])
+    ref_default = 0.5 * float(np.sum(g["sol_ref_rf"] ** 2))  # reference settings (ftol=0.1)
+    assert hist[-1]["cost"] <= ref_tight * (1 + 1e-6)
+    assert hist[-1]["cost"] <= ref_default
+
+
+def test_planner_pairs_cover_schur_structure():
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(1, 7, 200, 4)
+    # add a duplicate observation (camera sees a point twice) and an isolated obs
+    ci = np.append(ci, ci[0])
+    pi = np.append(pi, pi[0])
+    pl = ba.plan(7, 200, ci, pi, cam_chunk=16, pair_chunk=8)
+    # every point with n obs contributes sum over ordered pairs with cam_i <= cam_j
+    o1, o2 = pl["pair_o"][:, 0], pl["pair_o"][:, 1]
+    assert (pl["obs_pt"][o1] == pl["obs_pt"][o2]).all()
+    assert (pl["obs_cam"][o1] <= pl["obs_cam"][o2]).all()
+    exp = 0
+    for p in range(200):
+        cs = pl["obs_cam"][pl["pt_ptr"][p]:pl["pt_ptr"][p + 1]]
+        exp += int((cs[:, None] <= cs[None, :]).sum())
+    assert len(o1) == exp
+    # chunks tile each camera's observation list and each block's pair list
+    cc = pl["cam_chunks"]
+    assert cc[0, 1] == 0 and cc[-1, 2] == len(ci) and (cc[1:, 1] == cc[:-1, 2]).all()
+    assert ((cc[:, 2] - cc[:, 1]) <= 16).all()
+    pc = pl["pair_chunks"]
+    assert pc[0, 1] == 0 and pc[-1, 2] == len(o1) and (pc[1:, 1] == pc[:-1, 2]).all()
+
+
+def test_bal_file_roundtrip(tmp_path):
+    from slam355 import BundleAdjustment as B
+
+    cams, pts, ci, pi, qs = make_problem(2, 4, 30, 3)
+    fn = str(tmp_path / "p.txt")
+    B.write_bal_data(fn, cams, pts, ci, pi, qs)
+    c2, p2, ci2, pi2, q2 = B.read_bal_data(fn)
+    assert np.array_equal(c2, cams) and np.array_equal(p2, pts)
+    assert np.array_equal(ci2, ci) and np.array_equal(pi2, pi) and np.array_equal(q2, qs)
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+def test_gpu_residual_matches_reference_objective(g):
+    from slam355 import BundleAdjustment as B
+
+    params = np.hstack((g["res_cams"].ravel(), g["res_pts"].ravel()))
+    r = B.objective(params, 6, 300, g["res_cam_idx"], g["res_pt_idx"], g["res_qs"])
+    ref = g["res_out"]
+    assert np.all(np.abs(r - ref) <= 1e-9 * np.maximum(1.0, np.abs(ref)))
+
+
+@pytest.mark.gpu
+def test_gpu_jacobian_matches_oracle(g):
+    from slam355 import ba
+
+    cams, pts = g["res_cams"], g["res_pts"]
+    ci, pi, qs = g["res_cam_idx"], g["res_pt_idx"], g["res_qs"]
+    r, J = ba.residuals(cams, pts, ci, pi, qs, jacobian=True)
+    er, eJ = oba.residual_and_jacobian(cams, pts, ci, pi, qs)
+    assert np.all(np.abs(r - er) <= 1e-9 * np.maximum(1.0, np.abs(er)))
+    assert np.all(np.abs(J - eJ) <= 1e-8 * np.maximum(1.0, np.abs(eJ)))
+
+
+@pytest.mark.gpu
+def test_gpu_lm_iterates_match_oracle():
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(3, 6, 150, 4)
+    rng = np.random.default_rng(4)
+    cams0 = cams.copy()
+    cams0[:, :3] += rng.normal(0, 1e-3, (6, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (6, 3))
+    pts0 = pts + rng.normal(0, 0.05, pts.shape)
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
+    st = oba.LMState(1e-4)
+    oc, op = cams0.copy(), pts0.copy()
+    for it in range(8):
+        prob.iterate(1)
+        oc, op, info = oba.lm_iteration(oc, op, ci, pi, qs, st)
+        s = prob.state()
+        assert bool(s["ACCEPTED"]) == bool(info["accepted"]), it
+        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-9 * info["cost_new"] + 1e-12, it
+        assert abs(s["LAMBDA"] - st.lam) <= 1e-6 * st.lam, it
+        gc, gp = prob.params()
+        assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9), it
+        assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), it
+
+
+@pytest.mark.gpu
+def test_gpu_solver_reaches_reference_optimum(g):
+    from slam355 import BundleAdjustment as B
+
+    A = B.bundle_adjustment_sparsity(5, 120, g["sol_cam_idx"], g["sol_pt_idx"])
+    r0, rf, x = B.bundle_adjustment_with_sparsity(g["sol_cams0"], g["sol_pts0"], g["sol_cam_idx"],
+                                                  g["sol_pt_idx"], g["sol_qs"], A)
+    assert np.allclose(r0, g["sol_ref_r0"], rtol=1e-9, atol=1e-9)
+    cost = 0.5 * float(np.sum(rf ** 2))
+    assert cost <= float(g["sol_tight_cost"]) * (1 + 1e-6)
+    # same optimum as the oracle LM (gauge fixed identically: same start, same algorithm)
+    oc, op, hist = oba.lm_solve(g["sol_cams0"], g["sol_pts0"], g["sol_cam_idx"], g["sol_pt_idx"],
+                                g["sol_qs"], iters=60)
+    assert abs(cost - hist[-1]["cost"]) <= 1e-6 * cost
+    cams = x[:45].reshape(5, 9)
+    A_ = np.vstack([oba.camera_centers(cams), x[45:].reshape(-1, 3)])
+    B_ = np.vstack([oba.camera_centers(oc), op])
+    s, R, t = oba.sim3_align(A_, B_)
+    err = np.abs((s * (R @ A_.T)).T + t - B_).max() / np.abs(B_).max()
+    assert err < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,P,k", [(10, 5000, 6), (16, 3000, 5)])
+def test_gpu_local_ba_config3_converges(C, P, k):
+    """C3 shape (10 KF x 5k pts x 30k obs) and a 9C > 120 case (global-memory Cholesky)."""
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(5 + C, C, P, k)
+    rng = np.random.default_rng(6)
+    cams0 = cams.copy()
+    cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
+    pts0 = pts + rng.normal(0, 0.05, pts.shape)
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
+    c0 = 0.5 * float(np.sum(oba.residual_and_jacobian(cams0, pts0, ci, pi, qs)[0] ** 2))
+    st = prob.solve(max_iters=60, ftol=1e-12)
+    # converged to the noise floor: 0.5 * sum r^2 ~ 0.5 * (2O - dof) * sigma^2
+    O = len(ci)
+    assert st["COST"] < 0.5 * 2 * O * 0.25 * 1.1
+    assert st["COST"] < 1e-2 * c0
+    gc, gp = prob.params()
+    r = oba.residual_and_jacobian(gc, gp, ci, pi, qs)[0]
+    assert abs(0.5 * float(np.sum(r * r)) - st["COST"]) <= 1e-8 * st["COST"]
