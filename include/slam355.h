@@ -84,6 +84,33 @@ int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,
 
 
 /* ------------------------------------------------------------------------
+ * Tiled ORB detector + rBRIEF descriptor.
+ *
+ * Replaces orb_detector_using_tiles (/root/reference/orb.py:4-25), i.e. the
+ * per-patch cv2.ORB_create(nfeatures=max_kp, scaleFactor=1.2).detect() +
+ * .compute() of orb_extraction_detect (orb.py:28-38), with the OpenCV 4.x ORB
+ * semantics restated in oracle/orb.c (bit-exact against it; canonical keypoint
+ * order: level, Harris response desc, y, x).  Tiles follow orb.py exactly:
+ * tile_h = int(H/height_div), tile_w = int(W/width_div), patches of
+ * int(tile + tile/overlap_div) starting at every multiple of the tile size
+ * below H - tile_h (resp. W - tile_w), clipped to the image.
+ * height_div == width_div == 0 runs ORB on the whole image as one patch
+ * (orb_extraction_detect itself); patches must fit the 160 KiB LDS budget.
+ *
+ *   d_img   [batch][H][stride] u8
+ *   d_kp    [batch][kp_cap][5] f32  (x, y, size, angle [deg], response)
+ *   d_octave[batch][kp_cap] i32, d_desc [batch][kp_cap][32] u8
+ *   d_count [batch] i32: number of keypoints, or -(n)-1 on overflow
+ *   d_ws    workspace of slam_orb_workspace_bytes(...) bytes
+ * ---------------------------------------------------------------------- */
+int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int overlap_div,
+                             int height_div, int width_div, size_t* bytes);
+int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int stride, int max_kp,
+                   int overlap_div, int height_div, int width_div, void* d_ws,
+                   size_t ws_bytes, float* d_kp, int32_t* d_octave, uint8_t* d_desc,
+                   int32_t* d_count, int kp_cap, void* stream);
+
+/* ------------------------------------------------------------------------
  * Bundle adjustment (BAL model) — replaces the reference's BAL block
  * /root/reference/BundleAdjustment.py:287-402 (rotate / project / objective /
  * bundle_adjustment_sparsity / least_squares TRF) with Levenberg-Marquardt on

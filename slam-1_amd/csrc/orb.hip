@@ -1,0 +1,691 @@
+// Tiled ORB (FAST-9 + Harris + IC angle + rBRIEF) for gfx950.
+//
+// Replaces /root/reference/orb.py:4-38: orb_detector_using_tiles cuts the image
+// into overlapping patches and runs cv2.ORB_create(n, scaleFactor=1.2)
+// .detect()/.compute() on each.  The semantics restated in oracle/orb.c (OpenCV
+// 4.x ORB, canonical keypoint order) are reproduced bit for bit.
+//
+// Design: one workgroup per (image, patch).  The patch never leaves LDS: the
+// pyramid is built level by level in two ping-pong LDS buffers with the
+// 8-bit fixed-point INTER_LINEAR_EXACT resize, and each level runs the whole
+// chain before the next is built:
+//   FAST-9 score map (bit-mask arc test, cornerScore<16>) over the NMS region
+//   -> strict 3x3 NMS + border filter -> LDS atomic candidate list + score
+//   histogram -> retainBest(2n) threshold from a wave suffix scan -> Harris on
+//   the survivors -> exact rank (response desc, y, x) -> retainBest(n) with
+//   ties -> IC angle (one wave per keypoint, integer moments) -> 7x7 Gaussian
+//   of the sampled region (sliding-window separable float FMA chains) ->
+//   rBRIEF (32 lanes per keypoint, one descriptor byte per lane).
+// HBM traffic per patch = its bytes read once + ~56 B per keypoint written.
+#include "common.hpp"
+
+#include <cmath>
+#include <cstring>
+
+namespace {
+
+#include "orb_pattern.inc"
+
+constexpr int kNLev = 8;
+constexpr int kEdge = 31;
+constexpr int kFastT = 20;
+constexpr int kOrbWG = 512;
+constexpr int kMaxTiles = 256;
+constexpr int kMaxShapes = 4;
+constexpr int kNMS0 = 29;  // score-map region starts here (needs [30, w-31])
+constexpr int kBl0 = 9;    // blurred region starts here (samples within +-19 of [31, w-32])
+
+__constant__ int8_t c_pattern[256 * 4];
+__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
+
+struct OrbGeom {
+  int H, W, stride;
+  int n_tiles, ntx, tile_h, tile_w;
+  int tcap;       // keypoint slots per tile in the workspace
+  int cand_cap;   // NMS survivors per level (LDS)
+  int list_cap;   // kept keypoints per level (LDS)
+  int lds_a, lds_b, lds_u, lds_l, lds_m;  // byte offsets of the LDS regions
+  int lds_total;
+  float ls[kNLev];  // (float)pow(1.2, l)
+  int nl[kNLev];    // per-level budget
+  float gk[7];      // Gaussian 7-tap, sigma 2 (float)
+  int nshapes;
+  int sw[kMaxShapes], sh[kMaxShapes];
+  int lw[kMaxShapes][kNLev], lh[kMaxShapes][kNLev];
+  int nlev[kMaxShapes];  // levels to run for this shape (0..nlev-1)
+  uint8_t tile_shape[kMaxTiles];
+};
+
+__device__ __forceinline__ int rne_f(float v) { return (int)rintf(v); }
+
+// ------------------------------------------------------------------ FAST
+__device__ __forceinline__ int fast_score(const uint8_t* im, int st, int x, int y) {
+  const uint8_t* c = im + y * st + x;
+  const int v = c[0];
+  int d[16];
+  d[0] = v - c[3 * st];
+  d[1] = v - c[3 * st + 1];
+  d[2] = v - c[2 * st + 2];
+  d[3] = v - c[st + 3];
+  d[4] = v - c[3];
+  d[5] = v - c[-st + 3];
+  d[6] = v - c[-2 * st + 2];
+  d[7] = v - c[-3 * st + 1];
+  d[8] = v - c[-3 * st];
+  d[9] = v - c[-3 * st - 1];
+  d[10] = v - c[-2 * st - 2];
+  d[11] = v - c[-st - 3];
+  d[12] = v - c[-3];
+  d[13] = v - c[st - 3];
+  d[14] = v - c[2 * st - 2];
+  d[15] = v - c[3 * st - 1];
+  unsigned dark = 0, bright = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    dark |= (d[k] > kFastT ? 1u : 0u) << k;     // p < v - t
+    bright |= (d[k] < -kFastT ? 1u : 0u) << k;  // p > v + t
+  }
+  auto run9 = [](unsigned m) {
+    unsigned mm = m | (m << 16), r = mm;
+#pragma unroll
+    for (int i = 1; i <= 8; ++i) r &= mm >> i;
+    return (r & 0xFFFFu) != 0u;
+  };
+  if (!run9(dark) && !run9(bright)) return 0;
+  // OpenCV cornerScore<16>
+  int a0 = kFastT;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = d[(k + 1) & 15];
+#pragma unroll
+    for (int j = 2; j <= 8; ++j) a = min(a, d[(k + j) & 15]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[(k + 9) & 15]));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = d[(k + 1) & 15];
+#pragma unroll
+    for (int j = 2; j <= 8; ++j) b = max(b, d[(k + j) & 15]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[(k + 9) & 15]));
+  }
+  return -b0 - 1;
+}
+
+__device__ __forceinline__ float harris(const uint8_t* im, int st, int x0, int y0) {
+  int a = 0, b = 0, c = 0;
+  for (int i = 0; i < 7; ++i) {
+    const uint8_t* row = im + (y0 - 3 + i) * st + (x0 - 3);
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const uint8_t* p = row + j;
+      const int Ix = (p[1] - p[-1]) * 2 + (p[-st + 1] - p[-st - 1]) + (p[st + 1] - p[st - 1]);
+      const int Iy = (p[st] - p[-st]) * 2 + (p[st - 1] - p[-st - 1]) + (p[st + 1] - p[-st + 1]);
+      a += Ix * Ix;
+      b += Iy * Iy;
+      c += Ix * Iy;
+    }
+  }
+  const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+  const float ssss = scale * scale * scale * scale;
+  const float k = 0.04f;
+  return ((float)a * b - (float)c * c - k * ((float)a + b) * ((float)a + b)) * ssss;
+}
+
+__device__ __forceinline__ float fast_atan2_deg(float y, float x) {
+  const float r2d = (float)(180 / 3.14159265358979323846);
+  const float p1 = 0.9997878412794807f * r2d, p3 = -0.3258083974640975f * r2d;
+  const float p5 = 0.1555786518463281f * r2d, p7 = -0.04432655554792128f * r2d;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// INTER_LINEAR_EXACT coefficient of destination index d: (ofs << 9) | c1.
+__device__ __forceinline__ int lin_coeff(int d, int dsize, int ssize) {
+  const double inv = (double)dsize / ssize;
+  const double scale = 1.0 / inv;
+  const double fval = scale * ((double)d + 0.5) - 0.5;
+  const int ival = (int)floor(fval);
+  if (ival >= 0 && ssize > 1) {
+    if (ival < ssize - 1) return (ival << 9) | (int)rint((fval - (double)ival) * 256.0);
+    return (ssize - 1) << 9;  // replicate the last source sample
+  }
+  return 0;  // replicate the first
+}
+
+struct KP {  // one kept keypoint of the current level (LDS)
+  int x, y;
+  float resp, angle;
+};
+
+__global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
+                                                     float* __restrict__ ws_kp,
+                                                     int32_t* __restrict__ ws_oct,
+                                                     uint8_t* __restrict__ ws_desc,
+                                                     int32_t* __restrict__ ws_cnt) {
+  // All LDS is one dynamic region with a 16-byte aligned base (Guideline 17).
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  int* hist = reinterpret_cast<int*>(lds + g.lds_m);  // 256 bins of FAST score
+  int* ctr = hist + 256;   // 0: candidates, 1: survivors, 2: threshold, 3: kept
+  int* tabx = ctr + 16;    // resize coefficients (<= 1024 each)
+  int* taby = tabx + 1024;
+
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int ty = tile / g.ntx, tx = tile - ty * g.ntx;
+  const int x0 = tx * g.tile_w, y0 = ty * g.tile_h;
+  const int shp = g.tile_shape[tile];
+  const int pw = g.sw[shp], ph = g.sh[shp];
+  uint8_t* bufs[2] = {lds + g.lds_a, lds + g.lds_b};
+  uint8_t* U = lds + g.lds_u;
+  KP* L = reinterpret_cast<KP*>(lds + g.lds_l);
+  const size_t slot = (size_t)b * g.n_tiles + tile;
+  float* okp = ws_kp + slot * g.tcap * 5;
+  int32_t* ooct = ws_oct + slot * g.tcap;
+  uint8_t* odesc = ws_desc + slot * g.tcap * 32;
+
+  // ---- stage the patch (level 0) into LDS, 16 B per lane where aligned
+  {
+    const uint8_t* src = img + (size_t)b * g.H * g.stride + (size_t)y0 * g.stride + x0;
+    uint8_t* dst = bufs[0];
+    if ((pw & 15) == 0 && (((uintptr_t)src) & 15) == 0 && (g.stride & 15) == 0) {
+      const int vpr = pw >> 4;
+      for (int i = t; i < vpr * ph; i += kOrbWG) {
+        const int r = i / vpr, c = i - r * vpr;
+        *reinterpret_cast<uint4*>(dst + r * pw + 16 * c) =
+            *reinterpret_cast<const uint4*>(src + (size_t)r * g.stride + 16 * c);
+      }
+    } else {
+      for (int i = t; i < pw * ph; i += kOrbWG) {
+        const int r = i / pw, c = i - r * pw;
+        dst[i] = src[(size_t)r * g.stride + c];
+      }
+    }
+  }
+  __syncthreads();
+
+  int nout = 0;      // keypoints written for this tile (uniform)
+  int overflow = 0;  // uniform
+  const int nlev = g.nlev[shp];
+  for (int l = 0; l < nlev; ++l) {
+    const int W = g.lw[shp][l], H = g.lh[shp][l];
+    uint8_t* I = bufs[l & 1];
+    if (l > 0) {
+      // ---- resize level l-1 -> l (INTER_LINEAR_EXACT)
+      const int SW = g.lw[shp][l - 1], SH = g.lh[shp][l - 1];
+      const uint8_t* S = bufs[(l - 1) & 1];
+      for (int i = t; i < W; i += kOrbWG) tabx[i] = lin_coeff(i, W, SW);
+      for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
+      __syncthreads();
+      for (int i = t; i < W * H; i += kOrbWG) {
+        const int y = i / W, x = i - y * W;
+        const int cx = tabx[x], cy = taby[y];
+        const int xo = cx >> 9, c1 = cx & 511, c0 = 256 - c1;
+        const int yo = cy >> 9, d1 = cy & 511, d0 = 256 - d1;
+        const uint8_t* r0 = S + yo * SW + xo;
+        int h0 = c0 * r0[0] + (c1 ? c1 * r0[1] : 0);
+        int v = d0 * h0;
+        if (d1) {
+          const uint8_t* r1 = r0 + SW;
+          const int h1 = c0 * r1[0] + (c1 ? c1 * r1[1] : 0);
+          v += d1 * h1;
+        }
+        I[i] = (uint8_t)min((v + 32768) >> 16, 255);
+      }
+      __syncthreads();
+    }
+    const int n_l = g.nl[l];
+    if (W <= 2 * kEdge || H <= 2 * kEdge || n_l == 0) continue;  // uniform
+
+    // ---- FAST score map over [29, W-30] x [29, H-30]
+    const int SWd = W - 2 * kNMS0, SHd = H - 2 * kNMS0;
+    uint8_t* Smap = U;
+    uint32_t* cand = reinterpret_cast<uint32_t*>(U + ((SWd * SHd + 15) & ~15));
+    float* cresp = reinterpret_cast<float*>(cand + g.cand_cap);
+    for (int i = t; i < SWd * SHd; i += kOrbWG) {
+      const int y = i / SWd, x = i - y * SWd;
+      Smap[i] = (uint8_t)fast_score(I, W, x + kNMS0, y + kNMS0);
+    }
+    for (int i = t; i < 256; i += kOrbWG) hist[i] = 0;
+    if (t < 8) ctr[t] = 0;
+    __syncthreads();
+    // ---- strict 3x3 NMS + border [31, W-32] -> candidates
+    {
+      const int CW = W - 2 * kEdge, CH = H - 2 * kEdge;
+      for (int i = t; i < CW * CH; i += kOrbWG) {
+        const int yy = i / CW, xx = i - yy * CW;
+        const int x = xx + kEdge, y = yy + kEdge;
+        const uint8_t* sp = Smap + (y - kNMS0) * SWd + (x - kNMS0);
+        const int s = sp[0];
+        if (s == 0) continue;
+        if (s > sp[-1] && s > sp[1] && s > sp[-SWd - 1] && s > sp[-SWd] && s > sp[-SWd + 1] &&
+            s > sp[SWd - 1] && s > sp[SWd] && s > sp[SWd + 1]) {
+          const int k = atomicAdd(&ctr[0], 1);
+          if (k < g.cand_cap) cand[k] = ((uint32_t)s << 20) | ((uint32_t)y << 10) | (uint32_t)x;
+          atomicAdd(&hist[s], 1);
+        }
+      }
+    }
+    __syncthreads();
+    const int ncand = ctr[0];
+    if (ncand > g.cand_cap) {  // cannot happen for strict maxima (density <= 1/4); guard anyway
+      overflow = 1;
+      break;
+    }
+    // ---- retainBest(2 n_l) threshold by FAST score (ties kept)
+    if (wid == 0) {
+      int T = 0;
+      const int K = 2 * n_l;
+      if (ncand > K) {
+        const int c0 = hist[4 * lane], c1 = hist[4 * lane + 1];
+        const int c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
+        const int s = c0 + c1 + c2 + c3;
+        int suf = s;  // inclusive suffix sum over lanes
+        for (int off = 1; off < 64; off <<= 1) {
+          const int o = __shfl_down(suf, off, 64);
+          if (lane + off < 64) suf += o;
+        }
+        int acc = suf - s;  // scores in bins >= 4*lane+4
+        int tl = -1;
+        acc += c3;
+        if (acc >= K) tl = 4 * lane + 3;
+        else {
+          acc += c2;
+          if (acc >= K) tl = 4 * lane + 2;
+          else {
+            acc += c1;
+            if (acc >= K) tl = 4 * lane + 1;
+            else {
+              acc += c0;
+              if (acc >= K) tl = 4 * lane;
+            }
+          }
+        }
+        for (int off = 32; off > 0; off >>= 1) tl = max(tl, __shfl_xor(tl, off, 64));
+        T = tl;
+      }
+      if (lane == 0) ctr[2] = T;
+    }
+    __syncthreads();
+    // ---- survivors of retainBest(2n) -> front of cand (via cresp as scratch)
+    {
+      const int T = ctr[2];
+      for (int i = t; i < ncand; i += kOrbWG) {
+        const uint32_t c = cand[i];
+        if ((int)(c >> 20) >= T) {
+          const int k = atomicAdd(&ctr[1], 1);
+          reinterpret_cast<uint32_t*>(cresp)[k] = c;
+        }
+      }
+    }
+    __syncthreads();
+    const int nk = ctr[1];
+    for (int i = t; i < nk; i += kOrbWG) cand[i] = reinterpret_cast<uint32_t*>(cresp)[i];
+    __syncthreads();
+    for (int i = t; i < nk; i += kOrbWG) {
+      const uint32_t c = cand[i];
+      cresp[i] = harris(I, W, (int)(c & 1023u), (int)((c >> 10) & 1023u));
+    }
+    __syncthreads();
+    // ---- exact rank by (response desc, y asc, x asc); L[rank] holds the sorted list
+    for (int i = t; i < nk; i += kOrbWG) {
+      const float ri = cresp[i];
+      const uint32_t ci = cand[i];
+      const uint32_t yxi = ci & 0xFFFFFu;  // (y << 10) | x: y-major order
+      int rank = 0;
+      for (int j = 0; j < nk; ++j) {
+        const float rj = cresp[j];
+        const uint32_t yxj = cand[j] & 0xFFFFFu;
+        rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
+      }
+      if (rank < g.list_cap) {
+        L[rank].x = (int)(ci & 1023u);
+        L[rank].y = (int)((ci >> 10) & 1023u);
+        L[rank].resp = ri;
+      }
+    }
+    __syncthreads();
+    // retainBest(n_l): everything at least as good as the n_l-th response (ties kept)
+    if (t == 0) {
+      int m = nk;
+      int ovf = 0;
+      if (nk > n_l) {
+        const float rs = L[n_l - 1].resp;
+        m = n_l;
+        while (m < nk && m < g.list_cap && L[m].resp == rs) ++m;
+        if (m == g.list_cap && m < nk) ovf = 1;
+      } else if (nk > g.list_cap) {
+        ovf = 1;
+      }
+      ctr[3] = ovf ? -1 : m;
+    }
+    __syncthreads();
+    const int m = ctr[3];
+    if (m < 0 || nout + m > g.tcap) {
+      overflow = 1;
+      break;
+    }
+    // ---- IC angle: one wave per keypoint, lanes 0..30 <-> u = -15..15
+    for (int k = wid; k < m; k += kOrbWG / 64) {
+      const int cx = L[k].x, cy = L[k].y;
+      int m10 = 0, m01 = 0;
+      const int u = lane - 15;
+      if (lane < 31) {
+        const int au = u < 0 ? -u : u;
+        for (int v = -15; v <= 15; ++v) {
+          const int av = v < 0 ? -v : v;
+          if (au <= c_umax[av]) {
+            const int val = I[(cy + v) * W + cx + u];
+            m10 += u * val;
+            m01 += v * val;
+          }
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        m10 += __shfl_xor(m10, off, 64);
+        m01 += __shfl_xor(m01, off, 64);
+      }
+      if (lane == 0) L[k].angle = fast_atan2_deg((float)m01, (float)m10);
+    }
+    // ---- 7x7 Gaussian (float path) over [9, W-10] x [9, H-10] into U
+    const int BW = W - 2 * kBl0, BH = H - 2 * kBl0;
+    uint8_t* Bl = U;
+    __syncthreads();  // Smap/cand/cresp dead from here (L holds the level)
+    {
+      const float k0 = g.gk[0], k1 = g.gk[1], k2 = g.gk[2], k3 = g.gk[3];
+      const float k4 = g.gk[4], k5 = g.gk[5], k6 = g.gk[6];
+      const int nseg = (kOrbWG + BW - 1) / BW;
+      const int seg = (BH + nseg - 1) / nseg;
+      for (int item = t; item < BW * nseg; item += kOrbWG) {
+        const int s = item / BW, c = item - s * BW;
+        const int r0 = s * seg, r1 = min(BH, r0 + seg);
+        if (r0 >= r1) continue;
+        const int x = c + kBl0;
+        auto rowf = [&](int y) {
+          const uint8_t* p = I + y * W + x - 3;
+          float acc = 0.f;
+          acc = fmaf((float)p[0], k0, acc);
+          acc = fmaf((float)p[1], k1, acc);
+          acc = fmaf((float)p[2], k2, acc);
+          acc = fmaf((float)p[3], k3, acc);
+          acc = fmaf((float)p[4], k4, acc);
+          acc = fmaf((float)p[5], k5, acc);
+          acc = fmaf((float)p[6], k6, acc);
+          return acc;
+        };
+        const int yb = r0 + kBl0;  // first output row (image coords)
+        float w0 = rowf(yb - 3), w1 = rowf(yb - 2), w2 = rowf(yb - 1), w3 = rowf(yb);
+        float w4 = rowf(yb + 1), w5 = rowf(yb + 2), w6 = rowf(yb + 3);
+        for (int r = r0; r < r1; ++r) {
+          float s0 = w3 * k3;
+          s0 = fmaf(w4 + w2, k4, s0);
+          s0 = fmaf(w5 + w1, k5, s0);
+          s0 = fmaf(w6 + w0, k6, s0);
+          const int v = (int)rintf(s0);
+          Bl[r * BW + c] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+          if (r + 1 < r1) {
+            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
+            w6 = rowf(r + 1 + kBl0 + 3);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ---- rBRIEF: 32 lanes per keypoint, one byte per lane; write the keypoint
+    {
+      const float ls = g.ls[l];
+      const int half = lane >> 5, byte = lane & 31;
+      for (int k = 2 * wid + half; k < m; k += 2 * (kOrbWG / 64)) {
+        const KP kp = L[k];
+        const float xl = (float)kp.x * ls, yl = (float)kp.y * ls;  // pt *= layerScale
+        const float inv = 1.f / ls;
+        const int cx = rne_f(xl * inv) - kBl0, cy = rne_f(yl * inv) - kBl0;
+        float ang = kp.angle;
+        ang *= (float)(3.14159265358979323846 / 180.f);
+        const float a = (float)cos((double)ang), bb = (float)sin((double)ang);
+        int val = 0;
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+          const int8_t* pp = c_pattern + (byte * 8 + bit) * 4;
+          const float px1 = (float)pp[0], py1 = (float)pp[1];
+          const float px2 = (float)pp[2], py2 = (float)pp[3];
+          const int ix1 = rne_f(px1 * a - py1 * bb), iy1 = rne_f(px1 * bb + py1 * a);
+          const int ix2 = rne_f(px2 * a - py2 * bb), iy2 = rne_f(px2 * bb + py2 * a);
+          const int t0 = Bl[(cy + iy1) * BW + cx + ix1];
+          const int t1 = Bl[(cy + iy2) * BW + cx + ix2];
+          val |= (t0 < t1 ? 1 : 0) << bit;
+        }
+        const int o = nout + k;
+        odesc[(size_t)o * 32 + byte] = (uint8_t)val;
+        if (byte == 0) {
+          okp[(size_t)o * 5 + 0] = (float)((double)xl + (double)x0);
+          okp[(size_t)o * 5 + 1] = (float)((double)yl + (double)y0);
+          okp[(size_t)o * 5 + 2] = 31.f * ls;
+          okp[(size_t)o * 5 + 3] = kp.angle;
+          okp[(size_t)o * 5 + 4] = kp.resp;
+          ooct[o] = l;
+        }
+      }
+    }
+    nout += m;
+    __syncthreads();
+  }
+  if (t == 0) ws_cnt[slot] = overflow ? -1 : nout;
+}
+
+// Concatenate the tiles of each image in orb.py order.
+__global__ __launch_bounds__(256) void k_orb_compact(const float* __restrict__ ws_kp,
+                                                     const int32_t* __restrict__ ws_oct,
+                                                     const uint8_t* __restrict__ ws_desc,
+                                                     const int32_t* __restrict__ ws_cnt,
+                                                     int n_tiles, int tcap, float* __restrict__ kp,
+                                                     int32_t* __restrict__ oct,
+                                                     uint8_t* __restrict__ desc,
+                                                     int32_t* __restrict__ count, int kp_cap) {
+  __shared__ int off[kMaxTiles + 1];
+  __shared__ int bad;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int s = 0, ovf = 0;
+    for (int i = 0; i < n_tiles; ++i) {
+      off[i] = s;
+      const int c = ws_cnt[(size_t)b * n_tiles + i];
+      if (c < 0) ovf = 1;
+      s += c < 0 ? 0 : c;
+    }
+    off[n_tiles] = s;
+    bad = ovf || s > kp_cap;
+    count[b] = bad ? -s - 1 : s;
+  }
+  __syncthreads();
+  if (bad) return;
+  for (int i = 0; i < n_tiles; ++i) {
+    const int n = off[i + 1] - off[i];
+    const size_t src = ((size_t)b * n_tiles + i) * tcap;
+    const size_t dst = (size_t)b * kp_cap + off[i];
+    for (int j = threadIdx.x; j < n * 5; j += 256) kp[dst * 5 + j] = ws_kp[src * 5 + j];
+    for (int j = threadIdx.x; j < n; j += 256) oct[dst + j] = ws_oct[src + j];
+    for (int j = threadIdx.x; j < n * 8; j += 256)
+      reinterpret_cast<uint32_t*>(desc)[dst * 8 + j] =
+          reinterpret_cast<const uint32_t*>(ws_desc)[src * 8 + j];
+  }
+}
+
+// ---------------------------------------------------------------- host side
+int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height_div,
+               int width_div, OrbGeom* g) {
+  SLAM_REQUIRE(H > 0 && W > 0 && stride >= W, "slam_orb: bad image shape");
+  SLAM_REQUIRE((overlap_div > 0 && height_div > 0 && width_div > 0) ||
+                   (height_div == 0 && width_div == 0),
+               "slam_orb: bad tiling");
+  SLAM_REQUIRE(max_kp >= 0, "slam_orb: max_kp < 0");
+  memset(g, 0, sizeof(*g));
+  g->H = H;
+  g->W = W;
+  g->stride = stride;
+  // orb.py:13-20 (Python int() truncation of positive floats)
+  int nty = 0, ntx = 0, ph, pw;
+  if (height_div == 0 && width_div == 0) {
+    // whole image as one patch: orb_extraction_detect (orb.py:28-38)
+    g->tile_h = H;
+    g->tile_w = W;
+    ph = H;
+    pw = W;
+    nty = ntx = 1;
+  } else {
+    g->tile_h = (int)((double)H / height_div);
+    g->tile_w = (int)((double)W / width_div);
+    SLAM_REQUIRE(g->tile_h > 0 && g->tile_w > 0, "slam_orb: image smaller than the tile grid");
+    ph = (int)(g->tile_h + (double)g->tile_h / overlap_div);
+    pw = (int)(g->tile_w + (double)g->tile_w / overlap_div);
+    for (int y = 0; y < H - g->tile_h; y += g->tile_h) ++nty;
+    for (int x = 0; x < W - g->tile_w; x += g->tile_w) ++ntx;
+  }
+  g->ntx = ntx;
+  g->n_tiles = nty * ntx;
+  SLAM_REQUIRE(g->n_tiles <= kMaxTiles, "slam_orb: %d tiles > %d", g->n_tiles, kMaxTiles);
+  // levels: budget (float arithmetic of ORB_Impl) and scales
+  const float factor = (float)(1.0 / 1.2);
+  float d = (float)max_kp * (1 - factor) / (1 - (float)pow((double)factor, (double)kNLev));
+  int sum = 0;
+  for (int l = 0; l < kNLev - 1; ++l) {
+    g->nl[l] = (int)nearbyintf(d);
+    sum += g->nl[l];
+    d *= factor;
+  }
+  g->nl[kNLev - 1] = max_kp - sum > 0 ? max_kp - sum : 0;
+  for (int l = 0; l < kNLev; ++l) g->ls[l] = (float)pow(1.2, (double)l);
+  {
+    double t[7], s = 0;
+    for (int i = 0; i < 7; ++i) {
+      const double x = i - 3.0;
+      t[i] = exp(-0.5 / (2.0 * 2.0) * x * x);
+      g->gk[i] = (float)t[i];
+      s += g->gk[i];
+    }
+    s = 1.0 / s;
+    for (int i = 0; i < 7; ++i) g->gk[i] = (float)(g->gk[i] * s);
+  }
+  // shapes (edge tiles may be clipped by the image bounds, numpy slicing)
+  int max_a = 0, max_b = 0, max_smap = 0, max_bl = 0, max_cand = 0;
+  for (int ty = 0; ty < nty; ++ty)
+    for (int tx = 0; tx < ntx; ++tx) {
+      const int y0 = ty * g->tile_h, x0 = tx * g->tile_w;
+      const int h = min(ph, H - y0), w = min(pw, W - x0);
+      int s = 0;
+      for (; s < g->nshapes; ++s)
+        if (g->sw[s] == w && g->sh[s] == h) break;
+      if (s == g->nshapes) {
+        SLAM_REQUIRE(g->nshapes < kMaxShapes, "slam_orb: too many distinct patch shapes");
+        SLAM_REQUIRE(w <= 1023 && h <= 1023, "slam_orb: patch %dx%d too large", w, h);
+        g->sw[s] = w;
+        g->sh[s] = h;
+        int last = -1;
+        for (int l = 0; l < kNLev; ++l) {
+          g->lw[s][l] = (int)nearbyintf((float)w / g->ls[l]);
+          g->lh[s][l] = (int)nearbyintf((float)h / g->ls[l]);
+          if (g->lw[s][l] > 2 * kEdge && g->lh[s][l] > 2 * kEdge && g->nl[l] > 0) last = l;
+        }
+        g->nlev[s] = last + 1;
+        max_a = max(max_a, w * h);
+        if (last >= 1) max_b = max(max_b, g->lw[s][1] * g->lh[s][1]);
+        const int W0 = w, H0 = h;
+        if (W0 > 2 * kEdge && H0 > 2 * kEdge) {
+          const int cand = ((W0 - 2 * kEdge + 1) / 2) * ((H0 - 2 * kEdge + 1) / 2);
+          const int smap = (((W0 - 2 * kNMS0) * (H0 - 2 * kNMS0)) + 15) & ~15;
+          const int bl = (W0 - 2 * kBl0) * (H0 - 2 * kBl0);
+          max_cand = max(max_cand, cand);
+          max_smap = max(max_smap, smap);
+          max_bl = max(max_bl, bl);
+        }
+        ++g->nshapes;
+      }
+      g->tile_shape[ty * ntx + tx] = (uint8_t)s;
+    }
+  auto al = [](int v) { return (v + 15) & ~15; };
+  const int max_u = max(max_smap + 8 * max_cand, max_bl);
+  int nmax = 0;
+  for (int l = 0; l < kNLev; ++l) nmax = max(nmax, g->nl[l]);
+  g->cand_cap = max_cand;
+  g->list_cap = max(2 * nmax, nmax + 256);
+  g->lds_a = 0;
+  g->lds_b = al(max_a);
+  g->lds_u = g->lds_b + al(max_b);
+  g->lds_l = g->lds_u + al(max_u);
+  g->lds_m = g->lds_l + al(g->list_cap * (int)sizeof(KP));
+  g->lds_total = g->lds_m + (256 + 16 + 2 * 1024) * 4;
+  g->tcap = max_kp + 64;
+  SLAM_REQUIRE(g->lds_total <= 160 * 1024,
+               "slam_orb: patch %dx%d needs %d B of LDS (> 160 KiB)", pw, ph, g->lds_total);
+  return SLAM_OK;
+}
+
+bool g_pattern_uploaded[64] = {false};
+
+}  // namespace
+
+extern "C" int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int overlap_div,
+                                        int height_div, int width_div, size_t* bytes) {
+  OrbGeom g;
+  if (int rc = build_geom(H, W, W, max_kp, overlap_div, height_div, width_div, &g)) return rc;
+  SLAM_REQUIRE(bytes != nullptr && batch >= 0, "slam_orb_workspace_bytes: bad args");
+  const size_t slots = (size_t)batch * g.n_tiles * g.tcap;
+  *bytes = slots * (5 * sizeof(float) + sizeof(int32_t) + 32) + (size_t)batch * g.n_tiles * 4 + 256;
+  return SLAM_OK;
+}
+
+extern "C" int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int stride,
+                              int max_kp, int overlap_div, int height_div, int width_div,
+                              void* d_ws, size_t ws_bytes, float* d_kp, int32_t* d_octave,
+                              uint8_t* d_desc, int32_t* d_count, int kp_cap, void* stream) {
+  OrbGeom g;
+  if (int rc = build_geom(H, W, stride, max_kp, overlap_div, height_div, width_div, &g)) return rc;
+  SLAM_REQUIRE(batch >= 0 && kp_cap >= 0, "slam_orb_tiles: bad batch/kp_cap");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_img && d_ws && d_kp && d_octave && d_desc && d_count,
+               "slam_orb_tiles: null pointer");
+  size_t need = 0;
+  if (int rc = slam_orb_workspace_bytes(batch, H, W, max_kp, overlap_div, height_div, width_div,
+                                        &need))
+    return rc;
+  if (ws_bytes < need) {
+    slam::set_error("slam_orb_tiles: workspace %zu < %zu bytes", ws_bytes, need);
+    return SLAM_ERR_WORKSPACE;
+  }
+  hipStream_t s = slam::as_stream(stream);
+  int dev = 0;
+  SLAM_HIP(hipGetDevice(&dev));
+  if (dev < 64 && !g_pattern_uploaded[dev]) {
+    SLAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern, sizeof(kOrbPattern)));
+    g_pattern_uploaded[dev] = true;
+  }
+  const size_t slots = (size_t)batch * g.n_tiles * g.tcap;
+  uint8_t* base = static_cast<uint8_t*>(d_ws);
+  float* ws_kp = reinterpret_cast<float*>(base);
+  int32_t* ws_oct = reinterpret_cast<int32_t*>(base + slots * 5 * sizeof(float));
+  uint8_t* ws_desc = base + slots * (5 * sizeof(float) + sizeof(int32_t));
+  int32_t* ws_cnt = reinterpret_cast<int32_t*>(ws_desc + slots * 32);
+  SLAM_REQUIRE(((uintptr_t)ws_cnt & 3) == 0, "slam_orb_tiles: workspace misaligned");
+  k_orb_tile<<<dim3(g.n_tiles, batch), kOrbWG, g.lds_total, s>>>(d_img, g, ws_kp, ws_oct,
+                                                                  ws_desc, ws_cnt);
+  SLAM_LAUNCHED("k_orb_tile");
+  k_orb_compact<<<batch, 256, 0, s>>>(ws_kp, ws_oct, ws_desc, ws_cnt, g.n_tiles, g.tcap, d_kp,
+                                      d_octave, d_desc, d_count, kp_cap);
+  SLAM_LAUNCHED("k_orb_compact");
+  return SLAM_OK;
+}

@@ -46,6 +46,10 @@ SIGNATURES = {
     "slam_device_count": [],
     "slam_hamming_knn2": [c_p, c_p, c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p],
     "slam_compact_matches": [c_p, c_p, c_p, c_int, c_int, c_p, c_double, c_p, c_p, c_p],
+    "slam_orb_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 ctypes.POINTER(c_size_t)],
+    "slam_orb_tiles": [c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
+                       c_size_t, c_p, c_p, c_p, c_p, c_int, c_p],
     "slam_ba_residual": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p],
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_ba_red_slots": [c_int, c_int],

@@ -79,3 +79,124 @@ def perturb(rng, cams, pts, rot_s=1e-3, t_s=1e-2, p_s=0.05):
     c[:, :3] += rng.normal(0, rot_s, c[:, :3].shape)
     c[:, 3:6] += rng.normal(0, t_s, c[:, 3:6].shape)
     return c, pts + rng.normal(0, p_s, pts.shape)
+
+
+# ----------------------------------------------------------------------------- stereo sequences
+class StereoRig:
+    """Pinhole stereo pair of SURVEY.md §8d: fx = fy = 0.56 W, principal point at
+    the centre, baseline 0.54 m (P_r[0,3] = -fx * b), KITTI calib.txt layout."""
+
+    def __init__(self, W, H, baseline=0.54):
+        self.W, self.H = W, H
+        f = 0.56 * W
+        self.K = np.array([[f, 0, W / 2.0], [0, f, H / 2.0], [0, 0, 1.0]])
+        self.P_l = np.hstack([self.K, np.zeros((3, 1))])
+        self.P_r = self.P_l.copy()
+        self.P_r[0, 3] = -f * baseline
+        self.baseline = baseline
+
+    def calib_text(self):
+        """Two lines of 12 floats, the format load_calib reads
+        (/root/reference/visual_odometry_solution_methods.py:9-17)."""
+        return "\n".join(" ".join(repr(float(v)) for v in P.ravel())
+                         for P in (self.P_l, self.P_r)) + "\n"
+
+
+def _value_noise(rng, H, W, cell=48, lo=70, hi=170):
+    gh, gw = H // cell + 2, W // cell + 2
+    g = rng.uniform(lo, hi, (gh, gw))
+    ys = np.arange(H) / cell
+    xs = np.arange(W) / cell
+    y0, x0 = ys.astype(int), xs.astype(int)
+    fy, fx = (ys - y0)[:, None], (xs - x0)[None, :]
+    a = g[y0][:, x0]
+    b = g[y0][:, x0 + 1]
+    c = g[y0 + 1][:, x0]
+    d = g[y0 + 1][:, x0 + 1]
+    return (a * (1 - fx) + b * fx) * (1 - fy) + (c * (1 - fx) + d * fx) * fy
+
+
+def make_world(rng, n_frames, n_landmarks=20000):
+    """Corridor of landmarks: x in [-20,20], y in [-3,3], z in [5, 80 + frames]."""
+    z = rng.uniform(5.0, 80.0 + n_frames, n_landmarks)
+    X = np.stack([rng.uniform(-20, 20, n_landmarks), rng.uniform(-3, 3, n_landmarks), z], 1)
+    size = rng.integers(5, 12, n_landmarks)
+    val = np.where(rng.random(n_landmarks) < 0.5, rng.integers(0, 50, n_landmarks),
+                   rng.integers(205, 256, n_landmarks))
+    return X, size, val
+
+
+def trajectory(rng, n_frames, step=1.0, yaw_sigma_deg=0.2):
+    """Camera-to-world poses (4x4): forward 1 m/frame along +z, yaw jitter."""
+    poses = []
+    yaw = 0.0
+    pos = np.zeros(3)
+    for i in range(n_frames):
+        c, s = np.cos(yaw), np.sin(yaw)
+        R = np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+        T = np.eye(4)
+        T[:3, :3], T[:3, 3] = R, pos
+        poses.append(T)
+        pos = pos + R @ np.array([0, 0, step])
+        yaw += np.deg2rad(rng.normal(0, yaw_sigma_deg))
+    return np.stack(poses)
+
+
+def render(world, T_cw_inv, rig: StereoRig, rng, x_offset=0.0, bg=None, noise=2.0):
+    """Render one grayscale view: landmarks as fixed-size squares (painter's
+    order) over value noise, plus Gaussian noise; x_offset shifts the camera
+    along its x axis (right camera = +baseline)."""
+    X, size, val = world
+    H, W = rig.H, rig.W
+    img = (bg if bg is not None else _value_noise(rng, H, W)).copy()
+    R, t = T_cw_inv[:3, :3], T_cw_inv[:3, 3]
+    Xc = X @ R.T + t
+    Xc[:, 0] -= x_offset
+    vis = Xc[:, 2] > 1.0
+    Xc, sz, vv = Xc[vis], size[vis], val[vis]
+    u = rig.K[0, 0] * Xc[:, 0] / Xc[:, 2] + rig.K[0, 2]
+    v = rig.K[1, 1] * Xc[:, 1] / Xc[:, 2] + rig.K[1, 2]
+    inb = (u > -12) & (u < W + 12) & (v > -12) & (v < H + 12)
+    u, v, sz, vv, z = u[inb], v[inb], sz[inb], vv[inb], Xc[inb, 2]
+    order = np.argsort(-z, kind="stable")  # far first, near drawn last
+    u, v, sz, vv = u[order], v[order], sz[order], vv[order]
+    x0 = np.round(u - sz / 2).astype(np.int64)
+    y0 = np.round(v - sz / 2).astype(np.int64)
+    flat = img.reshape(-1)
+    for s in np.unique(sz):
+        m = np.nonzero(sz == s)[0]
+        dy, dx = np.meshgrid(np.arange(s), np.arange(s), indexing="ij")
+        yy = y0[m, None] + dy.ravel()[None, :]
+        xx = x0[m, None] + dx.ravel()[None, :]
+        ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
+        # keep painter's order across size groups: write in global order below
+        m_idx = np.broadcast_to(m[:, None], yy.shape)
+        if s == np.unique(sz)[0]:
+            all_pix, all_ord, all_val = [], [], []
+        all_pix.append((yy * W + xx)[ok])
+        all_ord.append(m_idx[ok])
+        all_val.append(np.broadcast_to(vv[m, None], yy.shape)[ok])
+    if len(u):
+        pix = np.concatenate(all_pix)
+        ordr = np.concatenate(all_ord)
+        vals = np.concatenate(all_val)
+        srt = np.argsort(ordr, kind="stable")
+        flat[pix[srt]] = vals[srt]  # later (nearer) writes win
+    img = img + rng.normal(0, noise, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def stereo_sequence(n_frames, W=1280, H=720, seed=0, n_landmarks=20000):
+    """(left [F,H,W] u8, right [F,H,W] u8, poses [F,4,4] camera-to-world, rig)."""
+    rng = np.random.default_rng(seed)
+    rig = StereoRig(W, H)
+    world = make_world(rng, n_frames, n_landmarks)
+    poses = trajectory(rng, n_frames)
+    bg = _value_noise(rng, H, W)
+    left = np.empty((n_frames, H, W), np.uint8)
+    right = np.empty((n_frames, H, W), np.uint8)
+    for i in range(n_frames):
+        Tinv = np.linalg.inv(poses[i])
+        left[i] = render(world, Tinv, rig, rng, 0.0, bg)
+        right[i] = render(world, Tinv, rig, rng, rig.baseline, bg)
+    return left, right, poses, rig

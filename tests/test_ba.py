@@ -198,10 +198,11 @@ def test_gpu_local_ba_config3_converges(C, P, k):
     prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
     c0 = 0.5 * float(np.sum(oba.residual_and_jacobian(cams0, pts0, ci, pi, qs)[0] ** 2))
     st = prob.solve(max_iters=60, ftol=1e-12)
-    # converged to the noise floor: 0.5 * sum r^2 ~ 0.5 * (2O - dof) * sigma^2
+    # converged to the noise floor: 0.5 * sum r^2 ~ 0.5 * (2O - n_params) * sigma^2
     O = len(ci)
-    assert st["COST"] < 0.5 * 2 * O * 0.25 * 1.1
-    assert st["COST"] < 1e-2 * c0
+    floor = 0.5 * (2 * O - 9 * C - 3 * P) * 0.25
+    assert 0.9 * floor < st["COST"] < 1.1 * floor
+    assert st["COST"] < 0.1 * c0
     gc, gp = prob.params()
     r = oba.residual_and_jacobian(gc, gp, ci, pi, qs)[0]
     assert abs(0.5 * float(np.sum(r * r)) - st["COST"]) <= 1e-8 * st["COST"]
