@@ -84,6 +84,42 @@ int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,
 
 
 /* ------------------------------------------------------------------------
+ * Geometry of one tracking step (main.py:82-97), batched over frame pairs.
+ * ---------------------------------------------------------------------- */
+
+/* Gather of matched keypoints (keypoint.py:96-100, Point3D.py:214-216):
+ * for k < count[b], (qi, ti) = pairs[b][k]:
+ *   ptq[b][k] = (double)kpq[b][qi].xy, ptt[b][k] = (double)kpt[b][ti].xy,
+ *   dq[b][k] = desq[b][qi], dt[b][k] = dest[b][ti]  (descriptors optional: NULL).
+ * kp arrays are [batch][cap][5] f32 as written by slam_orb_tiles. */
+int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int kt_cap,
+                        const uint8_t* d_desq, const uint8_t* d_dest, const int32_t* d_pairs,
+                        const int32_t* d_count, int p_cap, int batch, double* d_ptq,
+                        double* d_ptt, uint8_t* d_dq, uint8_t* d_dt, void* stream);
+
+/* cv2.triangulatePoints + dehomogenisation (Point3D.py:14-19): per point the
+ * null vector of the 4x4 DLT system (rows x*P[2]-P[0], y*P[2]-P[1] of both
+ * views), one-sided Jacobi SVD in f64.  d_ptl/d_ptr [batch][cap][2] f64,
+ * d_X [batch][cap][3] f64.  P matrices are 3x4 row-major f64: shared by all
+ * items (proj_stride 0) or one per item (proj_stride 12). */
+int slam_triangulate(const double* d_ptl, const double* d_ptr, const int32_t* d_count, int cap,
+                     int batch, const double* d_Pl, const double* d_Pr, int proj_stride,
+                     double* d_X, void* stream);
+
+/* cv2.solvePnPRansac(Q, q, K, zeros(5)) (transformation.py:11-13), restated
+ * deterministically (oracle/geometry.c): n_hyp hypotheses of 5 points drawn
+ * from splitmix64(seed, item0 + b, h), LM from r = t = 0 (hyp_iters), score =
+ * #(|reprojection error| <= reproj_thresh), best = max score / lowest h, LM
+ * refinement over its inliers (refine_iters).  One workgroup per item.
+ * Outputs: d_rvec/d_tvec [batch][3] (X_cam = R(rvec) X + tvec), d_ninliers
+ * [batch] (-1 when count < 5, the reference's `len(Q) > 4` guard, main.py:94),
+ * d_mask [batch][cap] u8 inliers of the chosen hypothesis. */
+int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count, int cap,
+                    int batch, const double* d_K, uint64_t seed, int item0, int n_hyp,
+                    double reproj_thresh, int hyp_iters, int refine_iters, double* d_rvec,
+                    double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, void* stream);
+
+/* ------------------------------------------------------------------------
  * Tiled ORB detector + rBRIEF descriptor.
  *
  * Replaces orb_detector_using_tiles (/root/reference/orb.py:4-25), i.e. the

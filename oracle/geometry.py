@@ -1,0 +1,103 @@
+"""ORACLE (test infrastructure only): triangulation, pose and PnP on the CPU.
+
+  triangulate_points_local  /root/reference/Point3D.py:14-19 (cv2.triangulatePoints:
+                            per point, rows x*P[2]-P[0], y*P[2]-P[1] of both views,
+                            null vector = last row of V^T of the 4x4 SVD; X = v[:3]/v[3])
+  relative_to_abs3DPoints   Point3D.py:22-30
+  sort_3D_points            Point3D.py:5-10
+  rodrigues / form_transf / calculate_transformation_matrix
+                            transformation.py:5-37 (incl. the r, t sign flip)
+  pnp_ransac                oracle/geometry.c (seeded RANSAC + LM spec)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _ptr, lib
+
+
+def triangulate_points_local(qs_l, qs_r, P_l, P_r):
+    ql = np.asarray(qs_l, np.float64).reshape(-1, 2)
+    qr = np.asarray(qs_r, np.float64).reshape(-1, 2)
+    M = len(ql)
+    A = np.empty((M, 4, 4))
+    for j, (q, P) in enumerate(((ql, np.asarray(P_l, float)), (qr, np.asarray(P_r, float)))):
+        A[:, 2 * j] = q[:, 0:1] * P[2][None] - P[0][None]
+        A[:, 2 * j + 1] = q[:, 1:2] * P[2][None] - P[1][None]
+    if M == 0:
+        return np.zeros((0, 3))
+    _, _, Vt = np.linalg.svd(A)
+    h = Vt[:, -1, :]
+    return h[:, :3] / h[:, 3:4]
+
+
+def relative_to_abs3DPoints(points3D, camera_frame):
+    P = np.asarray(points3D, float).reshape(-1, 3)
+    hom = np.hstack((P, np.ones((len(P), 1))))
+    a = np.matmul(camera_frame, hom.T)
+    return (a[:3] / a[3]).T
+
+
+def sort_3D_points(pts, close_def_in_m=100, far_def_in_m=1):
+    close = [(abs(x[0]) < close_def_in_m and abs(x[1]) < close_def_in_m and abs(x[2]) < close_def_in_m)
+             for x in pts]
+    far = [(abs(x[0]) > far_def_in_m or abs(x[1]) > far_def_in_m or abs(x[2]) > far_def_in_m)
+           for x in pts]
+    return close, far
+
+
+def rodrigues(r):
+    r = np.asarray(r, float).ravel()
+    th = np.linalg.norm(r)
+    if th < np.finfo(float).eps:
+        return np.eye(3)
+    k = r / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.cos(th) * np.eye(3) + (1 - np.cos(th)) * np.outer(k, k) + np.sin(th) * K
+
+
+def form_transf(R, t):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = np.asarray(t).ravel()
+    return T
+
+
+def pose_matrix_from_pnp(rvec, tvec):
+    """transformation.py:15-19: r <- -r, t <- -t, T = [Rodrigues(-r) | -t]."""
+    r = -1 * np.asarray(rvec, float).reshape(3, 1)
+    t = -1 * np.asarray(tvec, float).reshape(3, 1)
+    return form_transf(rodrigues(r), t.T), r, t
+
+
+_PNP = None
+
+
+def _pnp_fn():
+    global _PNP
+    if _PNP is None:
+        f = lib().oracle_pnp_ransac
+        p, i, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        f.argtypes = [p, p, i, p, ctypes.c_uint64, i, i, d, i, i, p, p, p, p, p]
+        f.restype = ctypes.c_int
+        _PNP = f
+    return _PNP
+
+
+def pnp_ransac(Q, q, K, seed=0, item=0, n_hyp=100, thresh=8.0, hyp_iters=10, refine_iters=20,
+               return_hypotheses=False):
+    Q = np.ascontiguousarray(Q, np.float64).reshape(-1, 3)
+    q = np.ascontiguousarray(q, np.float64).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float64).reshape(3, 3)
+    L = len(Q)
+    rvec = np.zeros(3)
+    tvec = np.zeros(3)
+    mask = np.zeros(max(L, 1), np.uint8)
+    hyp = np.zeros((n_hyp, 6))
+    hc = np.zeros(n_hyp, np.int32)
+    n = _pnp_fn()(_ptr(Q), _ptr(q), L, _ptr(K), seed & ((1 << 64) - 1), item, n_hyp, thresh,
+                  hyp_iters, refine_iters, _ptr(rvec), _ptr(tvec), _ptr(mask), _ptr(hyp), _ptr(hc))
+    out = (rvec, tvec, n, mask[:L].astype(bool))
+    return out + (hyp, hc) if return_hypotheses else out

@@ -1,0 +1,513 @@
+// Matched-point gather, DLT triangulation and RANSAC + LM PnP for gfx950.
+//
+// Replaces, per frame pair of the tracking loop (/root/reference/main.py:82-97):
+//   keypoint.py:96-100        gather of matched points (f64) and descriptors
+//   Point3D.py:14-19          cv2.triangulatePoints (per-point 4x4 SVD null vector)
+//   transformation.py:5-19    cv2.solvePnPRansac(Q, q, K, 0) (ITERATIVE flavour:
+//                             minimal 5-point LM hypotheses, 8 px reprojection
+//                             threshold, LM refinement on the inliers)
+// RANSAC sampling is a counter-based splitmix64 stream keyed by (seed, frame,
+// hypothesis) so the CPU oracle draws the same subsets (OpenCV's own RNG
+// sequence is not reproducible here).
+#include "common.hpp"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kBS = 256;
+
+// --------------------------------------------------------------- gather
+__global__ __launch_bounds__(kBS) void k_gather(const float* __restrict__ kpq, int kq_cap,
+                                                const float* __restrict__ kpt, int kt_cap,
+                                                const uint8_t* __restrict__ dq_in,
+                                                const uint8_t* __restrict__ dt_in,
+                                                const int2* __restrict__ pairs,
+                                                const int32_t* __restrict__ count, int p_cap,
+                                                double* __restrict__ ptq, double* __restrict__ ptt,
+                                                uint8_t* __restrict__ dq, uint8_t* __restrict__ dt) {
+  const int b = blockIdx.y;
+  const int n = min(max(count[b], 0), p_cap);
+  const int k = blockIdx.x * kBS + threadIdx.x;
+  if (k >= n) return;
+  const size_t o = (size_t)b * p_cap + k;
+  const int2 pr = pairs[o];
+  const float* a = kpq + ((size_t)b * kq_cap + pr.x) * 5;
+  const float* c = kpt + ((size_t)b * kt_cap + pr.y) * 5;
+  ptq[2 * o] = (double)a[0];
+  ptq[2 * o + 1] = (double)a[1];
+  ptt[2 * o] = (double)c[0];
+  ptt[2 * o + 1] = (double)c[1];
+  if (dq) {
+    const uint4* s0 = reinterpret_cast<const uint4*>(dq_in + ((size_t)b * kq_cap + pr.x) * 32);
+    const uint4* s1 = reinterpret_cast<const uint4*>(dt_in + ((size_t)b * kt_cap + pr.y) * 32);
+    uint4* d0 = reinterpret_cast<uint4*>(dq + o * 32);
+    uint4* d1 = reinterpret_cast<uint4*>(dt + o * 32);
+    d0[0] = s0[0];
+    d0[1] = s0[1];
+    d1[0] = s1[0];
+    d1[1] = s1[1];
+  }
+}
+
+// --------------------------------------------------------------- triangulation
+// Null vector of the 4x4 DLT matrix by one-sided (Hestenes) Jacobi SVD in f64.
+__device__ void null_vector4(double A[4][4], double v[4]) {
+  double V[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    double off = 0.0;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int q = p + 1; q < 4; ++q) {
+        double al = 0, be = 0, ga = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          al += A[i][p] * A[i][p];
+          be += A[i][q] * A[i][q];
+          ga += A[i][p] * A[i][q];
+        }
+        const double den = sqrt(al * be);
+        if (den == 0.0 || fabs(ga) <= 1e-15 * den) continue;
+        off = fmax(off, fabs(ga) / den);
+        const double zeta = (be - al) / (2.0 * ga);
+        const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + tt * tt), s = c * tt;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double ap = A[i][p], aq = A[i][q];
+          A[i][p] = c * ap - s * aq;
+          A[i][q] = s * ap + c * aq;
+          const double vp = V[i][p], vq = V[i][q];
+          V[i][p] = c * vp - s * vq;
+          V[i][q] = s * vp + c * vq;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  int best = 0;
+  double bn = 1e300;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double nn = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) nn += A[i][j] * A[i][j];
+    if (nn < bn) {
+      bn = nn;
+      best = j;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = V[i][best];
+}
+
+__global__ __launch_bounds__(kBS) void k_triangulate(const double* __restrict__ pl,
+                                                     const double* __restrict__ pr,
+                                                     const int32_t* __restrict__ count, int cap,
+                                                     const double* __restrict__ Pl,
+                                                     const double* __restrict__ Pr, int pstride,
+                                                     double* __restrict__ X) {
+  const int b = blockIdx.y;
+  const int n = min(max(count[b], 0), cap);
+  const int k = blockIdx.x * kBS + threadIdx.x;
+  if (k >= n) return;
+  const double* P[2] = {Pl + (size_t)b * pstride, Pr + (size_t)b * pstride};
+  const size_t o = (size_t)b * cap + k;
+  const double xy[2][2] = {{pl[2 * o], pl[2 * o + 1]}, {pr[2 * o], pr[2 * o + 1]}};
+  double A[4][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      A[2 * j][c] = xy[j][0] * P[j][8 + c] - P[j][c];
+      A[2 * j + 1][c] = xy[j][1] * P[j][8 + c] - P[j][4 + c];
+    }
+  double v[4];
+  null_vector4(A, v);
+  X[3 * o] = v[0] / v[3];
+  X[3 * o + 1] = v[1] / v[3];
+  X[3 * o + 2] = v[2] / v[3];
+}
+
+// --------------------------------------------------------------- PnP
+__device__ __host__ inline uint64_t splitmix64(uint64_t& s) {
+  s += 0x9E3779B97F4A7C15ull;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// cv::Rodrigues (rotation vector -> matrix)
+__device__ inline void rodrigues(const double r[3], double R[9]) {
+  const double th = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+  if (th < 2.220446049250313e-16) {
+    R[0] = 1; R[1] = 0; R[2] = 0; R[3] = 0; R[4] = 1; R[5] = 0; R[6] = 0; R[7] = 0; R[8] = 1;
+    return;
+  }
+  const double c = cos(th), s = sin(th), c1 = 1.0 - c, it = 1.0 / th;
+  const double x = r[0] * it, y = r[1] * it, z = r[2] * it;
+  R[0] = c + c1 * x * x; R[1] = c1 * x * y - s * z; R[2] = c1 * x * z + s * y;
+  R[3] = c1 * x * y + s * z; R[4] = c + c1 * y * y; R[5] = c1 * y * z - s * x;
+  R[6] = c1 * x * z - s * y; R[7] = c1 * y * z + s * x; R[8] = c + c1 * z * z;
+}
+
+struct Cam {
+  double fx, fy, cx, cy;
+};
+
+// reprojection residual of one point and (optionally) its 2x6 Jacobian wrt (r, t)
+template <bool JAC>
+__device__ inline void pnp_residual(const double p[6], const double R[9], const double* Q,
+                                    const double* q, const Cam& K, double r[2], double J[2][6]) {
+  const double X0 = Q[0], X1 = Q[1], X2 = Q[2];
+  const double RX0 = R[0] * X0 + R[1] * X1 + R[2] * X2;
+  const double RX1 = R[3] * X0 + R[4] * X1 + R[5] * X2;
+  const double RX2 = R[6] * X0 + R[7] * X1 + R[8] * X2;
+  const double Xc = RX0 + p[3], Yc = RX1 + p[4], Zc = RX2 + p[5];
+  const double iz = 1.0 / Zc;
+  r[0] = K.fx * (Xc * iz) + K.cx - q[0];
+  r[1] = K.fy * (Yc * iz) + K.cy - q[1];
+  if constexpr (JAC) {
+    const double du[3] = {K.fx * iz, 0.0, -K.fx * Xc * iz * iz};
+    const double dv[3] = {0.0, K.fy * iz, -K.fy * Yc * iz * iz};
+    // dRX/dr: Gallego & Yezzi, -[RX]x at r = 0
+    double D[3][3];
+    const double w0 = p[0], w1 = p[1], w2 = p[2];
+    const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+    if (th2 < 1e-24) {
+      D[0][0] = 0; D[0][1] = RX2; D[0][2] = -RX1;
+      D[1][0] = -RX2; D[1][1] = 0; D[1][2] = RX0;
+      D[2][0] = RX1; D[2][1] = -RX0; D[2][2] = 0;
+    } else {
+      const double W[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
+      const double w[3] = {w0, w1, w2};
+      double Am[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) {
+          double acc = w[i] * w[k];
+          for (int j = 0; j < 3; ++j) acc += R[3 * j + i] * W[j][k];
+          Am[i][k] = acc - W[i][k];
+        }
+      const double Xs[3][3] = {{0.0, -X2, X1}, {X2, 0.0, -X0}, {-X1, X0, 0.0}};
+      double B[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          B[i][k] = Xs[i][0] * Am[0][k] + Xs[i][1] * Am[1][k] + Xs[i][2] * Am[2][k];
+      const double inv = -1.0 / th2;
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          D[i][k] = (R[3 * i] * B[0][k] + R[3 * i + 1] * B[1][k] + R[3 * i + 2] * B[2][k]) * inv;
+    }
+    for (int k = 0; k < 3; ++k) {
+      J[0][k] = du[0] * D[0][k] + du[1] * D[1][k] + du[2] * D[2][k];
+      J[1][k] = dv[0] * D[0][k] + dv[1] * D[1][k] + dv[2] * D[2][k];
+      J[0][3 + k] = du[k];
+      J[1][3 + k] = dv[k];
+    }
+  }
+}
+
+// Solve (H + lam diag(H)) d = -g for the 6x6 SPD system (Cholesky); false on failure.
+__device__ inline bool solve6(const double H[21], const double g[6], double lam, double d[6]) {
+  double A[6][6];
+  int k = 0;
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j <= i; ++j) {
+      A[i][j] = H[k];
+      A[j][i] = H[k];
+      ++k;
+    }
+  for (int i = 0; i < 6; ++i) A[i][i] += lam * fmax(A[i][i], 1e-12);
+  for (int j = 0; j < 6; ++j) {
+    double s = A[j][j];
+    for (int p = 0; p < j; ++p) s -= A[j][p] * A[j][p];
+    if (!(s > 0.0)) return false;
+    A[j][j] = sqrt(s);
+    for (int i = j + 1; i < 6; ++i) {
+      double t = A[i][j];
+      for (int p = 0; p < j; ++p) t -= A[i][p] * A[j][p];
+      A[i][j] = t / A[j][j];
+    }
+  }
+  double y[6];
+  for (int i = 0; i < 6; ++i) {
+    double t = -g[i];
+    for (int p = 0; p < i; ++p) t -= A[i][p] * y[p];
+    y[i] = t / A[i][i];
+  }
+  for (int i = 5; i >= 0; --i) {
+    double t = y[i];
+    for (int p = i + 1; p < 6; ++p) t -= A[p][i] * d[p];
+    d[i] = t / A[i][i];
+  }
+  return true;
+}
+
+constexpr int kMinSample = 5;
+constexpr int kPnPWG = 256;
+constexpr int kMaxHyp = 256;
+
+// LM on a handful of points entirely in one thread (hypothesis generation).
+__device__ void lm_small(const double* Q, const double* q, const int* idx, int n, const Cam& K,
+                         int iters, double p[6]) {
+  double lam = 1e-3;
+  double R[9];
+  for (int it = 0; it < iters; ++it) {
+    rodrigues(p, R);
+    double H[21] = {0}, g[6] = {0}, cost = 0.0;
+    for (int s = 0; s < n; ++s) {
+      double r[2], J[2][6];
+      pnp_residual<true>(p, R, Q + 3 * idx[s], q + 2 * idx[s], K, r, J);
+      for (int a = 0; a < 2; ++a) {
+        int k = 0;
+        for (int i = 0; i < 6; ++i) {
+          for (int j = 0; j <= i; ++j) H[k++] += J[a][i] * J[a][j];
+          g[i] += J[a][i] * r[a];
+        }
+        cost += r[a] * r[a];
+      }
+    }
+    double d[6], pn[6];
+    if (!solve6(H, g, lam, d)) {
+      lam = fmin(lam * 10.0, 1e12);
+      continue;
+    }
+    for (int i = 0; i < 6; ++i) pn[i] = p[i] + d[i];
+    double Rn[9];
+    rodrigues(pn, Rn);
+    double cn = 0.0;
+    for (int s = 0; s < n; ++s) {
+      double r[2], J[2][6];
+      pnp_residual<false>(pn, Rn, Q + 3 * idx[s], q + 2 * idx[s], K, r, J);
+      cn += r[0] * r[0] + r[1] * r[1];
+    }
+    if (cn < cost) {
+      for (int i = 0; i < 6; ++i) p[i] = pn[i];
+      lam = fmax(lam * 0.1, 1e-12);
+    } else {
+      lam = fmin(lam * 10.0, 1e12);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
+                                                const double* __restrict__ qall,
+                                                const int32_t* __restrict__ count, int cap,
+                                                const double* __restrict__ Kp, uint64_t seed,
+                                                int item0, int n_hyp, double thresh,
+                                                int hyp_iters, int refine_iters,
+                                                double* __restrict__ rvec, double* __restrict__ tvec,
+                                                int32_t* __restrict__ ninl,
+                                                uint8_t* __restrict__ mask) {
+  __shared__ double hp[kMaxHyp][6];
+  __shared__ int hcnt[kMaxHyp];
+  __shared__ double red[kPnPWG / 64][28];
+  __shared__ double pose[6], stepd[6];
+  __shared__ int best_s, ok_s;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, wid = t >> 6;
+  const int L = min(max(count[b], 0), cap);
+  const double* Q = Qall + (size_t)b * cap * 3;
+  const double* q = qall + (size_t)b * cap * 2;
+  const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
+  if (L < kMinSample) {
+    if (t == 0) {
+      ninl[b] = -1;
+      for (int i = 0; i < 3; ++i) rvec[3 * b + i] = tvec[3 * b + i] = 0.0;
+    }
+    for (int i = t; i < L; i += kPnPWG) mask[(size_t)b * cap + i] = 0;
+    return;
+  }
+  const double thr2 = thresh * thresh;
+  // ---- hypotheses: one per thread, 5 distinct random points, LM from r = t = 0
+  for (int h = t; h < n_hyp; h += kPnPWG) {
+    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+    int idx[kMinSample];
+    for (int k = 0; k < kMinSample; ++k) {
+      int v;
+      bool dup;
+      do {
+        v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
+        dup = false;
+        for (int j = 0; j < k; ++j) dup |= idx[j] == v;
+      } while (dup);
+      idx[k] = v;
+    }
+    double p[6] = {0, 0, 0, 0, 0, 0};
+    lm_small(Q, q, idx, kMinSample, K, hyp_iters, p);
+    for (int i = 0; i < 6; ++i) hp[h][i] = p[i];
+    hcnt[h] = 0;
+  }
+  __syncthreads();
+  // ---- inlier counts: hypothesis-major, points across the workgroup
+  for (int h = 0; h < n_hyp; ++h) {
+    double R[9], p[6];
+    for (int i = 0; i < 6; ++i) p[i] = hp[h][i];
+    const bool finite = isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]) && isfinite(p[3]) &&
+                        isfinite(p[4]) && isfinite(p[5]);
+    rodrigues(p, R);
+    int c = 0;
+    if (finite)
+      for (int i = t; i < L; i += kPnPWG) {
+        double r[2], J[2][6];
+        pnp_residual<false>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
+        c += (r[0] * r[0] + r[1] * r[1] <= thr2) ? 1 : 0;
+      }
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (lane == 0) atomicAdd(&hcnt[h], finite ? c : 0);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int bh = 0;
+    for (int h = 1; h < n_hyp; ++h)
+      if (hcnt[h] > hcnt[bh]) bh = h;
+    best_s = bh;
+    for (int i = 0; i < 6; ++i) pose[i] = hp[bh][i];
+  }
+  __syncthreads();
+  // ---- LM refinement over the best hypothesis' inlier set (fixed set)
+  const int bh = best_s;
+  {
+    double R[9], p[6];
+    for (int i = 0; i < 6; ++i) p[i] = hp[bh][i];
+    rodrigues(p, R);
+    for (int i = t; i < L; i += kPnPWG) {
+      double r[2], J[2][6];
+      pnp_residual<false>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
+      mask[(size_t)b * cap + i] = (r[0] * r[0] + r[1] * r[1] <= thr2) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  double lam = 1e-3;  // uniform across the workgroup
+  for (int it = 0; it < refine_iters; ++it) {
+    double p[6], R[9];
+    for (int i = 0; i < 6; ++i) p[i] = pose[i];
+    rodrigues(p, R);
+    double acc[28];
+    for (int i = 0; i < 28; ++i) acc[i] = 0.0;
+    for (int i = t; i < L; i += kPnPWG) {
+      if (!mask[(size_t)b * cap + i]) continue;
+      double r[2], J[2][6];
+      pnp_residual<true>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
+      for (int a = 0; a < 2; ++a) {
+        int k = 0;
+        for (int u = 0; u < 6; ++u) {
+          for (int v = 0; v <= u; ++v) acc[k++] += J[a][u] * J[a][v];
+          acc[21 + u] += J[a][u] * r[a];
+        }
+        acc[27] += r[a] * r[a];
+      }
+    }
+    for (int i = 0; i < 28; ++i) {
+      double v = acc[i];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+      if (lane == 0) red[wid][i] = v;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double H[21], g[6], cost = 0.0;
+      for (int i = 0; i < 28; ++i) {
+        double v = 0.0;
+        for (int w = 0; w < kPnPWG / 64; ++w) v += red[w][i];
+        if (i < 21) H[i] = v;
+        else if (i < 27) g[i - 21] = v;
+        else cost = v;
+      }
+      double d[6];
+      ok_s = solve6(H, g, lam, d) ? 1 : 0;
+      for (int i = 0; i < 6; ++i) stepd[i] = ok_s ? p[i] + d[i] : p[i];
+      red[0][27] = cost;
+    }
+    __syncthreads();
+    const double cost = red[0][27];
+    // trial cost
+    double pn[6], Rn[9];
+    for (int i = 0; i < 6; ++i) pn[i] = stepd[i];
+    rodrigues(pn, Rn);
+    double cn = 0.0;
+    for (int i = t; i < L; i += kPnPWG) {
+      if (!mask[(size_t)b * cap + i]) continue;
+      double r[2], J[2][6];
+      pnp_residual<false>(pn, Rn, Q + 3 * i, q + 2 * i, K, r, J);
+      cn += r[0] * r[0] + r[1] * r[1];
+    }
+    for (int off = 32; off > 0; off >>= 1) cn += __shfl_down(cn, off, 64);
+    __syncthreads();
+    if (lane == 0) red[wid][0] = cn;
+    __syncthreads();
+    double cns = 0.0;
+    for (int w = 0; w < kPnPWG / 64; ++w) cns += red[w][0];
+    const bool accept = ok_s && cns < cost;
+    __syncthreads();
+    if (accept) {
+      if (t < 6) pose[t] = stepd[t];
+      lam = fmax(lam * 0.1, 1e-12);
+    } else {
+      lam = fmin(lam * 10.0, 1e12);
+    }
+    __syncthreads();
+  }
+  if (t < 3) {
+    rvec[3 * b + t] = pose[t];
+    tvec[3 * b + t] = pose[3 + t];
+  }
+  if (t == 0) ninl[b] = hcnt[bh];
+}
+
+}  // namespace
+
+extern "C" int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int kt_cap,
+                                   const uint8_t* d_desq, const uint8_t* d_dest,
+                                   const int32_t* d_pairs, const int32_t* d_count, int p_cap,
+                                   int batch, double* d_ptq, double* d_ptt, uint8_t* d_dq,
+                                   uint8_t* d_dt, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && p_cap >= 0 && kq_cap >= 0 && kt_cap >= 0,
+               "slam_gather_matches: bad shape");
+  if (batch == 0 || p_cap == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_kpq && d_kpt && d_pairs && d_count && d_ptq && d_ptt,
+               "slam_gather_matches: null pointer");
+  SLAM_REQUIRE((d_dq == nullptr) == (d_dt == nullptr) && (d_dq == nullptr || (d_desq && d_dest)),
+               "slam_gather_matches: descriptor pointers must be all set or all null");
+  dim3 grid((p_cap + kBS - 1) / kBS, batch);
+  k_gather<<<grid, kBS, 0, slam::as_stream(stream)>>>(
+      d_kpq, kq_cap, d_kpt, kt_cap, d_desq, d_dest, reinterpret_cast<const int2*>(d_pairs),
+      d_count, p_cap, d_ptq, d_ptt, d_dq, d_dt);
+  SLAM_LAUNCHED("k_gather");
+  return SLAM_OK;
+}
+
+extern "C" int slam_triangulate(const double* d_ptl, const double* d_ptr, const int32_t* d_count,
+                                int cap, int batch, const double* d_Pl, const double* d_Pr,
+                                int proj_stride, double* d_X, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_triangulate: bad shape");
+  SLAM_REQUIRE(proj_stride == 0 || proj_stride == 12, "slam_triangulate: proj_stride 0 or 12");
+  if (batch == 0 || cap == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_ptl && d_ptr && d_count && d_Pl && d_Pr && d_X, "slam_triangulate: null pointer");
+  dim3 grid((cap + kBS - 1) / kBS, batch);
+  k_triangulate<<<grid, kBS, 0, slam::as_stream(stream)>>>(d_ptl, d_ptr, d_count, cap, d_Pl, d_Pr,
+                                                           proj_stride, d_X);
+  SLAM_LAUNCHED("k_triangulate");
+  return SLAM_OK;
+}
+
+extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count,
+                               int cap, int batch, const double* d_K, uint64_t seed, int item0,
+                               int n_hyp, double reproj_thresh, int hyp_iters, int refine_iters,
+                               double* d_rvec, double* d_tvec, int32_t* d_ninliers,
+                               uint8_t* d_mask, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_pnp_ransac: bad shape");
+  SLAM_REQUIRE(n_hyp >= 1 && n_hyp <= kMaxHyp, "slam_pnp_ransac: n_hyp in [1, %d]", kMaxHyp);
+  SLAM_REQUIRE(hyp_iters >= 0 && refine_iters >= 0 && reproj_thresh > 0,
+               "slam_pnp_ransac: bad iteration/threshold arguments");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_Q && d_q && d_count && d_K && d_rvec && d_tvec && d_ninliers && d_mask,
+               "slam_pnp_ransac: null pointer");
+  k_pnp<<<batch, kPnPWG, 0, slam::as_stream(stream)>>>(d_Q, d_q, d_count, cap, d_K, seed, item0,
+                                                      n_hyp, reproj_thresh, hyp_iters,
+                                                      refine_iters, d_rvec, d_tvec, d_ninliers,
+                                                      d_mask);
+  SLAM_LAUNCHED("k_pnp");
+  return SLAM_OK;
+}

@@ -1,0 +1,64 @@
+"""Device wrappers for gather / triangulation / PnP (csrc/geometry.hip)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .device import ptr, require_gpu, stream_ptr
+
+PNP_DEFAULTS = dict(n_hyp=100, reproj_thresh=8.0, hyp_iters=10, refine_iters=20)
+
+
+def gather_matches(kpq, kpt, pairs, count, desq=None, dest=None, out=None, stream=None):
+    """kp [B,cap,5] f32 + pairs [B,p_cap,2] -> (ptq, ptt [B,p_cap,2] f64, dq, dt [B,p_cap,32])."""
+    B, p_cap, _ = pairs.shape
+    dev = pairs.device
+    if out is None:
+        ptq = torch.zeros((B, p_cap, 2), dtype=torch.float64, device=dev)
+        ptt = torch.zeros((B, p_cap, 2), dtype=torch.float64, device=dev)
+        dq = dt = None
+        if desq is not None:
+            dq = torch.zeros((B, p_cap, 32), dtype=torch.uint8, device=dev)
+            dt = torch.zeros((B, p_cap, 32), dtype=torch.uint8, device=dev)
+    else:
+        ptq, ptt, dq, dt = out
+    _lib.call("slam_gather_matches", ptr(kpq), kpq.shape[1], ptr(kpt), kpt.shape[1], ptr(desq),
+              ptr(dest), ptr(pairs), ptr(count), p_cap, B, ptr(ptq), ptr(ptt), ptr(dq), ptr(dt),
+              stream_ptr(stream))
+    return ptq, ptt, dq, dt
+
+
+def triangulate(ptl, ptr_, count, P_l, P_r, out=None, stream=None):
+    """ptl/ptr [B,cap,2] f64, P 3x4 (shared) or [B,3,4] -> X [B,cap,3] f64."""
+    B, cap, _ = ptl.shape
+    Pl = P_l if isinstance(P_l, torch.Tensor) else torch.as_tensor(np.asarray(P_l, np.float64),
+                                                                   device=ptl.device)
+    Pr = P_r if isinstance(P_r, torch.Tensor) else torch.as_tensor(np.asarray(P_r, np.float64),
+                                                                   device=ptl.device)
+    Pl, Pr = Pl.contiguous(), Pr.contiguous()
+    stride = 12 if Pl.dim() == 3 else 0
+    X = out if out is not None else torch.zeros((B, cap, 3), dtype=torch.float64, device=ptl.device)
+    _lib.call("slam_triangulate", ptr(ptl), ptr(ptr_), ptr(count), cap, B, ptr(Pl), ptr(Pr), stride,
+              ptr(X), stream_ptr(stream))
+    return X
+
+
+def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, **kw):
+    """Q [B,cap,3], q [B,cap,2] f64 -> (rvec [B,3], tvec [B,3], ninliers [B], mask [B,cap])."""
+    prm = dict(PNP_DEFAULTS, **kw)
+    B, cap, _ = Q.shape
+    dev = Q.device
+    Kt = K if isinstance(K, torch.Tensor) else torch.as_tensor(np.asarray(K, np.float64), device=dev)
+    if out is None:
+        rvec = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+        tvec = torch.zeros((B, 3), dtype=torch.float64, device=dev)
+        ninl = torch.zeros((B,), dtype=torch.int32, device=dev)
+        mask = torch.zeros((B, max(cap, 1)), dtype=torch.uint8, device=dev)
+    else:
+        rvec, tvec, ninl, mask = out
+    _lib.call("slam_pnp_ransac", ptr(Q), ptr(q), ptr(count), cap, B, ptr(Kt.contiguous()),
+              int(seed) & ((1 << 64) - 1), int(item0), prm["n_hyp"], float(prm["reproj_thresh"]),
+              prm["hyp_iters"], prm["refine_iters"], ptr(rvec), ptr(tvec), ptr(ninl), ptr(mask),
+              stream_ptr(stream))
+    return rvec, tvec, ninl, mask

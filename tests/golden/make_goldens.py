@@ -197,6 +197,14 @@ def make_matcher_goldens(Point3D, keypoint, tracking):
     q2b, Q1b, q1b = Point3D.find_2D_and_3D_correspondenses(
         dl[:10], pl[:10], kp_i1[:1], des_i1[:1], Q[:10], max_Distance=500)
     out.update(trunc_out_len=np.array([len(q2b), len(Q1b), len(q1b)]))
+    # pure-numpy helpers of Point3D.py (:5-10, :22-30) on the triangulated-point shape
+    Qr = rng.normal(0, 40, (200, 3))
+    pose = np.eye(4)
+    pose[:3, :3] = np.linalg.qr(rng.normal(size=(3, 3)))[0]
+    pose[:3, 3] = rng.normal(0, 5, 3)
+    out.update(abs_in=Qr, abs_pose=pose, abs_out=Point3D.relative_to_abs3DPoints(Qr, pose))
+    close, far = Point3D.sort_3D_points(Qr, 70)
+    out.update(sort_close=np.array(close), sort_far=np.array(far))
     np.savez_compressed(os.path.join(OUT, "matcher_golden.npz"), **out)
     return {k: np.shape(v) for k, v in out.items()}
 
