@@ -97,6 +97,29 @@ int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int 
                         const int32_t* d_count, int p_cap, int batch, double* d_ptq,
                         double* d_ptt, uint8_t* d_dq, uint8_t* d_dt, void* stream);
 
+/* 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:214-216):
+ * for k < count[b], (qi, ti) = pairs[b][k]: Q1[b][k] = X[b][qi], q1[b][k] =
+ * ptl[b][qi], q2[b][k] = (double)kp_next[b][ti].xy.  X [batch][xcap][3],
+ * ptl [batch][xcap][2] f64; kp_next [batch][kcap][5] f32. */
+int slam_gather_temporal(const double* d_X, const double* d_ptl, int xcap, const float* d_kp_next,
+                         int kcap, const int32_t* d_pairs, const int32_t* d_count, int pcap,
+                         int batch, double* d_Q1, double* d_q2, double* d_q1, void* stream);
+
+/* cv2.findFundamentalMat(pts_left, pts_right, FM_LMEDS) mask (keypoint.py:102-109),
+ * deterministic LMedS restated in oracle/fundamental.c: n_hyp seeded 7-point
+ * hypotheses (300 = OpenCV's LMeDS count at confidence 0.99), min median of
+ * the symmetric epipolar error, inliers err <= sigma^2 with OpenCV's robust
+ * sigma.  d_m1/d_m2 [batch][cap][2] f64; d_mask [batch][cap] u8; d_F
+ * [batch][9] (unit Frobenius norm); d_ninliers [batch] (-1: < 8 points / no model). */
+int slam_fundamental_lmeds(const double* d_m1, const double* d_m2, const int32_t* d_count,
+                           int cap, int batch, uint64_t seed, int item0, int n_hyp,
+                           uint8_t* d_mask, double* d_F, int32_t* d_ninliers, void* stream);
+
+/* Order-preserving compaction of pairs[b][k] (k < count[b]) where mask[b][k] != 0
+ * (the `pts_left[mask]` of keypoint.py:106-109). d_out must not alias d_pairs. */
+int slam_filter_pairs(const int32_t* d_pairs, const int32_t* d_count, const uint8_t* d_mask,
+                      int cap, int batch, int32_t* d_out, int32_t* d_out_count, void* stream);
+
 /* cv2.triangulatePoints + dehomogenisation (Point3D.py:14-19): per point the
  * null vector of the 4x4 DLT system (rows x*P[2]-P[0], y*P[2]-P[1] of both
  * views), one-sided Jacobi SVD in f64.  d_ptl/d_ptr [batch][cap][2] f64,

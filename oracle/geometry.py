@@ -73,6 +73,31 @@ def pose_matrix_from_pnp(rvec, tvec):
 
 
 _PNP = None
+_FM = None
+
+
+def _fm_fn():
+    global _FM
+    if _FM is None:
+        f = lib().oracle_fm_lmeds
+        p, i = ctypes.c_void_p, ctypes.c_int
+        f.argtypes = [p, p, i, ctypes.c_uint64, i, i, p, p, p]
+        f.restype = ctypes.c_int
+        _FM = f
+    return _FM
+
+
+def fundamental_lmeds(m1, m2, seed=0, item=0, n_hyp=300):
+    """Seeded LMedS F (oracle/fundamental.c) -> (mask [M] bool, F 3x3, n_inliers, median)."""
+    m1 = np.ascontiguousarray(m1, np.float64).reshape(-1, 2)
+    m2 = np.ascontiguousarray(m2, np.float64).reshape(-1, 2)
+    M = len(m1)
+    mask = np.zeros(max(M, 1), np.uint8)
+    F = np.zeros(9)
+    med = np.zeros(1, np.float32)
+    n = _fm_fn()(_ptr(m1), _ptr(m2), M, seed & ((1 << 64) - 1), item, n_hyp, _ptr(mask), _ptr(F),
+                 _ptr(med))
+    return mask[:M].astype(bool), F.reshape(3, 3), n, float(med[0])
 
 
 def _pnp_fn():

@@ -1,0 +1,443 @@
+// Fundamental-matrix LMedS outlier mask for gfx950, batched over frame pairs.
+//
+// Replaces cv2.findFundamentalMat(pts_left, pts_right, cv2.FM_LMEDS) and the
+// mask application of /root/reference/keypoint.py:102-109, following the
+// deterministic spec of oracle/fundamental.c (300 seeded 7-point hypotheses,
+// Hartley-normalised Gauss-Jordan null space, cubic roots, float errors,
+// min-median selection, OpenCV's robust sigma for the final inlier mask).
+//
+// One workgroup (8 waves) per frame pair:
+//   phase 1: one hypothesis per lane -> up to 3 candidate F in LDS;
+//   phase 2: wave w owns hypotheses h = w mod 8.  Per candidate the wave counts
+//            errors below its best median so far (exact reject: the median
+//            improves iff more than M/2 errors are below it); only improving
+//            candidates pay an exact radix-select median (4 x 8-bit passes,
+//            errors recomputed per pass instead of stored);
+//   phase 3: merge the 8 wave bests (min median, lowest candidate index);
+//   phase 4: inlier mask of the winner.
+#include "common.hpp"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kWG = 512;
+constexpr int kWaves = kWG / 64;
+constexpr int kMaxHyp = 512;
+constexpr int kS = 7;
+
+__device__ inline uint64_t splitmix64(uint64_t& s) {
+  s += 0x9E3779B97F4A7C15ull;
+  uint64_t z = s;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ inline double det3(const double* F) {
+  return F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) +
+         F[2] * (F[3] * F[7] - F[4] * F[6]);
+}
+
+__device__ inline double detmix(const double* F1, const double* F2, double a) {
+  double F[9];
+  for (int i = 0; i < 9; ++i) F[i] = a * F1[i] + (1.0 - a) * F2[i];
+  return det3(F);
+}
+
+__device__ int cubic_roots(double c3, double c2, double c1, double c0, double* r) {
+  const double mx = fmax(fmax(fabs(c3), fabs(c2)), fmax(fabs(c1), fabs(c0)));
+  if (mx == 0.0) return 0;
+  int n = 0;
+  if (fabs(c3) <= 1e-12 * mx) {
+    if (fabs(c2) <= 1e-12 * mx) {
+      if (fabs(c1) <= 1e-12 * mx) return 0;
+      r[0] = -c0 / c1;
+      return 1;
+    }
+    const double d = c1 * c1 - 4.0 * c2 * c0;
+    if (d < 0) return 0;
+    const double sq = sqrt(d);
+    const double q = -0.5 * (c1 + (c1 >= 0 ? sq : -sq));
+    r[n++] = q / c2;
+    if (q != 0.0) r[n++] = c0 / q;
+  } else {
+    const double a = c2 / c3, b = c1 / c3, c = c0 / c3;
+    const double p = b - a * a / 3.0;
+    const double q = 2.0 * a * a * a / 27.0 - a * b / 3.0 + c;
+    const double disc = q * q / 4.0 + p * p * p / 27.0;
+    if (disc > 0) {
+      const double sd = sqrt(disc);
+      const double u = cbrt(-q / 2.0 + sd), v = cbrt(-q / 2.0 - sd);
+      r[n++] = u + v - a / 3.0;
+    } else {
+      const double rr = sqrt(fmax(-p / 3.0, 0.0));
+      double ca = rr > 0 ? -q / (2.0 * rr * rr * rr) : 0.0;
+      ca = fmin(fmax(ca, -1.0), 1.0);
+      const double phi = acos(ca);
+      for (int k = 0; k < 3; ++k)
+        r[n++] = 2.0 * rr * cos((phi + 2.0 * 3.14159265358979323846 * k) / 3.0) - a / 3.0;
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    for (int it = 0; it < 2; ++it) {
+      const double x = r[i];
+      const double f = ((c3 * x + c2) * x + c1) * x + c0;
+      const double df = (3.0 * c3 * x + 2.0 * c2) * x + c1;
+      if (df != 0.0) r[i] = x - f / df;
+    }
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && r[j] < r[j - 1]; --j) {
+      const double t = r[j];
+      r[j] = r[j - 1];
+      r[j - 1] = t;
+    }
+  return n;
+}
+
+__device__ int seven_point(const double* m1, const double* m2, const int* idx, double* Fout) {
+  double c1x = 0, c1y = 0, c2x = 0, c2y = 0;
+  for (int i = 0; i < kS; ++i) {
+    c1x += m1[2 * idx[i]]; c1y += m1[2 * idx[i] + 1];
+    c2x += m2[2 * idx[i]]; c2y += m2[2 * idx[i] + 1];
+  }
+  c1x /= kS; c1y /= kS; c2x /= kS; c2y /= kS;
+  double d1 = 0, d2 = 0;
+  for (int i = 0; i < kS; ++i) {
+    d1 += sqrt((m1[2 * idx[i]] - c1x) * (m1[2 * idx[i]] - c1x) +
+               (m1[2 * idx[i] + 1] - c1y) * (m1[2 * idx[i] + 1] - c1y));
+    d2 += sqrt((m2[2 * idx[i]] - c2x) * (m2[2 * idx[i]] - c2x) +
+               (m2[2 * idx[i] + 1] - c2y) * (m2[2 * idx[i] + 1] - c2y));
+  }
+  d1 /= kS; d2 /= kS;
+  if (!(d1 > 1e-12) || !(d2 > 1e-12)) return 0;
+  const double s1 = sqrt(2.0) / d1, s2 = sqrt(2.0) / d2;
+  double A[7][9];
+  for (int i = 0; i < kS; ++i) {
+    const double x1 = (m1[2 * idx[i]] - c1x) * s1, y1 = (m1[2 * idx[i] + 1] - c1y) * s1;
+    const double x2 = (m2[2 * idx[i]] - c2x) * s2, y2 = (m2[2 * idx[i] + 1] - c2y) * s2;
+    A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
+    A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
+    A[i][6] = x1; A[i][7] = y1; A[i][8] = 1.0;
+  }
+  int pc[7], used[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = 0; r < 7; ++r) {
+    int bi = -1, bj = -1;
+    double bv = 0.0;
+    for (int i = r; i < 7; ++i)
+      for (int j = 0; j < 9; ++j)
+        if (!used[j] && fabs(A[i][j]) > bv) {
+          bv = fabs(A[i][j]);
+          bi = i;
+          bj = j;
+        }
+    if (bv < 1e-10) return 0;
+    if (bi != r)
+      for (int j = 0; j < 9; ++j) {
+        const double t = A[r][j];
+        A[r][j] = A[bi][j];
+        A[bi][j] = t;
+      }
+    used[bj] = 1;
+    pc[r] = bj;
+    const double inv = 1.0 / A[r][bj];
+    for (int j = 0; j < 9; ++j) A[r][j] *= inv;
+    for (int i = 0; i < 7; ++i) {
+      if (i == r) continue;
+      const double f = A[i][bj];
+      if (f != 0.0)
+        for (int j = 0; j < 9; ++j) A[i][j] -= f * A[r][j];
+    }
+  }
+  int fr[2], nf = 0;
+  for (int j = 0; j < 9; ++j)
+    if (!used[j] && nf < 2) fr[nf++] = j;
+  double F1[9], F2[9];
+  for (int k = 0; k < 2; ++k) {
+    double* f = k ? F2 : F1;
+    for (int j = 0; j < 9; ++j) f[j] = 0.0;
+    f[fr[k]] = 1.0;
+    for (int r = 0; r < 7; ++r) f[pc[r]] = -A[r][fr[k]];
+  }
+  const double v0 = detmix(F1, F2, 0.0), v1 = detmix(F1, F2, 1.0);
+  const double vm = detmix(F1, F2, -1.0), v2 = detmix(F1, F2, 2.0);
+  const double cc0 = v0;
+  const double cc2 = (v1 + vm) / 2.0 - cc0;
+  const double s = (v1 - vm) / 2.0;
+  const double u = v2 - 4.0 * cc2 - cc0;
+  const double cc3 = (u - 2.0 * s) / 6.0;
+  const double cc1 = s - cc3;
+  double roots[3];
+  const int nr = cubic_roots(cc3, cc2, cc1, cc0, roots);
+  const double T1[9] = {s1, 0, -s1 * c1x, 0, s1, -s1 * c1y, 0, 0, 1};
+  const double T2[9] = {s2, 0, -s2 * c2x, 0, s2, -s2 * c2y, 0, 0, 1};
+  int n = 0;
+  for (int k = 0; k < nr; ++k) {
+    double Fn[9], tmp[9], F[9];
+    for (int i = 0; i < 9; ++i) Fn[i] = roots[k] * F1[i] + (1.0 - roots[k]) * F2[i];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        tmp[3 * i + j] = Fn[3 * i] * T1[j] + Fn[3 * i + 1] * T1[3 + j] + Fn[3 * i + 2] * T1[6 + j];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        F[3 * i + j] = T2[i] * tmp[j] + T2[3 + i] * tmp[3 + j] + T2[6 + i] * tmp[6 + j];
+    double nrm = 0.0;
+    for (int i = 0; i < 9; ++i) nrm += F[i] * F[i];
+    nrm = sqrt(nrm);
+    if (!(nrm > 0.0) || !isfinite(nrm)) continue;
+    for (int i = 0; i < 9; ++i) Fout[9 * n + i] = F[i] / nrm;
+    ++n;
+  }
+  return n;
+}
+
+__device__ __forceinline__ float fm_error(const double* F, const double* p1, const double* p2) {
+  double a = F[0] * p1[0] + F[1] * p1[1] + F[2];
+  double b = F[3] * p1[0] + F[4] * p1[1] + F[5];
+  double c = F[6] * p1[0] + F[7] * p1[1] + F[8];
+  const double s2 = 1.0 / (a * a + b * b);
+  const double d2 = p2[0] * a + p2[1] * b + c;
+  a = F[0] * p2[0] + F[3] * p2[1] + F[6];
+  b = F[1] * p2[0] + F[4] * p2[1] + F[7];
+  c = F[2] * p2[0] + F[5] * p2[1] + F[8];
+  const double s1 = 1.0 / (a * a + b * b);
+  const double d1 = p1[0] * a + p1[1] * b + c;
+  const float e = (float)fmax(d1 * d1 * s1, d2 * d2 * s2);
+  return isnan(e) ? INFINITY : e;
+}
+
+__global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1all,
+                                                  const double* __restrict__ m2all,
+                                                  const int32_t* __restrict__ count, int cap,
+                                                  uint64_t seed, int item0, int n_hyp,
+                                                  uint8_t* __restrict__ mask,
+                                                  double* __restrict__ Fout,
+                                                  int32_t* __restrict__ ninl) {
+  __shared__ double cand[kMaxHyp / 2][3][9];  // hypotheses processed in rounds of 256
+  __shared__ int ncand[kMaxHyp / 2];
+  __shared__ int hist[kWaves][256];
+  __shared__ float wbest[kWaves];
+  __shared__ int wbidx[kWaves];
+  __shared__ double Fb[9];
+  __shared__ float best_s;
+  __shared__ int found_s, cnt_s;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  const int M = min(max(count[b], 0), cap);
+  const double* m1 = m1all + (size_t)b * cap * 2;
+  const double* m2 = m2all + (size_t)b * cap * 2;
+  uint8_t* mk = mask + (size_t)b * cap;
+  if (M < 8) {
+    for (int i = t; i < M; i += kWG) mk[i] = 0;
+    if (t == 0) ninl[b] = -1;
+    return;
+  }
+  float my_best = INFINITY;
+  int my_idx = 0x7FFFFFFF;
+  const int need = M / 2 + 1;  // #errors below a value for the median to be below it
+  for (int h0 = 0; h0 < n_hyp; h0 += kMaxHyp / 2) {
+    const int nh = min(kMaxHyp / 2, n_hyp - h0);
+    __syncthreads();
+    if (t < nh) {
+      const int h = h0 + t;
+      uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+                   ((uint64_t)h * 0x9FB21C651E98DF25ull);
+      int idx[kS];
+      for (int k = 0; k < kS; ++k) {
+        int v;
+        bool dup;
+        do {
+          v = (int)((splitmix64(s) >> 32) % (uint64_t)M);
+          dup = false;
+          for (int j = 0; j < k; ++j) dup |= idx[j] == v;
+        } while (dup);
+        idx[k] = v;
+      }
+      double F[27];
+      const int nc = seven_point(m1, m2, idx, F);
+      for (int k = 0; k < nc; ++k)
+        for (int i = 0; i < 9; ++i) cand[t][k][i] = F[9 * k + i];
+      ncand[t] = nc;
+    }
+    __syncthreads();
+    for (int hl = w; hl < nh; hl += kWaves) {
+      for (int k = 0; k < ncand[hl]; ++k) {
+        const double* F = cand[hl][k];
+        int below = 0;
+        for (int i = lane; i < M; i += 64)
+          below += fm_error(F, m1 + 2 * i, m2 + 2 * i) < my_best ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) below += __shfl_xor(below, off, 64);
+        if (below < need) continue;  // median >= my_best: cannot improve (uniform)
+        // exact median = (M/2)-th smallest error, radix select on the float bits
+        uint32_t prefix = 0, pmask = 0;
+        int krank = M / 2;
+        for (int shift = 24; shift >= 0; shift -= 8) {
+          for (int j = lane; j < 256; j += 64) hist[w][j] = 0;
+          __builtin_amdgcn_wave_barrier();
+          for (int i = lane; i < M; i += 64) {
+            const uint32_t bits = __float_as_uint(fm_error(F, m1 + 2 * i, m2 + 2 * i));
+            if ((bits & pmask) == prefix) atomicAdd(&hist[w][(bits >> shift) & 255u], 1);
+          }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_s_waitcnt(0xC07F);
+          // prefix sums over 256 bins, 4 per lane
+          const int c0 = hist[w][4 * lane], c1 = hist[w][4 * lane + 1];
+          const int c2 = hist[w][4 * lane + 2], c3 = hist[w][4 * lane + 3];
+          const int sm = c0 + c1 + c2 + c3;
+          int inc = sm;
+          for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+          }
+          const int exc = inc - sm;
+          int bin = -1, before = 0;
+          if (krank >= exc && krank < inc) {
+            int acc = exc;
+            if (krank < acc + c0) { bin = 4 * lane; before = acc; }
+            else if (krank < acc + c0 + c1) { bin = 4 * lane + 1; before = acc + c0; }
+            else if (krank < acc + c0 + c1 + c2) { bin = 4 * lane + 2; before = acc + c0 + c1; }
+            else { bin = 4 * lane + 3; before = acc + c0 + c1 + c2; }
+          }
+          const unsigned long long bal = __ballot(bin >= 0);
+          const int src = __ffsll((long long)bal) - 1;
+          bin = __shfl(bin, src, 64);
+          before = __shfl(before, src, 64);
+          krank -= before;
+          prefix |= (uint32_t)bin << shift;
+          pmask |= 255u << shift;
+        }
+        const float med = __uint_as_float(prefix);
+        if (med < my_best) {
+          my_best = med;
+          my_idx = (h0 + hl) * 3 + k;
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+    wbest[w] = my_best;
+    wbidx[w] = my_idx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    float bm = INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int i = 0; i < kWaves; ++i)
+      if (wbest[i] < bm || (wbest[i] == bm && wbidx[i] < bi)) {
+        bm = wbest[i];
+        bi = wbidx[i];
+      }
+    best_s = bm;
+    found_s = bi != 0x7FFFFFFF && bm < INFINITY;
+    cnt_s = 0;
+    if (found_s) {
+      // recompute the winner (its hypothesis round is gone from LDS)
+      const int h = bi / 3, k = bi % 3;
+      uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+                   ((uint64_t)h * 0x9FB21C651E98DF25ull);
+      int idx[kS];
+      for (int kk = 0; kk < kS; ++kk) {
+        int v;
+        bool dup;
+        do {
+          v = (int)((splitmix64(s) >> 32) % (uint64_t)M);
+          dup = false;
+          for (int j = 0; j < kk; ++j) dup |= idx[j] == v;
+        } while (dup);
+        idx[kk] = v;
+      }
+      double F[27];
+      seven_point(m1, m2, idx, F);
+      for (int i = 0; i < 9; ++i) Fb[i] = F[9 * k + i];
+    }
+  }
+  __syncthreads();
+  if (!found_s) {
+    for (int i = t; i < M; i += kWG) mk[i] = 0;
+    if (t == 0) ninl[b] = -1;
+    return;
+  }
+  double sigma = 2.5 * 1.4826 * (1 + 5.0 / (M - kS)) * sqrt((double)best_s);
+  sigma = fmax(sigma, 0.001);
+  const double thr = sigma * sigma;
+  double F[9];
+  for (int i = 0; i < 9; ++i) F[i] = Fb[i];
+  int c = 0;
+  for (int i = t; i < M; i += kWG) {
+    const uint8_t in = (double)fm_error(F, m1 + 2 * i, m2 + 2 * i) <= thr ? 1 : 0;
+    mk[i] = in;
+    c += in;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if (lane == 0) atomicAdd(&cnt_s, c);
+  __syncthreads();
+  if (t < 9) Fout[9 * b + t] = F[t];
+  if (t == 0) ninl[b] = cnt_s;
+}
+
+// Order-preserving compaction of pairs[b][k] (k < count[b]) by mask[b][k].
+constexpr int kCWG = 1024;
+__global__ __launch_bounds__(kCWG) void k_filter_pairs(const int2* __restrict__ pairs,
+                                                       const int32_t* __restrict__ count,
+                                                       const uint8_t* __restrict__ mask, int cap,
+                                                       int2* __restrict__ out,
+                                                       int32_t* __restrict__ out_count) {
+  __shared__ int wave_tot[kCWG / 64];
+  __shared__ int carry;
+  const int b = blockIdx.x;
+  const int n = min(max(count[b], 0), cap);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += kCWG) {
+    const int k = base + threadIdx.x;
+    const bool keep = k < n && mask[(size_t)b * cap + k] != 0;
+    const unsigned long long m = __ballot(keep);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wid] = __popcll(m);
+    __syncthreads();
+    int off = carry;
+    for (int i = 0; i < wid; ++i) off += wave_tot[i];
+    if (keep) out[(size_t)b * cap + off + before] = pairs[(size_t)b * cap + k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int i = 0; i < kCWG / 64; ++i) tot += wave_tot[i];
+      carry += tot;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out_count[b] = carry;
+}
+
+}  // namespace
+
+extern "C" int slam_fundamental_lmeds(const double* d_m1, const double* d_m2,
+                                      const int32_t* d_count, int cap, int batch, uint64_t seed,
+                                      int item0, int n_hyp, uint8_t* d_mask, double* d_F,
+                                      int32_t* d_ninliers, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_fundamental_lmeds: bad shape");
+  SLAM_REQUIRE(n_hyp >= 1 && n_hyp <= 4096, "slam_fundamental_lmeds: n_hyp in [1, 4096]");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_m1 && d_m2 && d_count && d_mask && d_F && d_ninliers,
+               "slam_fundamental_lmeds: null pointer");
+  k_fm_lmeds<<<batch, kWG, 0, slam::as_stream(stream)>>>(d_m1, d_m2, d_count, cap, seed, item0,
+                                                         n_hyp, d_mask, d_F, d_ninliers);
+  SLAM_LAUNCHED("k_fm_lmeds");
+  return SLAM_OK;
+}
+
+extern "C" int slam_filter_pairs(const int32_t* d_pairs, const int32_t* d_count,
+                                 const uint8_t* d_mask, int cap, int batch, int32_t* d_out,
+                                 int32_t* d_out_count, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_filter_pairs: bad shape");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_pairs && d_count && d_mask && d_out && d_out_count,
+               "slam_filter_pairs: null pointer");
+  SLAM_REQUIRE(d_out != d_pairs, "slam_filter_pairs: in-place filtering is not supported");
+  k_filter_pairs<<<batch, kCWG, 0, slam::as_stream(stream)>>>(
+      reinterpret_cast<const int2*>(d_pairs), d_count, d_mask, cap, reinterpret_cast<int2*>(d_out),
+      d_out_count);
+  SLAM_LAUNCHED("k_filter_pairs");
+  return SLAM_OK;
+}

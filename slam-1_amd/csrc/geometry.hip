@@ -50,6 +50,30 @@ __global__ __launch_bounds__(kBS) void k_gather(const float* __restrict__ kpq, i
   }
 }
 
+// 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:214-216):
+// Q1 = X[qi], q1 = ptl[qi] (tracked left points at t), q2 = kp_next[ti].xy.
+__global__ __launch_bounds__(kBS) void k_gather_temporal(
+    const double* __restrict__ X, const double* __restrict__ ptl, int xcap,
+    const float* __restrict__ kpn, int kcap, const int2* __restrict__ pairs,
+    const int32_t* __restrict__ count, int pcap, double* __restrict__ Q1,
+    double* __restrict__ q2, double* __restrict__ q1) {
+  const int b = blockIdx.y;
+  const int n = min(max(count[b], 0), pcap);
+  const int k = blockIdx.x * kBS + threadIdx.x;
+  if (k >= n) return;
+  const size_t o = (size_t)b * pcap + k;
+  const int2 pr = pairs[o];
+  const size_t xi = (size_t)b * xcap + pr.x;
+  Q1[3 * o] = X[3 * xi];
+  Q1[3 * o + 1] = X[3 * xi + 1];
+  Q1[3 * o + 2] = X[3 * xi + 2];
+  q1[2 * o] = ptl[2 * xi];
+  q1[2 * o + 1] = ptl[2 * xi + 1];
+  const float* c = kpn + ((size_t)b * kcap + pr.y) * 5;
+  q2[2 * o] = (double)c[0];
+  q2[2 * o + 1] = (double)c[1];
+}
+
 // --------------------------------------------------------------- triangulation
 // Null vector of the 4x4 DLT matrix by one-sided (Hestenes) Jacobi SVD in f64.
 __device__ void null_vector4(double A[4][4], double v[4]) {
@@ -475,6 +499,23 @@ extern "C" int slam_gather_matches(const float* d_kpq, int kq_cap, const float* 
       d_kpq, kq_cap, d_kpt, kt_cap, d_desq, d_dest, reinterpret_cast<const int2*>(d_pairs),
       d_count, p_cap, d_ptq, d_ptt, d_dq, d_dt);
   SLAM_LAUNCHED("k_gather");
+  return SLAM_OK;
+}
+
+extern "C" int slam_gather_temporal(const double* d_X, const double* d_ptl, int xcap,
+                                    const float* d_kp_next, int kcap, const int32_t* d_pairs,
+                                    const int32_t* d_count, int pcap, int batch, double* d_Q1,
+                                    double* d_q2, double* d_q1, void* stream) {
+  SLAM_REQUIRE(batch >= 0 && pcap >= 0 && xcap >= 0 && kcap >= 0,
+               "slam_gather_temporal: bad shape");
+  if (batch == 0 || pcap == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_X && d_ptl && d_kp_next && d_pairs && d_count && d_Q1 && d_q2 && d_q1,
+               "slam_gather_temporal: null pointer");
+  dim3 grid((pcap + kBS - 1) / kBS, batch);
+  k_gather_temporal<<<grid, kBS, 0, slam::as_stream(stream)>>>(
+      d_X, d_ptl, xcap, d_kp_next, kcap, reinterpret_cast<const int2*>(d_pairs), d_count, pcap,
+      d_Q1, d_q2, d_q1);
+  SLAM_LAUNCHED("k_gather_temporal");
   return SLAM_OK;
 }
 

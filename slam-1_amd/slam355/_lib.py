@@ -52,9 +52,14 @@ SIGNATURES = {
                        c_size_t, c_p, c_p, c_p, c_p, c_int, c_p],
     "slam_gather_matches": [c_p, c_int, c_p, c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p,
                             c_p, c_p, c_p],
+    "slam_gather_temporal": [c_p, c_p, c_int, c_p, c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p,
+                             c_p],
     "slam_triangulate": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "slam_pnp_ransac": [c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int, c_double, c_int,
                         c_int, c_p, c_p, c_p, c_p, c_p],
+    "slam_fundamental_lmeds": [c_p, c_p, c_p, c_int, c_int, c_uint64, c_int, c_int, c_p, c_p, c_p,
+                               c_p],
+    "slam_filter_pairs": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_ba_residual": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p],
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_ba_red_slots": [c_int, c_int],

@@ -29,6 +29,50 @@ def gather_matches(kpq, kpt, pairs, count, desq=None, dest=None, out=None, strea
     return ptq, ptt, dq, dt
 
 
+def gather_temporal(X, ptl, kp_next, pairs, count, out=None, stream=None):
+    """-> (Q1 [B,p,3], q2 [B,p,2], q1 [B,p,2]) f64 (Point3D.py:214-216)."""
+    B, pcap, _ = pairs.shape
+    dev = pairs.device
+    if out is None:
+        Q1 = torch.zeros((B, pcap, 3), dtype=torch.float64, device=dev)
+        q2 = torch.zeros((B, pcap, 2), dtype=torch.float64, device=dev)
+        q1 = torch.zeros((B, pcap, 2), dtype=torch.float64, device=dev)
+    else:
+        Q1, q2, q1 = out
+    _lib.call("slam_gather_temporal", ptr(X), ptr(ptl), X.shape[1], ptr(kp_next), kp_next.shape[1],
+              ptr(pairs), ptr(count), pcap, B, ptr(Q1), ptr(q2), ptr(q1), stream_ptr(stream))
+    return Q1, q2, q1
+
+
+def fundamental_lmeds(m1, m2, count, seed=0, item0=0, n_hyp=300, out=None, stream=None):
+    """m1/m2 [B,cap,2] f64 -> (mask [B,cap] u8, F [B,9] f64, ninliers [B] i32)."""
+    B, cap, _ = m1.shape
+    dev = m1.device
+    if out is None:
+        mask = torch.zeros((B, max(cap, 1)), dtype=torch.uint8, device=dev)
+        F = torch.zeros((B, 9), dtype=torch.float64, device=dev)
+        ninl = torch.zeros((B,), dtype=torch.int32, device=dev)
+    else:
+        mask, F, ninl = out
+    _lib.call("slam_fundamental_lmeds", ptr(m1), ptr(m2), ptr(count), cap, B,
+              int(seed) & ((1 << 64) - 1), int(item0), int(n_hyp), ptr(mask), ptr(F), ptr(ninl),
+              stream_ptr(stream))
+    return mask, F, ninl
+
+
+def filter_pairs(pairs, count, mask, out=None, stream=None):
+    """Keep pairs[b][k] with mask[b][k] (order preserved) -> (pairs', count')."""
+    B, cap, _ = pairs.shape
+    if out is None:
+        o = torch.empty_like(pairs)
+        oc = torch.empty((B,), dtype=torch.int32, device=pairs.device)
+    else:
+        o, oc = out
+    _lib.call("slam_filter_pairs", ptr(pairs), ptr(count), ptr(mask), cap, B, ptr(o), ptr(oc),
+              stream_ptr(stream))
+    return o, oc
+
+
 def triangulate(ptl, ptr_, count, P_l, P_r, out=None, stream=None):
     """ptl/ptr [B,cap,2] f64, P 3x4 (shared) or [B,3,4] -> X [B,cap,3] f64."""
     B, cap, _ = ptl.shape

@@ -1,0 +1,148 @@
+"""Batched stereo tracking on the GPU — the per-frame loop of
+/root/reference/main.py:76-132 restructured for MI355X.
+
+The reference processes one frame pair per Python iteration:
+  ORB(right_i), ORB(left_{i+1})                       main.py:79-80
+  stereo kNN-2 + ratio + F-LMedS mask                 main.py:82-84 (keypoint.py:78-109)
+  triangulate                                         main.py:86 (Point3D.py:14-19)
+  temporal kNN-2 + ratio + |Q| gate                   main.py:88-90 (Point3D.py:33-54)
+  PnP-RANSAC, sign flip, pose chaining                main.py:94-98, 120-124
+Every step depends only on frames (i, i+1), so `Tracker.track` runs B frame
+pairs per call as 13 kernel launches on one stream, with all intermediate
+data resident in HBM; only the B relative poses (and counters) come back to
+the host for the sequential 4x4 pose chain.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import geometry, matcher, orb
+from .device import require_gpu
+
+
+class Tracker:
+    """Device buffers for batches of B frame pairs of H x W images."""
+
+    def __init__(self, B, H, W, P_l, P_r, max_kp_per_tile=56, seed=0, max_distance=500.0,
+                 stream=None):
+        self.dev = require_gpu()
+        self.B, self.H, self.W = B, H, W
+        self.max_kp = max_kp_per_tile
+        self.seed = seed
+        self.max_distance = float(max_distance)
+        self.stream = stream
+        self.P_l = np.asarray(P_l, np.float64)
+        self.P_r = np.asarray(P_r, np.float64)
+        self.K = self.P_l[:3, :3].copy()
+        d = self.dev
+        self.tPl = torch.as_tensor(self.P_l, device=d).contiguous()
+        self.tPr = torch.as_tensor(self.P_r, device=d).contiguous()
+        self.tK = torch.as_tensor(self.K, device=d).contiguous()
+        # ORB on 2B+1 images: left_0..left_B then right_0..right_{B-1}
+        self.ows = orb.OrbWorkspace(2 * B + 1, H, W, max_kp_per_tile)
+        cap = self.cap = self.ows.kp_cap
+        i32 = dict(dtype=torch.int32, device=d)
+        f64 = dict(dtype=torch.float64, device=d)
+        u8 = dict(dtype=torch.uint8, device=d)
+        self.s_idx2 = torch.full((B, cap, 2), -1, **i32)
+        self.s_dist2 = torch.full((B, cap, 2), -1, **i32)
+        self.s_good = torch.zeros((B, cap), **u8)
+        self.s_pairs = torch.zeros((B, cap, 2), **i32)
+        self.s_cnt = torch.zeros((B,), **i32)
+        self.s_ptl = torch.zeros((B, cap, 2), **f64)
+        self.s_ptr = torch.zeros((B, cap, 2), **f64)
+        self.f_mask = torch.zeros((B, cap), **u8)
+        self.f_F = torch.zeros((B, 9), **f64)
+        self.f_ninl = torch.zeros((B,), **i32)
+        self.f_pairs = torch.zeros((B, cap, 2), **i32)
+        self.f_cnt = torch.zeros((B,), **i32)
+        self.f_ptl = torch.zeros((B, cap, 2), **f64)
+        self.f_ptr = torch.zeros((B, cap, 2), **f64)
+        self.f_dl = torch.zeros((B, cap, 32), **u8)
+        self.f_dr = torch.zeros((B, cap, 32), **u8)
+        self.X = torch.zeros((B, cap, 3), **f64)
+        self.t_idx2 = torch.full((B, cap, 2), -1, **i32)
+        self.t_dist2 = torch.full((B, cap, 2), -1, **i32)
+        self.t_good = torch.zeros((B, cap), **u8)
+        self.t_pairs = torch.zeros((B, cap, 2), **i32)
+        self.t_cnt = torch.zeros((B,), **i32)
+        self.Q1 = torch.zeros((B, cap, 3), **f64)
+        self.q2 = torch.zeros((B, cap, 2), **f64)
+        self.q1 = torch.zeros((B, cap, 2), **f64)
+        self.rvec = torch.zeros((B, 3), **f64)
+        self.tvec = torch.zeros((B, 3), **f64)
+        self.p_ninl = torch.zeros((B,), **i32)
+        self.p_mask = torch.zeros((B, cap), **u8)
+        self.imgs = torch.zeros((2 * B + 1, H, W), **u8)
+
+    # ------------------------------------------------------------------ device step
+    def track(self, frame0: int, imgs: torch.Tensor | None = None):
+        """Run the B frame pairs (frame0 + b, frame0 + b + 1), b < B, on device.
+
+        `imgs` [2B+1, H, W] u8 = left_{frame0..frame0+B}, right_{frame0..frame0+B-1}
+        (defaults to self.imgs, filled by the caller).  Asynchronous: returns
+        device tensors (rvec, tvec, n_inliers)."""
+        B, st = self.B, self.stream
+        im = self.imgs if imgs is None else imgs
+        kp, octv, desc, cnt = self.ows.run(im, st)
+        kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
+        dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
+        nL, nR = cnt[0:B], cnt[B + 1:2 * B + 1]
+        kpL1, dL1, nL1 = kp[1:B + 1], desc[1:B + 1], cnt[1:B + 1]
+        # stereo: kNN-2 + ratio (keypoint.py:87-94), gather (:96-97)
+        matcher.knn2_batch(dL, nL, dR, nR, out=(self.s_idx2, self.s_dist2, self.s_good), stream=st)
+        matcher.compact_matches(self.s_idx2, self.s_good, nL, out=(self.s_pairs, self.s_cnt),
+                                stream=st)
+        geometry.gather_matches(kpL, kpR, self.s_pairs, self.s_cnt,
+                                out=(self.s_ptl, self.s_ptr, None, None), stream=st)
+        # F-LMedS mask (keypoint.py:102-109), then the surviving pairs with descriptors
+        geometry.fundamental_lmeds(self.s_ptl, self.s_ptr, self.s_cnt, seed=self.seed,
+                                   item0=frame0, out=(self.f_mask, self.f_F, self.f_ninl),
+                                   stream=st)
+        geometry.filter_pairs(self.s_pairs, self.s_cnt, self.f_mask,
+                              out=(self.f_pairs, self.f_cnt), stream=st)
+        geometry.gather_matches(kpL, kpR, self.f_pairs, self.f_cnt, dL, dR,
+                                out=(self.f_ptl, self.f_ptr, self.f_dl, self.f_dr), stream=st)
+        # triangulate (Point3D.py:14-19)
+        geometry.triangulate(self.f_ptl, self.f_ptr, self.f_cnt, self.tPl, self.tPr, out=self.X,
+                             stream=st)
+        # temporal: tracked left descriptors at t vs left at t+1, ratio + |Q| gate
+        matcher.knn2_batch(self.f_dl, self.f_cnt, dL1, nL1,
+                           out=(self.t_idx2, self.t_dist2, self.t_good), stream=st)
+        matcher.compact_matches(self.t_idx2, self.t_good, self.f_cnt, gate_xyz=self.X,
+                                gate=self.max_distance, out=(self.t_pairs, self.t_cnt), stream=st)
+        geometry.gather_temporal(self.X, self.f_ptl, kpL1, self.t_pairs, self.t_cnt,
+                                 out=(self.Q1, self.q2, self.q1), stream=st)
+        # PnP-RANSAC (transformation.py:11-13)
+        geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,
+                            out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st)
+        return self.rvec, self.tvec, self.p_ninl
+
+    def counters(self):
+        return dict(orb=self.ows.count.cpu().numpy(), stereo=self.s_cnt.cpu().numpy(),
+                    f_inliers=self.f_cnt.cpu().numpy(), temporal=self.t_cnt.cpu().numpy(),
+                    pnp_inliers=self.p_ninl.cpu().numpy())
+
+
+def relative_transform(rvec, tvec):
+    """transformation.py:15-19: T = [Rodrigues(-rvec) | -tvec] (the reference's
+    sign flip, not the true inverse of the PnP pose)."""
+    from .transformation import translation_and_rotation_vector_to_matrix
+
+    return translation_and_rotation_vector_to_matrix(-1 * np.asarray(rvec).reshape(3, 1),
+                                                     -1 * np.asarray(tvec).reshape(3, 1))
+
+
+def chain_poses(pose0, rvecs, tvecs, ninl, T_prev=None):
+    """main.py:94-98, 120-124: pose_{i+1} = pose_i @ T_i; when PnP had <= 4 points
+    the previous T is reused (stale).  Returns (poses [B,4,4], last T)."""
+    poses = []
+    pose = np.asarray(pose0, float)
+    T = np.eye(4) if T_prev is None else T_prev
+    for r, t, n in zip(rvecs, tvecs, ninl):
+        if n >= 0:
+            T = relative_transform(r, t)
+        pose = pose @ T
+        poses.append(pose)
+    return np.stack(poses), T

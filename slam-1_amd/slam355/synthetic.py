@@ -102,7 +102,7 @@ class StereoRig:
                          for P in (self.P_l, self.P_r)) + "\n"
 
 
-def _value_noise(rng, H, W, cell=48, lo=70, hi=170):
+def _value_noise(rng, H, W, cell=240, lo=100, hi=150):
     gh, gw = H // cell + 2, W // cell + 2
     g = rng.uniform(lo, hi, (gh, gw))
     ys = np.arange(H) / cell
@@ -116,14 +116,17 @@ def _value_noise(rng, H, W, cell=48, lo=70, hi=170):
     return (a * (1 - fx) + b * fx) * (1 - fy) + (c * (1 - fx) + d * fx) * fy
 
 
-def make_world(rng, n_frames, n_landmarks=20000):
-    """Corridor of landmarks: x in [-20,20], y in [-3,3], z in [5, 80 + frames]."""
+def make_world(rng, n_frames, n_landmarks=800):
+    """Corridor of landmarks: x in [-20,20], y in [-3,3], z in [5, 80 + frames].
+    Each landmark is a square patch of 16..32 px carrying its own 4x4 grid of
+    random intensities, so its corners have distinctive rBRIEF descriptors
+    (a sparse scene: dense clutter turns most corners into occlusion
+    junctions that differ between the stereo views)."""
     z = rng.uniform(5.0, 80.0 + n_frames, n_landmarks)
     X = np.stack([rng.uniform(-20, 20, n_landmarks), rng.uniform(-3, 3, n_landmarks), z], 1)
-    size = rng.integers(5, 12, n_landmarks)
-    val = np.where(rng.random(n_landmarks) < 0.5, rng.integers(0, 50, n_landmarks),
-                   rng.integers(205, 256, n_landmarks))
-    return X, size, val
+    size = rng.integers(16, 33, n_landmarks)
+    tex = rng.integers(0, 256, (n_landmarks, 4, 4)).astype(np.float64)
+    return X, size, tex
 
 
 def trajectory(rng, n_frames, step=1.0, yaw_sigma_deg=0.2):
@@ -143,50 +146,47 @@ def trajectory(rng, n_frames, step=1.0, yaw_sigma_deg=0.2):
 
 
 def render(world, T_cw_inv, rig: StereoRig, rng, x_offset=0.0, bg=None, noise=2.0):
-    """Render one grayscale view: landmarks as fixed-size squares (painter's
-    order) over value noise, plus Gaussian noise; x_offset shifts the camera
-    along its x axis (right camera = +baseline)."""
-    X, size, val = world
+    """Render one grayscale view: textured landmark patches (painter's order:
+    far first) over value noise, plus Gaussian noise; x_offset shifts the
+    camera along its x axis (right camera = +baseline)."""
+    X, size, tex = world
     H, W = rig.H, rig.W
     img = (bg if bg is not None else _value_noise(rng, H, W)).copy()
     R, t = T_cw_inv[:3, :3], T_cw_inv[:3, 3]
     Xc = X @ R.T + t
     Xc[:, 0] -= x_offset
-    vis = Xc[:, 2] > 1.0
-    Xc, sz, vv = Xc[vis], size[vis], val[vis]
+    vis = np.nonzero(Xc[:, 2] > 1.0)[0]
+    Xc = Xc[vis]
     u = rig.K[0, 0] * Xc[:, 0] / Xc[:, 2] + rig.K[0, 2]
     v = rig.K[1, 1] * Xc[:, 1] / Xc[:, 2] + rig.K[1, 2]
-    inb = (u > -12) & (u < W + 12) & (v > -12) & (v < H + 12)
-    u, v, sz, vv, z = u[inb], v[inb], sz[inb], vv[inb], Xc[inb, 2]
-    order = np.argsort(-z, kind="stable")  # far first, near drawn last
-    u, v, sz, vv = u[order], v[order], sz[order], vv[order]
+    inb = (u > -20) & (u < W + 20) & (v > -20) & (v < H + 20)
+    lid, u, v, z = vis[inb], u[inb], v[inb], Xc[inb, 2]
+    order = np.argsort(-z, kind="stable")
+    lid, u, v = lid[order], u[order], v[order]
+    sz = size[lid]
     x0 = np.round(u - sz / 2).astype(np.int64)
     y0 = np.round(v - sz / 2).astype(np.int64)
-    flat = img.reshape(-1)
+    pix, rank, val = [], [], []
     for s in np.unique(sz):
         m = np.nonzero(sz == s)[0]
         dy, dx = np.meshgrid(np.arange(s), np.arange(s), indexing="ij")
+        cell = (dy * 4 // s).ravel() * 4 + (dx * 4 // s).ravel()
         yy = y0[m, None] + dy.ravel()[None, :]
         xx = x0[m, None] + dx.ravel()[None, :]
         ok = (yy >= 0) & (yy < H) & (xx >= 0) & (xx < W)
-        # keep painter's order across size groups: write in global order below
-        m_idx = np.broadcast_to(m[:, None], yy.shape)
-        if s == np.unique(sz)[0]:
-            all_pix, all_ord, all_val = [], [], []
-        all_pix.append((yy * W + xx)[ok])
-        all_ord.append(m_idx[ok])
-        all_val.append(np.broadcast_to(vv[m, None], yy.shape)[ok])
-    if len(u):
-        pix = np.concatenate(all_pix)
-        ordr = np.concatenate(all_ord)
-        vals = np.concatenate(all_val)
-        srt = np.argsort(ordr, kind="stable")
-        flat[pix[srt]] = vals[srt]  # later (nearer) writes win
+        vals = tex[lid[m]].reshape(len(m), 16)[:, cell]
+        pix.append((yy * W + xx)[ok])
+        rank.append(np.broadcast_to(m[:, None], yy.shape)[ok])
+        val.append(vals[ok])
+    if pix:
+        pix, rank, val = np.concatenate(pix), np.concatenate(rank), np.concatenate(val)
+        srt = np.argsort(rank, kind="stable")
+        img.reshape(-1)[pix[srt]] = val[srt]  # later (nearer) writes win
     img = img + rng.normal(0, noise, img.shape)
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
-def stereo_sequence(n_frames, W=1280, H=720, seed=0, n_landmarks=20000):
+def stereo_sequence(n_frames, W=1280, H=720, seed=0, n_landmarks=800):
     """(left [F,H,W] u8, right [F,H,W] u8, poses [F,4,4] camera-to-world, rig)."""
     rng = np.random.default_rng(seed)
     rig = StereoRig(W, H)

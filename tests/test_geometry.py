@@ -151,3 +151,57 @@ def test_gpu_reference_api_mirrors():
     ET, er, et = og.pose_matrix_from_pnp(erv, etv)
     assert rvec.shape == (3, 1) and tvec.shape == (3, 1)
     assert np.allclose(T, ET, atol=1e-8) and np.allclose(rvec, er, atol=1e-8)
+
+
+def _stereo_points(seed, n=300, outliers=0.3):
+    from slam355.synthetic import StereoRig
+
+    rig = StereoRig(1280, 720)
+    rng = np.random.default_rng(seed)
+    Q = np.stack([rng.uniform(-15, 15, n), rng.uniform(-3, 3, n), rng.uniform(5, 80, n)], 1)
+    pl = Q[:, :2] / Q[:, 2:3] * rig.K[0, 0] + rig.K[:2, 2] + rng.normal(0, 0.4, (n, 2))
+    Qr = Q - [rig.baseline, 0, 0]
+    pr = Qr[:, :2] / Qr[:, 2:3] * rig.K[0, 0] + rig.K[:2, 2] + rng.normal(0, 0.4, (n, 2))
+    k = int(outliers * n)
+    pr[:k] = rng.uniform([0, 0], [1280, 720], (k, 2))
+    return pl, pr
+
+
+def test_oracle_fundamental_lmeds_rejects_outliers():
+    pl, pr = _stereo_points(0)
+    mask, F, n, med = og.fundamental_lmeds(pl, pr, seed=1, item=3)
+    assert mask[:90].sum() <= 3 and mask[90:].mean() > 0.9
+    # epipolar constraint holds on inliers (normalised algebraic residual small)
+    h1 = np.hstack([pl, np.ones((len(pl), 1))])
+    h2 = np.hstack([pr, np.ones((len(pr), 1))])
+    assert np.median(np.abs(np.einsum("ij,jk,ik->i", h2[mask], F, h1[mask]))) < 1e-2
+    m2, F2, n2, _ = og.fundamental_lmeds(pl[:7], pr[:7])
+    assert n2 == -1 and not m2.any()  # < 8 points: no model, nothing kept
+
+
+@pytest.mark.gpu
+def test_gpu_fundamental_lmeds_matches_oracle():
+    import torch
+    from slam355 import geometry
+
+    B, cap = 4, 400
+    m1 = np.zeros((B, cap, 2))
+    m2 = np.zeros((B, cap, 2))
+    cnt = np.array([300, 120, 7, 399], np.int32)
+    for b in range(B):
+        a, c = _stereo_points(10 + b, n=int(cnt[b]), outliers=0.1 * b)
+        m1[b, :cnt[b]], m2[b, :cnt[b]] = a, c
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    mask, F, n = geometry.fundamental_lmeds(T(m1), T(m2), T(cnt), seed=9, item0=20)
+    mask, n = mask.cpu().numpy(), n.cpu().numpy()
+    for b in range(B):
+        em, eF, en, _ = og.fundamental_lmeds(m1[b, :cnt[b]], m2[b, :cnt[b]], seed=9, item=20 + b)
+        assert n[b] == en, b
+        assert np.array_equal(mask[b, :cnt[b]].astype(bool), em), b
+    # order-preserving filter of the pairs by that mask
+    pairs = np.stack([np.arange(cap), cap - np.arange(cap)], 1)[None].repeat(B, 0).astype(np.int32)
+    fp, fc = geometry.filter_pairs(T(pairs), T(cnt), T(mask))
+    fp, fc = fp.cpu().numpy(), fc.cpu().numpy()
+    for b in range(B):
+        keep = mask[b, :cnt[b]].astype(bool)
+        assert fc[b] == keep.sum() and np.array_equal(fp[b, :fc[b]], pairs[b, :cnt[b]][keep])

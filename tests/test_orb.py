@@ -22,7 +22,7 @@ CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0,
 def _frames(n=2, W=1280, H=720, seed=0):
     from slam355.synthetic import stereo_sequence
 
-    L, R, _, _ = stereo_sequence(n, W, H, seed=seed, n_landmarks=20000)
+    L, R, _, _ = stereo_sequence(n, W, H, seed=seed)
     return L, R
 
 
@@ -176,7 +176,7 @@ def _gpu_vs_oracle(imgs, max_kp, **tiling):
 def test_gpu_orb_c2_frames_bit_exact():
     L, R = _frames(2, 1280, 720, seed=0)
     cnt = _gpu_vs_oracle(np.concatenate([L, R]), 56)
-    assert (cnt > 1000).all()
+    assert (cnt > 900).all()
 
 
 @pytest.mark.gpu
