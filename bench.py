@@ -1,10 +1,20 @@
-"""slam355 benchmark — driver contract.
+"""slam355 benchmark — the driver contract.
 
-python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload tracking|ba|matcher]
 
-Prints ONE JSON line on rank 0.  For N>1 it is launched by torch.distributed.run
-(one process per GPU); each rank processes its own shard of frame pairs
-(weak scaling) and the time is the max over ranks.
+Default workload ("tracking", BASELINE.json metric "frames/sec tracking+local-BA
+@1280x720"): one step = B synthetic 1280x720 stereo frame pairs through the
+whole tracking hot path (ORB on 2B+1 images with 56 kp/tile = 2016 kp/frame,
+stereo kNN-2 + ratio, F-LMedS, triangulation, temporal kNN-2 + gate, PnP-RANSAC,
+host pose chain) plus the local bundle adjustment it schedules: every
+`ba_every` frames one LM solve of `ba_iters` iterations over a C3-shaped window
+(10 keyframes x 5k points x 30k observations).  N > 1: one process per GPU,
+each with its own frame shard and its own BA windows (weak scaling; no
+collective on this path).  `--workload ba` measures local-BA LM iterations/s:
+C3 on one GPU, or C4 (64 KF x 50k points) sharded by landmark over the ranks
+with one RCCL all-reduce of the reduced camera system per iteration.
+
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -24,10 +34,14 @@ import torch  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s (4 SIMD32 per CU)
-MATCH_OPS_PER_PAIR = 19  # 8 v_xor + 8 v_bcnt(+acc) + v_lshl_or + v_min + v_med3
+F64_PEAK_TFLOPS = 78.6        # FP64 vector == FP64 matrix on gfx950 (spec)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s (4 x SIMD32 per CU)
+MATCH_OPS_PER_PAIR = 19       # 8 v_xor + 8 v_bcnt(+acc) + v_lshl_or + v_min + v_med3
+ORB_OUT_BYTES = 56            # per keypoint: 5 f32 + octave i32 + 32 B descriptor
+W_IMG, H_IMG = 1280, 720
 
 
+# ---------------------------------------------------------------------------- plumbing
 def dist_init():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -49,107 +63,112 @@ def barrier(world):
         dist.barrier()
 
 
-def max_over_ranks(x: float, world: int) -> float:
+def reduce_scalar(x: float, world: int, op="max") -> float:
     if world == 1:
         return x
     import torch.distributed as dist
 
     t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 
 
-def sum_over_ranks(x: float, world: int) -> float:
-    if world == 1:
-        return x
-    import torch.distributed as dist
-
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t)
-    return float(t.item())
-
-
-# ---------------------------------------------------------------------------- matcher
-def matcher_workload(B: int, seed: int):
-    from slam355 import matcher
-    from slam355.synthetic import descriptor_batch
-
-    q, nq, t, nt = descriptor_batch(B, 2000, 2000, seed=seed)
-    dev = torch.device("cuda")
-    tq, tt = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
-    tnq, tnt = torch.from_numpy(nq).to(dev), torch.from_numpy(nt).to(dev)
-    out = matcher.knn2_batch(tq, tnq, tt, tnt)
-    pairs_per_step = float((nq.astype(np.int64) * nt).sum())
-
-    def step():
-        matcher.knn2_batch(tq, tnq, tt, tnt, out=out)
-
-    return step, pairs_per_step, (q, nq, t, nt)
-
-
-def cpu_baseline_matcher(host, budget_s=10.0):
-    import oracle
-
-    q, nq, t, nt = host
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    n = 1
-    pairs = 0.0
+def timed_loop(step, steps, warmup, world, marks_every=True):
+    """W untimed steps, then exactly K timed steps between barrier+synchronize
+    fences; per-step stage events are recorded on the launch stream."""
+    for _ in range(warmup):
+        step(None)
+    torch.cuda.synchronize()
+    all_marks = []
+    barrier(world)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    while True:
-        k = min(n, len(nq))
-        oracle.hamming_knn2_batch(q[:k], nq[:k], t[:k], nt[:k])
-        pairs += float((nq[:k].astype(np.int64) * nt[:k]).sum())
-        if time.perf_counter() - t0 > budget_s or k == len(nq) and n > 64:
-            break
-        n *= 2
+    for _ in range(steps):
+        marks = [] if marks_every else None
+        step(marks)
+        if marks is not None:
+            all_marks.append(marks)
+    torch.cuda.synchronize()
+    barrier(world)
     dt = time.perf_counter() - t0
-    return {"value": pairs / dt / 1e9, "unit": "Gpairs/s", "cores": threads, "kind": "port",
-            "sample": f"C oracle (oracle/hamming.c, OpenMP {threads} threads) on up to "
-                      f"{len(nq)} 2000x2000 descriptor pairs, {dt:.1f}s"}
+    stages = {}
+    for marks in all_marks:
+        for (n0, e0), (n1, e1) in zip(marks[:-1], marks[1:]):
+            stages.setdefault(n1, []).append(e0.elapsed_time(e1))
+    return reduce_scalar(dt, world, "max"), {k: float(np.mean(v)) for k, v in stages.items()}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="matcher", choices=["matcher"])
-    ap.add_argument("--batch", type=int, default=64, help="frame pairs per rank per step")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+def ba_flops_per_iter(C, P, O, n_per_pt):
+    """O(4c^2+16c+48) + sum_p 2(3c^2 n_p^2 + 9c n_p) + (cC)^3/3, c = 9."""
+    c = 9
+    return O * (4 * c * c + 16 * c + 48) + P * 2 * (3 * c * c * n_per_pt ** 2 + 9 * c * n_per_pt) \
+        + (c * C) ** 3 / 3
 
-    world, rank = dist_init()
-    step, units_per_step, host = matcher_workload(args.batch, seed=rank)
+
+# ---------------------------------------------------------------------------- tracking
+def run_tracking(args, world, rank):
+    from slam355.ba import BAProblem
+    from slam355.pipeline import Tracker, chain_poses
+    from slam355.synthetic import ba_problem, perturb, stereo_sequence
+
+    B = args.batch
+    L, R, poses, rig = stereo_sequence(B + 1, W_IMG, H_IMG, seed=1000 + rank)
+    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=56, seed=rank)
+    trk.imgs.copy_(torch.from_numpy(np.concatenate([L, R[:B]])))
+    rng = np.random.default_rng(2000 + rank)
+    C3 = (10, 5000, 6)
+    cams, pts, ci, pi, qs = ba_problem(rng, *C3)
+    c0, p0 = perturb(rng, cams, pts)
+    ba = BAProblem(c0, p0, ci, pi, qs)
+    n_solves = max(1, B // args.ba_every)
     stream = torch.cuda.current_stream()
+    state = {}
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
+    def step(marks):
+        trk.track(0, marks=marks)
+        for _ in range(n_solves):
+            ba.restore()
+            ba.iterate(args.ba_iters)
+        if marks is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            marks.append(("local_ba", ev))
+        rv, tv, n = trk.rvec.cpu().numpy(), trk.tvec.cpu().numpy(), trk.p_ninl.cpu().numpy()
+        state["poses"], _ = chain_poses(np.eye(4), rv, tv, n)  # main.py:120-124 (host)
 
-    # kernel-level timing: HIP events on the launch stream around each step
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    barrier(world)
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, world)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    dt, stages = timed_loop(step, args.steps, args.warmup, world)
+    frames = reduce_scalar(float(B * args.steps), world, "sum")
+    cnt = trk.counters()
+    # accuracy of the tracked trajectory against the synthetic ground truth
+    est = state["poses"]
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[i + 1] for i in range(B)])
+    t_err = np.linalg.norm(est[:, :3, 3] - gt[:, :3, 3], axis=1)
 
-    total_units = sum_over_ranks(units_per_step * args.steps, world)
-    ops = units_per_step * MATCH_OPS_PER_PAIR
-    achieved = ops / (kern_ms * 1e-3) / 1e12
-    hbm_bytes = float(args.batch * (2000 + 2000) * 32 + args.batch * 2000 * 17)
+    # roofline of the dominant stage
+    n_img = 2 * B + 1
+    patch_bytes = 36 * 216 * 192
+    kp_mean = float(np.mean(np.maximum(cnt["orb"], 0)))
+    orb_bytes = n_img * (patch_bytes + kp_mean * ORB_OUT_BYTES)
+    orb_ms = stages.get("orb", float("nan"))
+    ba_ms_iter = stages.get("local_ba", float("nan")) / (n_solves * args.ba_iters)
+    ba_flops = ba_flops_per_iter(*C3[:2], C3[1] * C3[2], C3[2])
+    roof = {
+        "orb": {"bound": "hbm", "achieved": orb_bytes / (orb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
+                "bytes_per_launch": orb_bytes},
+        "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration (10 kernels)",
+                     "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
+    }
+    for r in roof.values():
+        r["frac"] = r["achieved"] / r["peak"]
+        r["traffic"] = None
+    per_step = {k: v for k, v in stages.items()}
+    dominant = max(("orb", orb_ms), ("local_ba", stages.get("local_ba", 0.0)), key=lambda kv: kv[1])[0]
     rec = {
-        "metric": "BF-Hamming kNN-2 match throughput @ C2 (2000x2000 x 32B descriptors)",
-        "value": total_units / dt / 1e9,
-        "unit": "Gpairs/s",
+        "metric": "frames/sec tracking+local-BA @1280x720",
+        "value": frames / dt,
+        "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -157,19 +176,167 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded random 256-bit descriptors, 60% planted near-duplicates)",
-        "config": {"workload": "C2 matcher: 1280x720-class, 2000 kp/frame, BF-Hamming kNN-2",
-                   "batch_pairs_per_gpu": args.batch, "parallelism": f"frame-pair shards x{world}"},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
-                     "unit": "Tops/s", "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
-                     "kernel": "knn2_kernel", "kernel_ms": kern_ms,
-                     "hbm_achieved_GBs": hbm_bytes / (kern_ms * 1e-3) / 1e9,
-                     "hbm_peak_GBs": HBM_PEAK_GBS,
-                     "effective_scan_GBs": units_per_step * 32 / (kern_ms * 1e-3) / 1e9},
+        "dtype": "u8+f32+f64",
+        "data": "synthetic (seeded 1280x720 stereo sequence, 800 textured landmarks, GT poses)",
+        "config": {"workload": "C2 tracking (1280x720, 56 ORB kp/tile = 2016 kp/frame) + "
+                               f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
+                               f"x {args.ba_iters} LM iters",
+                   "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}"},
+        "roofline": dict(roof[dominant], stage=dominant),
+        "roofline_stages": roof,
+        "stage_ms_per_step": per_step,
+        "ba_iters_per_s": reduce_scalar((n_solves * args.ba_iters * args.steps) / dt, world, "sum"),
+        "tracking": {"orb_kp_mean": kp_mean, "stereo_matches_mean": float(np.mean(cnt["stereo"])),
+                     "f_inliers_mean": float(np.mean(cnt["f_inliers"])),
+                     "temporal_mean": float(np.mean(cnt["temporal"])),
+                     "pnp_inliers_mean": float(np.mean(cnt["pnp_inliers"])),
+                     "trajectory_t_err_m_max": float(t_err.max())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline_matcher(host)
+        rec["cpu_baseline"] = cpu_baseline_tracking(L, R, rig, args, C3, (c0, p0, ci, pi, qs))
+    return rec
+
+
+def cpu_baseline_tracking(L, R, rig, args, C3, ba_in, pairs=2):
+    """The CPU oracle (C ORB/kNN/F-LMedS/PnP + numpy DLT, numpy Schur LM) on a
+    bounded sample: `pairs` frame pairs of the same sequence and one LM
+    iteration of the same C3 window, combined with the same BA schedule."""
+    import oracle
+    from oracle import ba as oba
+    from oracle import pipeline as opl
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    cache = {}
+    kp, octv, desc, cnt = oracle.orb_tiles_batch(np.concatenate([L[:pairs + 1], R[:pairs]]), 56,
+                                                 1 << 13)
+    for i in range(pairs + 1):
+        cache[("L", i)] = (kp[i, :cnt[i]], octv[i, :cnt[i]], desc[i, :cnt[i]])
+    for i in range(pairs):
+        j = pairs + 1 + i
+        cache[("R", i)] = (kp[j, :cnt[j]], octv[j, :cnt[j]], desc[j, :cnt[j]])
+    for i in range(pairs):
+        opl.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, seed=0, frame=i, orb_cache=cache)
+    t_track = (time.perf_counter() - t0) / pairs
+    c0, p0, ci, pi, qs = ba_in
+    pr = oba._obs_pairs(ci, pi)
+    t1 = time.perf_counter()
+    oba.lm_iteration_schur(c0, p0, ci, pi, qs, oba.LMState(), pr)
+    t_iter = time.perf_counter() - t1
+    per_frame = t_track + args.ba_iters * t_iter / args.ba_every
+    return {"value": 1.0 / per_frame, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs} frame pairs through the oracle chain (ORB OpenMP x{threads} "
+                      f"over {2 * pairs + 1} images, rest single-thread C/numpy) = "
+                      f"{t_track * 1e3:.0f} ms/frame + 1 numpy Schur LM iteration on the C3 "
+                      f"window = {t_iter * 1e3:.0f} ms/iter (x{args.ba_iters}/{args.ba_every} "
+                      "per frame)"}
+
+
+# ---------------------------------------------------------------------------- local BA
+def run_ba(args, world, rank):
+    from slam355.ba import BAProblem
+    from slam355.synthetic import ba_problem, perturb
+
+    C, P, k = (10, 5000, 6) if world == 1 and not args.c4 else (64, 50000, 6)
+    rng = np.random.default_rng(7)  # same global problem on every rank
+    cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+    c0, p0 = perturb(rng, cams, pts)
+    if world > 1:
+        # landmark sharding by anchor keyframe (contiguous point ranges per rank)
+        anchor = np.zeros(P, np.int64)
+        np.minimum.at(anchor, pi, 0)
+        first = np.full(P, C, np.int64)
+        np.minimum.at(first, pi, ci)
+        order = np.argsort(first, kind="stable")
+        mine = np.zeros(P, bool)
+        mine[order[rank * P // world:(rank + 1) * P // world]] = True
+        keep = mine[pi]
+        remap = -np.ones(P, np.int64)
+        remap[mine] = np.arange(mine.sum())
+        prob = BAProblem(c0, p0[mine], ci[keep], remap[pi[keep]], qs[keep])
+        step_fn = prob.step_distributed
+    else:
+        prob = BAProblem(c0, p0, ci, pi, qs)
+        step_fn = lambda: prob.iterate(1)  # noqa: E731
+
+    def step(marks):
+        step_fn()
+
+    dt, _ = timed_loop(step, args.steps, args.warmup, world, marks_every=False)
+    flops = ba_flops_per_iter(C, P, P * k, k)
+    it_s = args.steps / dt
+    achieved = flops * it_s / 1e12
+    return {
+        "metric": "local-BA LM iterations/sec",
+        "value": it_s, "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic BA problem (seeded, 6 obs/point, sigma 0.5 px)",
+        "config": {"workload": f"{'C4' if C == 64 else 'C3'} local BA {C} KF x {P} pts x {P * k} obs",
+                   "parallelism": f"landmark shards x{world} + RCCL all-reduce" if world > 1 else "1 GPU"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / F64_PEAK_TFLOPS, "traffic": None,
+                     "kernel": "LM iteration", "flops_per_iter": flops},
+        "final_cost": prob.state()["COST"],
+    }
+
+
+# ---------------------------------------------------------------------------- matcher
+def run_matcher(args, world, rank):
+    from slam355 import matcher
+    from slam355.synthetic import descriptor_batch
+
+    q, nq, t, nt = descriptor_batch(args.batch, 2000, 2000, seed=rank)
+    dev = torch.device("cuda")
+    tq, tt = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
+    tnq, tnt = torch.from_numpy(nq).to(dev), torch.from_numpy(nt).to(dev)
+    out = matcher.knn2_batch(tq, tnq, tt, tnt)
+    stream = torch.cuda.current_stream()
+
+    def step(marks):
+        if marks is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            marks.append(("start", e))
+        matcher.knn2_batch(tq, tnq, tt, tnt, out=out)
+        if marks is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            marks.append(("knn2", e))
+
+    dt, stages = timed_loop(step, args.steps, args.warmup, world)
+    pairs = float((nq.astype(np.int64) * nt).sum())
+    kms = stages["knn2"]
+    achieved = pairs * MATCH_OPS_PER_PAIR / (kms * 1e-3) / 1e12
+    return {
+        "metric": "BF-Hamming kNN-2 match throughput @ C2 (2000x2000 x 32 B descriptors)",
+        "value": reduce_scalar(pairs * args.steps, world, "sum") / dt / 1e9, "unit": "Gpairs/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (seeded random descriptors, 60% planted near-duplicates)",
+        "config": {"workload": "C2 matcher", "batch_pairs_per_gpu": args.batch},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+                     "frac": achieved / VALU_PEAK_TOPS, "traffic": None, "kernel": "knn2_kernel",
+                     "ms_per_launch": kms},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="tracking", choices=["tracking", "ba", "matcher"])
+    ap.add_argument("--batch", type=int, default=32, help="frame pairs per GPU per step")
+    ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
+    ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
+    ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world, rank = dist_init()
+    run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher}[args.workload]
+    rec = run(args, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

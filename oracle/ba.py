@@ -223,3 +223,79 @@ def sim3_align(A, B):
 def camera_centers(cams):
     R = rotation_matrices(cams[:, :3])
     return -np.einsum("oji,oj->oi", R, cams[:, 3:6])
+
+
+# ----------------------------------------------------------------------------- LM (Schur)
+def _obs_pairs(cam_idx, pt_idx):
+    """All ordered observation pairs (o1, o2) of the same point with cam1 <= cam2."""
+    order = np.lexsort((cam_idx, pt_idx))
+    pts = pt_idx[order]
+    starts = np.flatnonzero(np.r_[True, pts[1:] != pts[:-1]])
+    counts = np.diff(np.r_[starts, len(pts)])
+    o1s, o2s = [], []
+    for n in np.unique(counts):
+        s = starts[counts == n]
+        a = (s[:, None, None] + np.arange(n)[None, :, None]).repeat(n, 2).reshape(len(s), -1)
+        b = (s[:, None, None] + np.arange(n)[None, None, :]).repeat(n, 1).reshape(len(s), -1)
+        a, b = order[a], order[b]
+        keep = cam_idx[a] <= cam_idx[b]
+        o1s.append(a[keep])
+        o2s.append(b[keep])
+    return np.concatenate(o1s), np.concatenate(o2s)
+
+
+def lm_iteration_schur(cams, pts, cam_idx, pt_idx, qs, st: LMState, pairs=None):
+    """The same LM iteration as lm_iteration, solved through the point-block
+    Schur complement (vectorised numpy; scales to the C3/C4 problems)."""
+    C, P = len(cams), len(pts)
+    cam_idx = np.asarray(cam_idx)
+    pt_idx = np.asarray(pt_idx)
+    r, J = residual_and_jacobian(cams, pts, cam_idx, pt_idx, qs)
+    cost = 0.5 * float(np.sum(r * r))
+    Jc, Jp = J[:, :, :9], J[:, :, 9:]
+    U = np.zeros((C, 9, 9))
+    np.add.at(U, cam_idx, np.einsum("oai,oaj->oij", Jc, Jc))
+    V = np.zeros((P, 3, 3))
+    np.add.at(V, pt_idx, np.einsum("oai,oaj->oij", Jp, Jp))
+    gc = np.zeros((C, 9))
+    np.add.at(gc, cam_idx, -np.einsum("oai,oa->oi", Jc, r))
+    gp = np.zeros((P, 3))
+    np.add.at(gp, pt_idx, -np.einsum("oai,oa->oi", Jp, r))
+    Dc = np.clip(np.diagonal(U, axis1=1, axis2=2), DIAG_MIN, DIAG_MAX)
+    Dp = np.clip(np.diagonal(V, axis1=1, axis2=2), DIAG_MIN, DIAG_MAX)
+    Vs = V + st.lam * Dp[:, :, None] * np.eye(3)[None]
+    Vi = np.linalg.inv(Vs)
+    W = np.einsum("oai,oaj->oij", Jc, Jp)
+    Y = np.einsum("oij,ojk->oik", W, Vi[pt_idx])
+    e = np.einsum("pij,pj->pi", Vi, gp)
+    if pairs is None:
+        pairs = _obs_pairs(cam_idx, pt_idx)
+    o1, o2 = pairs
+    S = np.zeros((C, C, 9, 9))
+    blk = np.einsum("oik,ojk->oij", Y[o1], W[o2])
+    np.add.at(S, (cam_idx[o1], cam_idx[o2]), -blk)
+    same = cam_idx[o1] == cam_idx[o2]
+    S = S + np.transpose(S, (1, 0, 3, 2)) * (1 - np.eye(C))[:, :, None, None]
+    del same
+    S[np.arange(C), np.arange(C)] += U + st.lam * Dc[:, :, None] * np.eye(9)[None]
+    Sd = S.transpose(0, 2, 1, 3).reshape(9 * C, 9 * C)
+    b = gc.copy()
+    np.add.at(b, cam_idx, -np.einsum("oij,oj->oi", Y, gp[pt_idx]))
+    dc = np.linalg.solve(Sd, b.ravel()).reshape(C, 9)
+    dp = e.copy()
+    np.add.at(dp, pt_idx, -np.einsum("oji,oj->oi", Y, dc[cam_idx]))
+    cams_n, pts_n = cams + dc, pts + dp
+    rn = residual_and_jacobian(cams_n, pts_n, cam_idx, pt_idx, qs)[0]
+    cost_new = 0.5 * float(np.sum(rn * rn))
+    pred = 0.5 * (float(np.sum(dc * (st.lam * Dc * dc + gc))) +
+                  float(np.sum(dp * (st.lam * Dp * dp + gp))))
+    rho = (cost - cost_new) / pred if pred > 0 else -1.0
+    accepted = rho > 0 and np.isfinite(cost_new)
+    if accepted:
+        st.lam = min(max(st.lam * max(1.0 / 3.0, 1.0 - (2.0 * rho - 1.0) ** 3), LAM_MIN), LAM_MAX)
+        st.nu = 2.0
+        cams, pts = cams_n, pts_n
+    else:
+        st.lam = min(st.lam * st.nu, LAM_MAX)
+        st.nu *= 2.0
+    return cams, pts, dict(cost=cost, cost_new=cost_new, pred=pred, rho=rho, accepted=accepted)

@@ -148,6 +148,14 @@ class BAProblem:
         self._s = s
         self.reset(lam0)
 
+        self._init = (t["cams0"].clone(), t["pts0"].clone())
+
+    def restore(self, lam0=1e-4):
+        """Reload the initial parameters and reset the LM state (device copies)."""
+        self.t["cams0"].copy_(self._init[0])
+        self.t["pts0"].copy_(self._init[1])
+        self.reset(lam0)
+
     # -- primitive phases -------------------------------------------------------
     def _sp(self):
         return stream_ptr(self.stream)

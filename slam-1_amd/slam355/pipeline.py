@@ -77,7 +77,7 @@ class Tracker:
         self.imgs = torch.zeros((2 * B + 1, H, W), **u8)
 
     # ------------------------------------------------------------------ device step
-    def track(self, frame0: int, imgs: torch.Tensor | None = None):
+    def track(self, frame0: int, imgs: torch.Tensor | None = None, marks=None):
         """Run the B frame pairs (frame0 + b, frame0 + b + 1), b < B, on device.
 
         `imgs` [2B+1, H, W] u8 = left_{frame0..frame0+B}, right_{frame0..frame0+B-1}
@@ -85,7 +85,16 @@ class Tracker:
         device tensors (rvec, tvec, n_inliers)."""
         B, st = self.B, self.stream
         im = self.imgs if imgs is None else imgs
+
+        def mark(name):  # optional stage events on the launch stream (bench.py)
+            if marks is not None:
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(st if st is not None else torch.cuda.current_stream())
+                marks.append((name, ev))
+
+        mark("start")
         kp, octv, desc, cnt = self.ows.run(im, st)
+        mark("orb")
         kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
         nL, nR = cnt[0:B], cnt[B + 1:2 * B + 1]
@@ -96,10 +105,12 @@ class Tracker:
                                 stream=st)
         geometry.gather_matches(kpL, kpR, self.s_pairs, self.s_cnt,
                                 out=(self.s_ptl, self.s_ptr, None, None), stream=st)
+        mark("stereo_match")
         # F-LMedS mask (keypoint.py:102-109), then the surviving pairs with descriptors
         geometry.fundamental_lmeds(self.s_ptl, self.s_ptr, self.s_cnt, seed=self.seed,
                                    item0=frame0, out=(self.f_mask, self.f_F, self.f_ninl),
                                    stream=st)
+        mark("f_lmeds")
         geometry.filter_pairs(self.s_pairs, self.s_cnt, self.f_mask,
                               out=(self.f_pairs, self.f_cnt), stream=st)
         geometry.gather_matches(kpL, kpR, self.f_pairs, self.f_cnt, dL, dR,
@@ -114,9 +125,11 @@ class Tracker:
                                 gate=self.max_distance, out=(self.t_pairs, self.t_cnt), stream=st)
         geometry.gather_temporal(self.X, self.f_ptl, kpL1, self.t_pairs, self.t_cnt,
                                  out=(self.Q1, self.q2, self.q1), stream=st)
+        mark("triangulate_temporal")
         # PnP-RANSAC (transformation.py:11-13)
         geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,
                             out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st)
+        mark("pnp")
         return self.rvec, self.tvec, self.p_ninl
 
     def counters(self):
