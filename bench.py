@@ -242,18 +242,10 @@ def run_ba(args, world, rank):
     cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
     c0, p0 = perturb(rng, cams, pts)
     if world > 1:
-        # landmark sharding by anchor keyframe (contiguous point ranges per rank)
-        anchor = np.zeros(P, np.int64)
-        np.minimum.at(anchor, pi, 0)
-        first = np.full(P, C, np.int64)
-        np.minimum.at(first, pi, ci)
-        order = np.argsort(first, kind="stable")
-        mine = np.zeros(P, bool)
-        mine[order[rank * P // world:(rank + 1) * P // world]] = True
-        keep = mine[pi]
-        remap = -np.ones(P, np.int64)
-        remap[mine] = np.arange(mine.sum())
-        prob = BAProblem(c0, p0[mine], ci[keep], remap[pi[keep]], qs[keep])
+        from slam355.dist import shard_by_anchor
+
+        mine, keep, local_pi = shard_by_anchor(C, P, ci, pi, rank, world)
+        prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep])
         step_fn = prob.step_distributed
     else:
         prob = BAProblem(c0, p0, ci, pi, qs)

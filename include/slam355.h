@@ -214,7 +214,7 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
 typedef struct slam_ba_problem {
   int32_t n_cams, n_pts, n_obs;
   int32_t n_cam_chunks;  /* camera-Gram work items                          */
-  int32_t n_blocks;      /* upper camera-pair blocks of S with >= 1 obs pair */
+  int32_t n_blocks;      /* upper camera-pair blocks of S: C(C+1)/2            */
   int32_t n_pair_chunks; /* Schur work items                                 */
   int32_t n_pairs;
   int32_t reserved;
@@ -229,15 +229,18 @@ typedef struct slam_ba_problem {
   const int32_t* cam_chunk_ptr; /* [C+1] chunk range of each camera            */
   const int32_t* pair_o;        /* [n_pairs][2] (o1 in c1, o2 in c2), by block */
   const int32_t* pair_chunks;   /* [n_pair_chunks][3] (block, begin, end)      */
-  const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2)                    */
-  const int32_t* block_chunk_ptr; /* [n_blocks+1]                              */
-  double* rec;                  /* [O][2][16] Jc(9) r u Jp(3) 0 0              */
+  const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2), every upper block */
+  const int32_t* block_chunk_ptr; /* [n_blocks+1] (empty range: no common point) */
+  const int32_t* obs_campos;    /* [O] position of obs o in cam_obs            */
+  double* rec;                  /* [O][2][16] Jc(9) r u Jp(3) 0 0 (by point)   */
+  double* recc;                 /* [O][2][16] Jc(9) r u 0.. (camera order)     */
   double* wy;                   /* [O][54] W = Jc^T Jp (9x3), Y = W V*^-1       */
-  double* ptdata;               /* [P][12] e(3) g(3) diagV(3) -                 */
+  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) V*^-1(6) -        */
+  double* dy;                   /* [O][3] Y_o^T dc back-substitution terms     */
   double* cam_part;             /* [n_cam_chunks][256] Gram partials           */
   double* pair_part;            /* [n_pair_chunks][81] Schur partials          */
   double* sys;                  /* S[(9C)^2] b[9C] g[9C] diagU[9C] cost[C]     */
-  double* chol;                 /* [(9C)^2] factor workspace (9C > 120 only)   */
+  double* chol;                 /* [slam_ba_chol_len] (9C > 120 only)           */
   double* delta_c;              /* [9C]                                        */
   double* red_part;             /* [slam_ba_red_slots(P, O)]                   */
   double* small;                /* [4] trial |r|^2, sum pred_p (all-reduced)   */
@@ -246,6 +249,8 @@ typedef struct slam_ba_problem {
 
 /* Number of doubles red_part needs for a problem of P points and O obs. */
 int slam_ba_red_slots(int n_pts, int n_obs);
+/* Doubles of the factorisation workspace `chol` (needed only when 9C > 120). */
+long long slam_ba_chol_len(int n_cams);
 /* Doubles in the all-reduced system buffer: (9C)^2 + 27C + C. */
 long long slam_ba_sys_len(int n_cams);
 

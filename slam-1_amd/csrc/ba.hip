@@ -201,10 +201,12 @@ __global__ __launch_bounds__(kBS) void k_linearize(slam_ba_problem p) {
   reproject<true>(p.cams[cur] + 9 * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o], p.obs_q + 2 * o,
                   r, J);
   clamp_rows<true>(r, J);
+  // point-ordered record (k_points / k_obs_wy) and camera-ordered record (k_cam_gram)
   double* rec = p.rec + (size_t)o * 2 * kRecW;
+  double* recc = p.recc + (size_t)p.obs_campos[o] * 2 * kRecW;
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
-    double* row = rec + a * kRecW;
+    double row[kRecW];
     for (int k = 0; k < 9; ++k) row[k] = J[a][k];
     row[9] = r[a];
     row[10] = 0.0;
@@ -213,11 +215,22 @@ __global__ __launch_bounds__(kBS) void k_linearize(slam_ba_problem p) {
     row[13] = J[a][11];
     row[14] = 0.0;
     row[15] = 0.0;
+    double2* d0 = reinterpret_cast<double2*>(rec + a * kRecW);
+    double2* d1 = reinterpret_cast<double2*>(recc + a * kRecW);
+#pragma unroll
+    for (int k = 0; k < kRecW / 2; ++k) {
+      const double2 v = make_double2(row[2 * k], row[2 * k + 1]);
+      d0[k] = v;
+      d1[k] = k < 5 ? v : make_double2(0.0, 0.0);  // M = [Jc | r | u | 0 ...]
+    }
   }
 }
 
 __device__ __forceinline__ double clampd(double d) { return fmin(fmax(d, kDiagMin), kDiagMax); }
 
+constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) V*^-1 (6, symmetric) pad
+
+// Per point: V = sum Jp^T Jp, g = -Jp^T r, V* = V + lam diag, V*^-1, e = V*^-1 g.
 __global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
   const int pt = blockIdx.x * kBS + threadIdx.x;
   if (pt >= p.n_pts) return;
@@ -226,6 +239,7 @@ __global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
   double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
   for (int o = b; o < e; ++o) {
     const double* rec = p.rec + (size_t)o * 2 * kRecW;
+#pragma unroll
     for (int a = 0; a < 2; ++a) {
       const double* row = rec + a * kRecW;
       const double j0 = row[11], j1 = row[12], j2 = row[13], rr = row[9];
@@ -237,7 +251,6 @@ __global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
   const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
   const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
   const double a01 = V01, a02 = V02, a12 = V12;
-  // inverse of the symmetric 3x3 by cofactors
   const double c00 = a11 * a22 - a12 * a12;
   const double c01 = a02 * a12 - a01 * a22;
   const double c02 = a01 * a12 - a02 * a11;
@@ -246,42 +259,60 @@ __global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
   const double c22 = a00 * a11 - a01 * a01;
   const double det = a00 * c00 + a01 * c01 + a02 * c02;
   const double id = det != 0.0 ? 1.0 / det : 0.0;
-  const double Vi[3][3] = {{c00 * id, c01 * id, c02 * id},
-                           {c01 * id, c11 * id, c12 * id},
-                           {c02 * id, c12 * id, c22 * id}};
-  const double e0 = Vi[0][0] * g0 + Vi[0][1] * g1 + Vi[0][2] * g2;
-  const double e1 = Vi[1][0] * g0 + Vi[1][1] * g1 + Vi[1][2] * g2;
-  const double e2 = Vi[2][0] * g0 + Vi[2][1] * g1 + Vi[2][2] * g2;
-  double* pd = p.ptdata + (size_t)pt * 12;
-  pd[0] = e0; pd[1] = e1; pd[2] = e2;
+  const double i00 = c00 * id, i01 = c01 * id, i02 = c02 * id;
+  const double i11 = c11 * id, i12 = c12 * id, i22 = c22 * id;
+  double* pd = p.ptdata + (size_t)pt * kPtData;
+  pd[0] = i00 * g0 + i01 * g1 + i02 * g2;
+  pd[1] = i01 * g0 + i11 * g1 + i12 * g2;
+  pd[2] = i02 * g0 + i12 * g1 + i22 * g2;
   pd[3] = g0; pd[4] = g1; pd[5] = g2;
   pd[6] = d0; pd[7] = d1; pd[8] = d2;
-  for (int o = b; o < e; ++o) {
-    double* rec = p.rec + (size_t)o * 2 * kRecW;
-    double W[9][3];
-    for (int i = 0; i < 9; ++i) {
-      const double a0 = rec[i], a1 = rec[kRecW + i];
-      for (int c = 0; c < 3; ++c) W[i][c] = a0 * rec[11 + c] + a1 * rec[kRecW + 11 + c];
-    }
-    double* wy = p.wy + (size_t)o * 54;
-    for (int i = 0; i < 9; ++i) {
-      for (int c = 0; c < 3; ++c) wy[i * 3 + c] = W[i][c];
-      for (int c = 0; c < 3; ++c)
-        wy[27 + i * 3 + c] = W[i][0] * Vi[0][c] + W[i][1] * Vi[1][c] + W[i][2] * Vi[2][c];
-    }
-    for (int a = 0; a < 2; ++a) {
-      double* row = rec + a * kRecW;
-      row[10] = row[11] * e0 + row[12] * e1 + row[13] * e2;
-    }
-  }
+  pd[9] = i00; pd[10] = i01; pd[11] = i02; pd[12] = i11; pd[13] = i12; pd[14] = i22;
 }
 
-// f64 MFMA Gram of M = [Jc | r | u | Jp | 0 0] over one chunk of a camera's
-// observations: G = M^T M.  v_mfma_f64_16x16x4_f64: lane l holds
-// A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; with A = M^T, B = M both are
-// the same element M[k][l&15], so every lane loads one double per MFMA and one
-// MFMA consumes 4 residual rows = 2 observations.
+// Per observation: W = Jc^T Jp (9x3), Y = W V*^-1, u = Jp e (into both records, col 10).
+__global__ __launch_bounds__(kBS) void k_obs_wy(slam_ba_problem p) {
+  const int o = blockIdx.x * kBS + threadIdx.x;
+  if (o >= p.n_obs) return;
+  double* rec = p.rec + (size_t)o * 2 * kRecW;
+  const double* pd = p.ptdata + (size_t)p.obs_pt[o] * kPtData;
+  const double Vi[3][3] = {{pd[9], pd[10], pd[11]}, {pd[10], pd[12], pd[13]},
+                           {pd[11], pd[13], pd[14]}};
+  const double e0 = pd[0], e1 = pd[1], e2 = pd[2];
+  double r0[kRecW], r1[kRecW];
+#pragma unroll
+  for (int k = 0; k < kRecW; ++k) {
+    r0[k] = rec[k];
+    r1[k] = rec[kRecW + k];
+  }
+  double* wy = p.wy + (size_t)o * 54;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    double W[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) W[c] = r0[i] * r0[11 + c] + r1[i] * r1[11 + c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) wy[i * 3 + c] = W[c];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) wy[27 + i * 3 + c] = W[0] * Vi[0][c] + W[1] * Vi[1][c] + W[2] * Vi[2][c];
+  }
+  const double u0 = r0[11] * e0 + r0[12] * e1 + r0[13] * e2;
+  const double u1 = r1[11] * e0 + r1[12] * e1 + r1[13] * e2;
+  rec[10] = u0;
+  rec[kRecW + 10] = u1;
+  double* recc = p.recc + (size_t)p.obs_campos[o] * 2 * kRecW;
+  recc[10] = u0;
+  recc[kRecW + 10] = u1;
+}
+
+// f64 MFMA Gram of M = [Jc | r | u | 0...] over one chunk of a camera's
+// observations (camera-ordered record: contiguous rows, no gather): G = M^T M.
+// v_mfma_f64_16x16x4_f64: lane l holds A[i = l&15][k = l>>4] and
+// B[k = l>>4][j = l&15]; with A = M^T, B = M both are the same element
+// M[k][l&15], so each lane loads one double per MFMA and one MFMA consumes 4
+// residual rows = 2 observations.  8 steps are loaded before they are consumed.
 constexpr int kGramWG = 256;
+constexpr int kGramUnroll = 8;
 __global__ __launch_bounds__(kGramWG) void k_cam_gram(slam_ba_problem p) {
   __shared__ double red[4][256];
   const int ch = blockIdx.x;
@@ -289,15 +320,18 @@ __global__ __launch_bounds__(kGramWG) void k_cam_gram(slam_ba_problem p) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int krow = lane >> 4, col = lane & 15;
   d4 acc = {0.0, 0.0, 0.0, 0.0};
-  // each MFMA step covers 2 observations; the 4 waves interleave steps
-  for (int s = beg + 2 * wid; s < end; s += 8) {
-    const int oi = s + (krow >> 1);
-    double v = 0.0;
-    if (oi < end) {
-      const int o = p.cam_obs[oi];
-      v = p.rec[(size_t)o * 2 * kRecW + (krow & 1) * kRecW + col];
+  // rows of the chunk: 2 per observation; each MFMA step takes 4 rows
+  const int row0 = 2 * beg, row1 = 2 * end;
+  const double* M = p.recc;
+  for (int base = row0 + 4 * wid; base < row1; base += 16 * kGramUnroll) {
+    double v[kGramUnroll];
+#pragma unroll
+    for (int u = 0; u < kGramUnroll; ++u) {
+      const int r = base + 16 * u + krow;
+      v[u] = r < row1 ? M[(size_t)r * kRecW + col] : 0.0;
     }
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < kGramUnroll; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[u], v[u], acc, 0, 0, 0);
   }
   // D layout (f64): col = lane&15, row = (lane>>4) + 4*reg
 #pragma unroll
@@ -337,9 +371,12 @@ __global__ __launch_bounds__(kPairWG) void k_pair_partials(slam_ba_problem p) {
   if (t < 81) p.pair_part[(size_t)ch * 81 + t] = (red[0][t] + red[1][t]) + red[2][t];
 }
 
-// One workgroup per upper block (c1 <= c2): S block = [U_c] - sum(Y W^T).
+// One workgroup per upper camera-pair block (c1 <= c2), ALL C(C+1)/2 of them:
+// S block = [U_c] - sum(Y W^T); blocks without common points are written as
+// zeros, so sys needs no separate clearing.  Partial sums are read 4 at a time.
 __global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
   __shared__ double G[256];
+  __shared__ double T3[3][81];
   const int blk = blockIdx.x;
   const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
   const int C9 = 9 * p.n_cams;
@@ -350,16 +387,35 @@ __global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
   double* costc = diagU + C9;
   const int t = threadIdx.x;
   if (c1 == c2) {
-    double acc = 0.0;
-    for (int ch = p.cam_chunk_ptr[c1]; ch < p.cam_chunk_ptr[c1 + 1]; ++ch)
-      acc += p.cam_part[(size_t)ch * 256 + t];
-    G[t] = acc;
+    const int cb = p.cam_chunk_ptr[c1], ce = p.cam_chunk_ptr[c1 + 1];
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int ch = cb;
+    for (; ch + 3 < ce; ch += 4) {
+      a0 += p.cam_part[(size_t)ch * 256 + t];
+      a1 += p.cam_part[(size_t)(ch + 1) * 256 + t];
+      a2 += p.cam_part[(size_t)(ch + 2) * 256 + t];
+      a3 += p.cam_part[(size_t)(ch + 3) * 256 + t];
+    }
+    for (; ch < ce; ++ch) a0 += p.cam_part[(size_t)ch * 256 + t];
+    G[t] = (a0 + a1) + (a2 + a3);
+  }
+  {
+    const int g = t / 81, ent = t - g * 81;
+    if (g < 3) {
+      const int pb = p.block_chunk_ptr[blk], pe = p.block_chunk_ptr[blk + 1];
+      double a0 = 0.0, a1 = 0.0;
+      int ch = pb + g;
+      for (; ch + 3 < pe; ch += 6) {
+        a0 += p.pair_part[(size_t)ch * 81 + ent];
+        a1 += p.pair_part[(size_t)(ch + 3) * 81 + ent];
+      }
+      for (; ch < pe; ch += 3) a0 += p.pair_part[(size_t)ch * 81 + ent];
+      T3[g][ent] = a0 + a1;
+    }
   }
   __syncthreads();
   if (t < 81) {
-    double acc = 0.0;
-    for (int ch = p.block_chunk_ptr[blk]; ch < p.block_chunk_ptr[blk + 1]; ++ch)
-      acc += p.pair_part[(size_t)ch * 81 + t];
+    const double acc = (T3[0][t] + T3[1][t]) + T3[2][t];
     const int i = t / 9, j = t - i * 9;
     if (c1 == c2) {
       S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = G[i * 16 + j] - acc;
@@ -378,46 +434,66 @@ __global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
 }
 
 // ---------------------------------------------------------------- solve
-constexpr int kSolveWG = 1024;
-constexpr int kLdsMaxN = 120;  // 120*120*8 = 115 KB of LDS
-constexpr int kSolveHdr = 32;  // doubles of LDS header in k_solve
+// Reduced camera system S x = b, S SPD (damped).  LDL^T right-looking
+// elimination on packed lower-triangle storage ordered column by column from
+// the RIGHT: column j occupies [poff(j), poff(j) + n - j) with
+// poff(j) = (n-1-j)(n-j)/2, so at step k the trailing elements still to update
+// (columns > k) are exactly the prefix [0, poff(k)).  Forward substitution is
+// fused into the elimination (b is carried as an extra column), leaving one
+// workgroup barrier per column; back substitution is blocked by 16 rows (the
+// triangle by one wave, the rectangle by all waves).
+constexpr int kSolveWG = 512;
+constexpr int kLdsMaxN = 120;   // packed S + (i,j) table + rhs fit in LDS
+constexpr int kSolveHdr = 32;   // doubles of LDS header in k_solve
+constexpr int kBackNB = 16;
 
-// Right-looking Cholesky (lower) of the n x n matrix A (row stride ld) in
-// place, then solve A x = b (b overwritten with x).  Returns false if not SPD.
-__device__ bool chol_solve(double* A, int n, int ld, double* b, int* fail) {
-  const int t = threadIdx.x;
+__device__ __forceinline__ int poff(int n, int j) { return ((n - 1 - j) * (n - j)) >> 1; }
+
+template <int NT>
+__device__ bool ldl_solve(double* P, uint32_t* tab, int n, double* b, int* fail) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   for (int k = 0; k < n; ++k) {
-    if (t == 0) {
-      const double akk = A[(size_t)k * ld + k];
-      if (!(akk > 0.0) || !isfinite(akk)) *fail = 1;
-      A[(size_t)k * ld + k] = sqrt(fmax(akk, 1e-300));
+    const int ck = poff(n, k);
+    const double akk = P[ck];
+    if (!(akk > 0.0) || !isfinite(akk)) {
+      if (t == 0) *fail = 1;
+      return false;  // uniform: every thread read the same pivot
     }
-    __syncthreads();
-    if (*fail) return false;
-    const double dk = A[(size_t)k * ld + k];
-    for (int i = k + 1 + t; i < n; i += kSolveWG) A[(size_t)i * ld + k] /= dk;
-    __syncthreads();
-    const int m = n - k - 1;
-    for (int idx = t; idx < m * m; idx += kSolveWG) {
-      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-      if (j <= i) A[(size_t)i * ld + j] -= A[(size_t)i * ld + k] * A[(size_t)j * ld + k];
+    const double inv = 1.0 / akk;
+    const double bk = b[k];
+    for (int e = t; e < ck; e += NT) {
+      const uint32_t ij = tab[e];
+      const int i = (int)(ij >> 16), j = (int)(ij & 0xFFFFu);
+      P[e] -= P[ck + i - k] * P[ck + j - k] * inv;
     }
+    for (int i = k + 1 + t; i < n; i += NT) b[i] -= P[ck + i - k] * inv * bk;
     __syncthreads();
   }
-  // forward: L y = b
-  for (int k = 0; k < n; ++k) {
-    if (t == 0) b[k] /= A[(size_t)k * ld + k];
+  // z = D^-1 y
+  for (int i = t; i < n; i += NT) b[i] /= P[poff(n, i)];
+  __syncthreads();
+  // back substitution L^T x = z, L[i][r] = P(i, r) / D_r; blocks from the bottom
+  for (int hi = n; hi > 0; hi -= kBackNB) {
+    const int lo = max(0, hi - kBackNB);
+    if (wid == 0) {
+      for (int k = hi - 1; k >= lo; --k) {
+        const double xk = b[k];  // final
+        const int r = lo + lane;
+        if (r < k) {
+          const int cr = poff(n, r);
+          b[r] -= P[cr + k - r] / P[cr] * xk;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    }
     __syncthreads();
-    const double yk = b[k];
-    for (int i = k + 1 + t; i < n; i += kSolveWG) b[i] -= A[(size_t)i * ld + k] * yk;
-    __syncthreads();
-  }
-  // backward: L^T x = y
-  for (int k = n - 1; k >= 0; --k) {
-    if (t == 0) b[k] /= A[(size_t)k * ld + k];
-    __syncthreads();
-    const double xk = b[k];
-    for (int i = t; i < k; i += kSolveWG) b[i] -= A[(size_t)k * ld + i] * xk;
+    for (int r = t; r < lo; r += NT) {
+      const int cr = poff(n, r);
+      const double dr = P[cr];
+      double acc = 0.0;
+      for (int k = lo; k < hi; ++k) acc += P[cr + k - r] * b[k];
+      b[r] -= acc / dr;
+    }
     __syncthreads();
   }
   return true;
@@ -425,11 +501,12 @@ __device__ bool chol_solve(double* A, int n, int ld, double* b, int* fail) {
 
 __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
   // All LDS in the dynamic region (16-byte aligned base, Guideline 17):
-  // [0,16) block_sum scratch, [16] fail flag, [32, ...) A then x when in LDS.
+  // [0,16) block_sum scratch, [16] fail flag, [32, ...) packed S, rhs, (i,j) table.
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* red = lds;
   int* fail_p = reinterpret_cast<int*>(lds + 16);
   const int C9 = 9 * p.n_cams;
+  const int ne = C9 * (C9 + 1) / 2;
   const double* S = p.sys;
   const double* bvec = S + (size_t)C9 * C9;
   const double* gvec = bvec + C9;
@@ -439,18 +516,24 @@ __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
   const double lam = state[SLAM_BA_ST_LAMBDA];
   const int t = threadIdx.x;
   const bool in_lds = C9 <= kLdsMaxN;
-  double* A = in_lds ? lds + kSolveHdr : p.chol;
-  double* x = in_lds ? lds + kSolveHdr + (size_t)C9 * C9 : p.delta_c;
+  double* P = in_lds ? lds + kSolveHdr : p.chol;
+  double* x = in_lds ? P + ne : p.chol + ne;
+  uint32_t* tab = reinterpret_cast<uint32_t*>(x + C9);
   if (t == 0) *fail_p = 0;
-  for (int idx = t; idx < C9 * C9; idx += kSolveWG) {
-    const int i = idx / C9, j = idx - i * C9;
-    double a = S[idx];
-    if (i == j) a += lam * clampd(diagU[i]);
-    A[idx] = a;
+  // load the damped lower triangle in packed right-to-left column order
+  for (int j = 0; j < C9; ++j) {
+    const int cj = poff(C9, j);
+    for (int i = j + t; i < C9; i += kSolveWG) {
+      double a = S[(size_t)i * C9 + j];
+      if (i == j) a += lam * clampd(diagU[i]);
+      P[cj + i - j] = a;
+      tab[cj + i - j] = ((uint32_t)i << 16) | (uint32_t)j;
+    }
   }
   for (int i = t; i < C9; i += kSolveWG) x[i] = bvec[i];
   __syncthreads();
-  const bool ok = chol_solve(A, C9, C9, x, fail_p);
+  const bool ok = ldl_solve<kSolveWG>(P, tab, C9, x, fail_p);
+  __syncthreads();
   const int cur = cur_of(state);
   double pc = 0.0;
   for (int i = t; i < C9; i += kSolveWG) {
@@ -469,6 +552,26 @@ __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
   }
 }
 
+// Back substitution, split for parallelism: per observation dy_o = Y_o^T dc_cam(o)
+// (27 FMA), then per point dp = e - sum_o dy_o over its contiguous observations.
+__global__ __launch_bounds__(kBS) void k_obs_delta(slam_ba_problem p) {
+  const int o = blockIdx.x * kBS + threadIdx.x;
+  if (o >= p.n_obs) return;
+  const double* Y = p.wy + (size_t)o * 54 + 27;
+  const double* dc = p.delta_c + 9 * p.obs_cam[o];
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const double c = dc[i];
+    d0 += Y[3 * i] * c;
+    d1 += Y[3 * i + 1] * c;
+    d2 += Y[3 * i + 2] * c;
+  }
+  p.dy[3 * o] = d0;
+  p.dy[3 * o + 1] = d1;
+  p.dy[3 * o + 2] = d2;
+}
+
 __global__ __launch_bounds__(kBS) void k_backsub(slam_ba_problem p, double* __restrict__ part) {
   __shared__ double red[kBS / 64];
   const int pt = blockIdx.x * kBS + threadIdx.x;
@@ -476,16 +579,12 @@ __global__ __launch_bounds__(kBS) void k_backsub(slam_ba_problem p, double* __re
   const double lam = p.state[SLAM_BA_ST_LAMBDA];
   double pred = 0.0;
   if (pt < p.n_pts) {
-    const double* pd = p.ptdata + (size_t)pt * 12;
+    const double* pd = p.ptdata + (size_t)pt * kPtData;
     double d0 = pd[0], d1 = pd[1], d2 = pd[2];
     for (int o = p.pt_ptr[pt]; o < p.pt_ptr[pt + 1]; ++o) {
-      const double* Y = p.wy + (size_t)o * 54 + 27;
-      const double* dc = p.delta_c + 9 * p.obs_cam[o];
-      for (int i = 0; i < 9; ++i) {
-        d0 -= Y[3 * i] * dc[i];
-        d1 -= Y[3 * i + 1] * dc[i];
-        d2 -= Y[3 * i + 2] * dc[i];
-      }
+      d0 -= p.dy[3 * o];
+      d1 -= p.dy[3 * o + 1];
+      d2 -= p.dy[3 * o + 2];
     }
     const double* x = p.pts[cur] + 3 * pt;
     double* xn = p.pts[1 - cur] + 3 * pt;
@@ -516,10 +615,14 @@ __global__ __launch_bounds__(kBS) void k_trial_cost(slam_ba_problem p, double* _
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+__device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
+
 constexpr int kRedWG = 1024;
+template <bool DECIDE>
 __global__ __launch_bounds__(kRedWG) void k_reduce_small(const double* __restrict__ cost_part,
                                                          int n_cost, const double* __restrict__ pred_part,
-                                                         int n_pred, double* __restrict__ small) {
+                                                         int n_pred, double* __restrict__ small,
+                                                         double* __restrict__ state) {
   __shared__ double red[kRedWG / 64];
   double a = 0.0, b = 0.0;
   for (int i = threadIdx.x; i < n_cost; i += kRedWG) a += cost_part[i];
@@ -529,11 +632,15 @@ __global__ __launch_bounds__(kRedWG) void k_reduce_small(const double* __restric
   if (threadIdx.x == 0) {
     small[0] = a;
     small[1] = b;
+    if (DECIDE) lm_decide(state, small);
   }
 }
 
 __global__ void k_decide(double* __restrict__ state, const double* __restrict__ small) {
-  if (threadIdx.x != 0) return;
+  if (threadIdx.x == 0) lm_decide(state, small);
+}
+
+__device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small) {
   const double cost = state[SLAM_BA_ST_COST];
   const double cost_new = 0.5 * small[0];
   const double pred = state[SLAM_BA_ST_PRED_CAM] + 0.5 * small[1];
@@ -576,11 +683,14 @@ inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
 int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
   SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
-  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->rec && p->wy && p->sys && p->state && p->small &&
-                   p->red_part && p->delta_c,
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->rec && p->recc && p->wy && p->ptdata && p->dy &&
+                   p->obs_campos && p->sys && p->state && p->small && p->red_part && p->delta_c,
                "slam_ba: null buffer");
+  SLAM_REQUIRE(p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
+               "slam_ba: n_blocks must list all C(C+1)/2 upper blocks");
   SLAM_REQUIRE(9 * p->n_cams <= kLdsMaxN || p->chol != nullptr,
-               "slam_ba: chol workspace required for 9C > %d", kLdsMaxN);
+               "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
+               kLdsMaxN);
   return SLAM_OK;
 }
 
@@ -588,6 +698,12 @@ int check_problem(const slam_ba_problem* p) {
 
 extern "C" int slam_ba_red_slots(int n_pts, int n_obs) {
   return nblk(n_obs, kBS) + nblk(n_pts, kBS) + 1;
+}
+
+extern "C" long long slam_ba_chol_len(int n_cams) {
+  const long long c9 = 9ll * n_cams;
+  const long long ne = c9 * (c9 + 1) / 2;
+  return ne + c9 + (ne + 1) / 2;  // packed factor + rhs + (i,j) table (u32)
 }
 
 extern "C" long long slam_ba_sys_len(int n_cams) {
@@ -633,7 +749,7 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
   if (int rc = check_problem(prob)) return rc;
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
-  SLAM_HIP(hipMemsetAsync(p.sys, 0, sizeof(double) * slam_ba_sys_len(p.n_cams), s));
+  // every entry of sys is written by k_assemble (all upper blocks), so no clearing
   if (p.n_obs > 0) {
     k_linearize<<<nblk(p.n_obs, kBS), kBS, 0, s>>>(p);
     SLAM_LAUNCHED("k_linearize");
@@ -641,6 +757,10 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
   if (p.n_pts > 0) {
     k_points<<<nblk(p.n_pts, kBS), kBS, 0, s>>>(p);
     SLAM_LAUNCHED("k_points");
+  }
+  if (p.n_obs > 0) {
+    k_obs_wy<<<nblk(p.n_obs, kBS), kBS, 0, s>>>(p);
+    SLAM_LAUNCHED("k_obs_wy");
   }
   if (p.n_cam_chunks > 0) {
     k_cam_gram<<<p.n_cam_chunks, kGramWG, 0, s>>>(p);
@@ -650,24 +770,28 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
     k_pair_partials<<<p.n_pair_chunks, kPairWG, 0, s>>>(p);
     SLAM_LAUNCHED("k_pair_partials");
   }
-  if (p.n_blocks > 0) {
-    k_assemble<<<p.n_blocks, kBS, 0, s>>>(p);
-    SLAM_LAUNCHED("k_assemble");
-  }
+  k_assemble<<<p.n_blocks, kBS, 0, s>>>(p);
+  SLAM_LAUNCHED("k_assemble");
   return SLAM_OK;
 }
 
-extern "C" int slam_ba_solve_step(const slam_ba_problem* prob, void* stream) {
+static int solve_step(const slam_ba_problem* prob, bool fuse_decide, void* stream) {
   if (int rc = check_problem(prob)) return rc;
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
   const int C9 = 9 * p.n_cams;
-  const size_t lds = sizeof(double) * (kSolveHdr + (C9 <= kLdsMaxN ? (size_t)C9 * C9 + C9 : 0));
+  const size_t ne = (size_t)C9 * (C9 + 1) / 2;
+  const size_t lds = sizeof(double) * kSolveHdr +
+                     (C9 <= kLdsMaxN ? sizeof(double) * (ne + C9) + sizeof(uint32_t) * ne : 0);
   k_solve<<<1, kSolveWG, lds, s>>>(p);
   SLAM_LAUNCHED("k_solve");
   const int nb_cost = nblk(p.n_obs, kBS), nb_pts = nblk(p.n_pts, kBS);
   double* cost_part = p.red_part;
   double* pred_part = p.red_part + nb_cost;
+  if (p.n_obs > 0) {
+    k_obs_delta<<<nb_cost, kBS, 0, s>>>(p);
+    SLAM_LAUNCHED("k_obs_delta");
+  }
   if (p.n_pts > 0) {
     k_backsub<<<nb_pts, kBS, 0, s>>>(p, pred_part);
     SLAM_LAUNCHED("k_backsub");
@@ -676,9 +800,18 @@ extern "C" int slam_ba_solve_step(const slam_ba_problem* prob, void* stream) {
     k_trial_cost<<<nb_cost, kBS, 0, s>>>(p, cost_part);
     SLAM_LAUNCHED("k_trial_cost");
   }
-  k_reduce_small<<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small);
+  if (fuse_decide)
+    k_reduce_small<true><<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small,
+                                              p.state);
+  else
+    k_reduce_small<false><<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small,
+                                               p.state);
   SLAM_LAUNCHED("k_reduce_small");
   return SLAM_OK;
+}
+
+extern "C" int slam_ba_solve_step(const slam_ba_problem* prob, void* stream) {
+  return solve_step(prob, false, stream);
 }
 
 extern "C" int slam_ba_decide(const slam_ba_problem* prob, void* stream) {
@@ -691,8 +824,7 @@ extern "C" int slam_ba_decide(const slam_ba_problem* prob, void* stream) {
 extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream) {
   for (int i = 0; i < n_iter; ++i) {
     if (int rc = slam_ba_build_system(prob, stream)) return rc;
-    if (int rc = slam_ba_solve_step(prob, stream)) return rc;
-    if (int rc = slam_ba_decide(prob, stream)) return rc;
+    if (int rc = solve_step(prob, true, stream)) return rc;  // reduce + decide fused
   }
   return SLAM_OK;
 }

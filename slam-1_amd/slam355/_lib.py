@@ -31,7 +31,8 @@ class BAProblemStruct(ctypes.Structure):
         ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p),
         ("cam_obs", c_p), ("cam_chunks", c_p), ("cam_chunk_ptr", c_p),
         ("pair_o", c_p), ("pair_chunks", c_p), ("blocks", c_p), ("block_chunk_ptr", c_p),
-        ("rec", c_p), ("wy", c_p), ("ptdata", c_p), ("cam_part", c_p), ("pair_part", c_p),
+        ("obs_campos", c_p), ("rec", c_p), ("recc", c_p), ("wy", c_p), ("ptdata", c_p),
+        ("dy", c_p), ("cam_part", c_p), ("pair_part", c_p),
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
         ("state", c_p),
     ]
@@ -64,13 +65,15 @@ SIGNATURES = {
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_ba_red_slots": [c_int, c_int],
     "slam_ba_sys_len": [c_int],
+    "slam_ba_chol_len": [c_int],
     "slam_ba_build_system": [_PROB, c_p],
     "slam_ba_solve_step": [_PROB, c_p],
     "slam_ba_decide": [_PROB, c_p],
     "slam_ba_iterate": [_PROB, c_int, c_p],
     "slam_ba_reset": [_PROB, c_double, c_p],
 }
-_RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong}
+_RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
+            "slam_ba_chol_len": ctypes.c_longlong}
 
 
 class SlamError(RuntimeError):

@@ -50,9 +50,11 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
     pt_ptr = np.zeros(n_pts + 1, np.int64)
     np.cumsum(np.bincount(obs_pt, minlength=n_pts), out=pt_ptr[1:])
     cam_obs = np.argsort(obs_cam, kind="stable").astype(np.int32)
+    obs_campos = np.empty(O, np.int32)
+    obs_campos[cam_obs] = np.arange(O, dtype=np.int32)
+    # cameras without observations are allowed (a rank's shard may not see every
+    # camera); their blocks assemble to zeros and the damping keeps S definite
     cam_cnt = np.bincount(obs_cam, minlength=n_cams)
-    if (cam_cnt == 0).any():
-        raise ValueError(f"cameras without observations: {np.nonzero(cam_cnt == 0)[0][:8]}")
     cam_ptr = np.concatenate([[0], np.cumsum(cam_cnt)])
     chunks, cptr = [], [0]
     for c in range(n_cams):
@@ -82,15 +84,21 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
     o1, o2, bid = o1[so], o2[so], bid[so]
     ub, bstart = np.unique(bid, return_index=True)
     bend = np.append(bstart[1:], len(bid))
-    blocks = np.stack([ub // n_cams, ub % n_cams], 1).astype(np.int32)
+    # every upper block (c1 <= c2) gets a workgroup in k_assemble, so the whole
+    # of S is written each iteration; blocks with no common point have no chunks
+    c1, c2 = np.triu_indices(n_cams)
+    blocks = np.stack([c1, c2], 1).astype(np.int32)
+    span = dict(zip(ub.tolist(), zip(bstart.tolist(), bend.tolist())))
     pchunks, bptr = [], [0]
-    for k in range(len(ub)):
-        for b in range(bstart[k], bend[k], pair_chunk):
-            pchunks.append((k, b, min(b + pair_chunk, bend[k])))
+    for k, key in enumerate((c1.astype(np.int64) * n_cams + c2).tolist()):
+        if key in span:
+            lo, hi = span[key]
+            for b in range(lo, hi, pair_chunk):
+                pchunks.append((k, b, min(b + pair_chunk, hi)))
         bptr.append(len(pchunks))
     return dict(
         order=order, obs_cam=obs_cam, obs_pt=obs_pt, pt_ptr=pt_ptr.astype(np.int32),
-        cam_obs=cam_obs, cam_chunks=cam_chunks, cam_chunk_ptr=np.asarray(cptr, np.int32),
+        cam_obs=cam_obs, obs_campos=obs_campos, cam_chunks=cam_chunks, cam_chunk_ptr=np.asarray(cptr, np.int32),
         pair_o=np.stack([o1, o2], 1).astype(np.int32),
         pair_chunks=np.asarray(pchunks, np.int32).reshape(-1, 3), blocks=blocks,
         block_chunk_ptr=np.asarray(bptr, np.int32), n_obs=O)
@@ -115,20 +123,22 @@ class BAProblem:
         self.t = t = {}
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
-        for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
-                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr"):
+        for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "obs_campos", "cam_chunks",
+                  "cam_chunk_ptr", "pair_o", "pair_chunks", "blocks", "block_chunk_ptr"):
             arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
             t[k] = T(arr.astype(np.int32))
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
         O, C9 = self.O, 9 * C
         t["rec"] = z(O * 32)
+        t["recc"] = z(O * 32)
         t["wy"] = z(O * 54)
-        t["ptdata"] = z(P * 12)
+        t["ptdata"] = z(P * 16)
+        t["dy"] = z(O * 3)
         t["cam_part"] = z(len(pl["cam_chunks"]) * 256)
         t["pair_part"] = z(len(pl["pair_chunks"]) * 81)
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C))
         t["sys"] = z(self.sys_len)
-        t["chol"] = z(C9 * C9 if C9 > LDS_MAX_N else 1)
+        t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
         t["delta_c"] = z(C9)
         t["red_part"] = z(_lib.lib.slam_ba_red_slots(P, O))
         t["small"] = z(4)
@@ -142,8 +152,9 @@ class BAProblem:
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         for k in ("obs_cam", "obs_pt", "obs_q", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
-                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "rec", "wy", "ptdata",
-                  "cam_part", "pair_part", "sys", "chol", "delta_c", "red_part", "small", "state"):
+                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "obs_campos", "rec",
+                  "recc", "wy", "ptdata", "dy", "cam_part", "pair_part", "sys", "chol", "delta_c",
+                  "red_part", "small", "state"):
             setattr(s, k, t[k].data_ptr())
         self._s = s
         self.reset(lam0)

@@ -100,6 +100,17 @@ def test_planner_pairs_cover_schur_structure():
     assert ((cc[:, 2] - cc[:, 1]) <= 16).all()
     pc = pl["pair_chunks"]
     assert pc[0, 1] == 0 and pc[-1, 2] == len(o1) and (pc[1:, 1] == pc[:-1, 2]).all()
+    # camera-ordered record positions invert cam_obs; all 28 upper blocks listed
+    assert np.array_equal(pl["cam_obs"][pl["obs_campos"]], np.arange(len(ci)))
+    assert len(pl["blocks"]) == 7 * 8 // 2 and (pl["blocks"][:, 0] <= pl["blocks"][:, 1]).all()
+    bcp = pl["block_chunk_ptr"]
+    for k, (a, b) in enumerate(pl["blocks"]):
+        for ch in range(bcp[k], bcp[k + 1]):
+            lo, hi = pc[ch, 1], pc[ch, 2]
+            assert (pl["obs_cam"][o1[lo:hi]] == a).all() and (pl["obs_cam"][o2[lo:hi]] == b).all()
+    # a camera with no observations still plans (sharded problems)
+    pl2 = ba.plan(9, 200, ci, pi)
+    assert len(pl2["blocks"]) == 45 and pl2["cam_chunk_ptr"][-1] == pl2["cam_chunk_ptr"][-2]
 
 
 def test_bal_file_roundtrip(tmp_path):

@@ -1,0 +1,142 @@
+"""Multi-rank local BA: landmark sharding + summed reduced camera systems.
+
+CPU (gloo, world_size 2): the oracle's partial Schur systems of the two
+landmark shards, all-reduced, equal the single-process system.
+GPU (gloo on one device, world_size 2): BAProblem.step_distributed on two
+shards follows the single-process GPU LM iterates.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _problem():
+    from slam355.synthetic import ba_problem, perturb
+
+    rng = np.random.default_rng(21)
+    cams, pts, ci, pi, qs = ba_problem(rng, 8, 600, 4)
+    c0, p0 = perturb(rng, cams, pts)
+    return c0, p0, ci, pi, qs
+
+
+def _partial_system(c0, p0, ci, pi, qs, lam):
+    """Camera-block system of one shard: S (without camera damping), b, g, diagU."""
+    from oracle import ba as oba
+
+    C, P = len(c0), len(p0)
+    r, J = oba.residual_and_jacobian(c0, p0, ci, pi, qs)
+    Jc, Jp = J[:, :, :9], J[:, :, 9:]
+    U = np.zeros((C, 9, 9))
+    np.add.at(U, ci, np.einsum("oai,oaj->oij", Jc, Jc))
+    V = np.zeros((P, 3, 3))
+    np.add.at(V, pi, np.einsum("oai,oaj->oij", Jp, Jp))
+    gc = np.zeros((C, 9))
+    np.add.at(gc, ci, -np.einsum("oai,oa->oi", Jc, r))
+    gp = np.zeros((P, 3))
+    np.add.at(gp, pi, -np.einsum("oai,oa->oi", Jp, r))
+    Dp = np.clip(np.diagonal(V, axis1=1, axis2=2), 1e-6, 1e32)
+    Vi = np.linalg.inv(V + lam * Dp[:, :, None] * np.eye(3)[None])
+    W = np.einsum("oai,oaj->oij", Jc, Jp)
+    Y = np.einsum("oij,ojk->oik", W, Vi[pi])
+    S = np.zeros((C, C, 9, 9))
+    o1, o2 = oba._obs_pairs(ci, pi)
+    np.add.at(S, (ci[o1], ci[o2]), -np.einsum("oik,ojk->oij", Y[o1], W[o2]))
+    S = S + np.transpose(S, (1, 0, 3, 2)) * (1 - np.eye(C))[:, :, None, None]
+    S[np.arange(C), np.arange(C)] += U
+    b = gc.copy()
+    np.add.at(b, ci, -np.einsum("oij,oj->oi", Y, gp[pi]))
+    return np.concatenate([S.transpose(0, 2, 1, 3).ravel(), b.ravel(), gc.ravel(),
+                           np.diagonal(U, axis1=1, axis2=2).ravel()])
+
+
+def _cpu_worker(rank, world, port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "slam-1_amd")]
+    import torch
+    import torch.distributed as dist
+    from slam355.dist import shard_by_anchor
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    c0, p0, ci, pi, qs = _problem()
+    mine, keep, lpi = shard_by_anchor(len(c0), len(p0), ci, pi, rank, world)
+    sysv = torch.from_numpy(_partial_system(c0, p0[mine], ci[keep], lpi, qs[keep], 1e-3))
+    dist.all_reduce(sysv)
+    if rank == 0:
+        np.save(out, sysv.numpy())
+    dist.destroy_process_group()
+
+
+def test_gloo_sharded_system_equals_full(tmp_path):
+    c0, p0, ci, pi, qs = _problem()
+    full = _partial_system(c0, p0, ci, pi, qs, 1e-3)
+    out = str(tmp_path / "sys.npy")
+    mp.spawn(_cpu_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = np.load(out)
+    assert np.allclose(got, full, rtol=1e-9, atol=1e-9 * np.abs(full).max())
+
+
+def test_shards_partition_points_and_observations():
+    from slam355.dist import shard_by_anchor
+
+    c0, p0, ci, pi, qs = _problem()
+    masks = [shard_by_anchor(len(c0), len(p0), ci, pi, r, 3) for r in range(3)]
+    assert (sum(m[0].astype(int) for m in masks) == 1).all()
+    assert (sum(m[1].astype(int) for m in masks) == 1).all()
+
+
+def _gpu_worker(rank, world, port, out):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "slam-1_amd")]
+    import torch
+    import torch.distributed as dist
+    from slam355.ba import BAProblem
+    from slam355.dist import shard_by_anchor
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    c0, p0, ci, pi, qs = _problem()
+    mine, keep, lpi = shard_by_anchor(len(c0), len(p0), ci, pi, rank, world)
+    prob = BAProblem(c0, p0[mine], ci[keep], lpi, qs[keep])
+    costs = []
+    for _ in range(6):
+        prob.step_distributed()
+        costs.append(prob.state()["COST_NEW"])
+    cams, _ = prob.params()
+    if rank == 0:
+        np.savez(out, costs=np.array(costs), cams=cams)
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_step_distributed_matches_single_rank(tmp_path):
+    from slam355.ba import BAProblem
+
+    c0, p0, ci, pi, qs = _problem()
+    prob = BAProblem(c0, p0, ci, pi, qs)
+    costs = []
+    for _ in range(6):
+        prob.iterate(1)
+        costs.append(prob.state()["COST_NEW"])
+    cams, _ = prob.params()
+    out = str(tmp_path / "d.npz")
+    mp.spawn(_gpu_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    d = np.load(out)
+    assert np.allclose(d["costs"], costs, rtol=1e-8)
+    assert np.allclose(d["cams"], cams, rtol=1e-6, atol=1e-9)

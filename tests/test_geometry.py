@@ -171,10 +171,13 @@ def test_oracle_fundamental_lmeds_rejects_outliers():
     pl, pr = _stereo_points(0)
     mask, F, n, med = og.fundamental_lmeds(pl, pr, seed=1, item=3)
     assert mask[:90].sum() <= 3 and mask[90:].mean() > 0.9
-    # epipolar constraint holds on inliers (normalised algebraic residual small)
-    h1 = np.hstack([pl, np.ones((len(pl), 1))])
-    h2 = np.hstack([pr, np.ones((len(pr), 1))])
-    assert np.median(np.abs(np.einsum("ij,jk,ik->i", h2[mask], F, h1[mask]))) < 1e-2
+    # epipolar constraint holds on inliers: median point-to-epipolar-line distance
+    # in the right image at the 0.4 px noise level
+    h1 = np.hstack([pl, np.ones((len(pl), 1))])[mask]
+    h2 = np.hstack([pr, np.ones((len(pr), 1))])[mask]
+    lines = h1 @ F.T
+    d = np.abs(np.sum(lines * h2, 1)) / np.hypot(lines[:, 0], lines[:, 1])
+    assert np.median(d) < 1.0
     m2, F2, n2, _ = og.fundamental_lmeds(pl[:7], pr[:7])
     assert n2 == -1 and not m2.any()  # < 8 points: no model, nothing kept
 
