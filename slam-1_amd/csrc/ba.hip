@@ -499,44 +499,19 @@ __device__ bool ldl_solve(double* P, uint32_t* tab, int n, double* b, int* fail)
   return true;
 }
 
-__global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
-  // All LDS in the dynamic region (16-byte aligned base, Guideline 17):
-  // [0,16) block_sum scratch, [16] fail flag, [32, ...) packed S, rhs, (i,j) table.
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* red = lds;
-  int* fail_p = reinterpret_cast<int*>(lds + 16);
-  const int C9 = 9 * p.n_cams;
-  const int ne = C9 * (C9 + 1) / 2;
-  const double* S = p.sys;
-  const double* bvec = S + (size_t)C9 * C9;
+// Shared epilogue: camera step, trial cameras, predicted reduction of the camera
+// part, LM cost at the live parameters.
+__device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool ok, double* red) {
+  const int C9 = 9 * p.n_cams, t = threadIdx.x;
+  const double* bvec = p.sys + (size_t)C9 * C9;
   const double* gvec = bvec + C9;
   const double* diagU = gvec + C9;
   const double* costc = diagU + C9;
   double* state = p.state;
   const double lam = state[SLAM_BA_ST_LAMBDA];
-  const int t = threadIdx.x;
-  const bool in_lds = C9 <= kLdsMaxN;
-  double* P = in_lds ? lds + kSolveHdr : p.chol;
-  double* x = in_lds ? P + ne : p.chol + ne;
-  uint32_t* tab = reinterpret_cast<uint32_t*>(x + C9);
-  if (t == 0) *fail_p = 0;
-  // load the damped lower triangle in packed right-to-left column order
-  for (int j = 0; j < C9; ++j) {
-    const int cj = poff(C9, j);
-    for (int i = j + t; i < C9; i += kSolveWG) {
-      double a = S[(size_t)i * C9 + j];
-      if (i == j) a += lam * clampd(diagU[i]);
-      P[cj + i - j] = a;
-      tab[cj + i - j] = ((uint32_t)i << 16) | (uint32_t)j;
-    }
-  }
-  for (int i = t; i < C9; i += kSolveWG) x[i] = bvec[i];
-  __syncthreads();
-  const bool ok = ldl_solve<kSolveWG>(P, tab, C9, x, fail_p);
-  __syncthreads();
   const int cur = cur_of(state);
   double pc = 0.0;
-  for (int i = t; i < C9; i += kSolveWG) {
+  for (int i = t; i < C9; i += blockDim.x) {
     const double d = ok ? x[i] : 0.0;
     p.delta_c[i] = d;
     p.cams[1 - cur][i] = p.cams[cur][i] + d;
@@ -550,6 +525,330 @@ __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
     state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : 1.0;
   }
+}
+
+// Large systems (9C > kLdsMaxN): packed factor in global memory (p.chol).
+__global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* red = lds;
+  int* fail_p = reinterpret_cast<int*>(lds + 16);
+  const int C9 = 9 * p.n_cams;
+  const int ne = C9 * (C9 + 1) / 2;
+  const double* S = p.sys;
+  const double* bvec = S + (size_t)C9 * C9;
+  const double* diagU = bvec + 2 * C9;
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  const int t = threadIdx.x;
+  double* P = p.chol;
+  double* x = p.chol + ne;
+  uint32_t* tab = reinterpret_cast<uint32_t*>(x + C9);
+  if (t == 0) *fail_p = 0;
+  for (int j = 0; j < C9; ++j) {
+    const int cj = poff(C9, j);
+    for (int i = j + t; i < C9; i += kSolveWG) {
+      double a = S[(size_t)i * C9 + j];
+      if (i == j) a += lam * clampd(diagU[i]);
+      P[cj + i - j] = a;
+      tab[cj + i - j] = ((uint32_t)i << 16) | (uint32_t)j;
+    }
+  }
+  for (int i = t; i < C9; i += kSolveWG) x[i] = bvec[i];
+  __syncthreads();
+  const bool ok = ldl_solve<kSolveWG>(P, tab, C9, x, fail_p);
+  __syncthreads();
+  solve_epilogue(p, x, ok, red);
+}
+
+// -DSLAM_SOLVE_PROFILE: phase timestamps (wall_clock64, 100 MHz) of k_solve_blk
+// into the spare LM state slots 12..15 (ns): load, eliminate, back-substitute, epilogue.
+#ifdef SLAM_SOLVE_PROFILE
+#define SOLVE_PROF_T(i) uint64_t prof_t##i = wall_clock64()
+#define SOLVE_PROF_END()                                                        \
+  do {                                                                          \
+    const uint64_t prof_e = wall_clock64();                                     \
+    if (threadIdx.x == 0) {                                                     \
+      p.state[12] = 10.0 * (double)(prof_t1 - prof_t0);                         \
+      p.state[13] = 10.0 * (double)(prof_t2 - prof_t1);                         \
+      p.state[14] = 10.0 * (double)(prof_t3 - prof_t2);                         \
+      p.state[15] = 10.0 * (double)(prof_e - prof_t3);                          \
+    }                                                                           \
+  } while (0)
+#else
+#define SOLVE_PROF_T(i) (void)0
+#define SOLVE_PROF_END() (void)0
+#endif
+
+// Small systems (9C <= kLdsMaxN, the local-BA window): blocked LDL^T with the
+// trailing updates on the f64 matrix cores.
+//
+// The augmented matrix [S ; b^T] ((n+1) x n, b carried as row n so the
+// elimination also performs the forward substitution) is kept as 16x16 f64
+// MFMA accumulator tiles, lower tiles only, spread round-robin over the 4
+// waves (<= 36 tiles for n <= 120, <= 9 per wave).  One block step per camera
+// (9 columns):
+//   (a) the owners of the 9 panel columns copy them to LDS;        barrier
+//   (b) wave 0 factors the panel in registers, two rows per lane, pivot rows
+//       broadcast with v_readlane (no LDS round trips, no barriers); it writes
+//       W = -A_panel and L = A_panel D^-1 for the rows below the panel (zeros
+//       elsewhere) and the final factor columns;                    barrier
+//   (c) every wave updates its live tiles: T -= W_I L_J^T, 3 MFMAs
+//       (v_mfma_f64_16x16x4_f64, K = 9 padded to 12) per tile.
+// 2 barriers per camera instead of one per column.  Back substitution runs in
+// wave 0 with x in registers (two rows per lane) and x_k broadcast by readlane.
+constexpr int kBlkWG = 256;   // 4 waves, one per SIMD: 512 registers per lane
+constexpr int kBlkWaves = kBlkWG / 64;
+constexpr int kTileMax = 9;   // lower 16x16 tiles per wave: 4 * 9 >= 36
+constexpr int kPanelW = 9;    // columns per block step (one camera)
+constexpr int kWLs = 12;      // W/L row stride: K = 9 padded to 3 MFMA steps of 4
+static_assert(kBlkWaves * kTileMax >= ((kLdsMaxN + 16) / 16) * ((kLdsMaxN + 16) / 16 + 1) / 2,
+              "kTileMax too small");
+
+// 1/d from v_rcp_f64 refined by two Newton steps (full double precision, off
+// the v_div_* sequence's long dependent chain)
+__device__ __forceinline__ double rcp_f64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// LDS layout of k_solve_blk (doubles, after the kSolveHdr header)
+struct BlkLds {
+  int n16;        // rows rounded up to a tile multiple (>= n + 1)
+  int pn, wl, ll, lf, dd, yy, xx, total;
+  __host__ __device__ explicit BlkLds(int n) {
+    n16 = ((n + 1 + 15) / 16) * 16;
+    pn = kSolveHdr;                       // [n16][kPanelW] panel copy
+    wl = pn + n16 * kPanelW;              // [n16][kWLs] W = -A_panel (rows below the panel)
+    ll = wl + n16 * kWLs;                 // [n16][kWLs] L = A_panel D^-1
+    lf = ll + n16 * kWLs;                 // [n(n-1)/2] factor L, packed by rows
+    dd = lf + ((n * (n - 1) / 2 + 1) & ~1);  // [n] D
+    yy = dd + ((n + 1) & ~1);             // [n] y = L^-1 b
+    xx = yy + ((n + 1) & ~1);             // [n] solution
+    total = xx + ((n + 1) & ~1);
+  }
+};
+
+__global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* red = lds;
+  int* fail_p = reinterpret_cast<int*>(lds + 16);
+  const int n = 9 * p.n_cams;
+  const BlkLds g(n);
+  double* Pn = lds + g.pn;
+  double* WL = lds + g.wl;
+  double* LL = lds + g.ll;
+  double* LF = lds + g.lf;
+  double* Dd = lds + g.dd;
+  double* Yy = lds + g.yy;
+  double* X = lds + g.xx;
+  const double* S = p.sys;
+  const double* bvec = S + (size_t)n * n;
+  const double* diagU = bvec + 2 * n;
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int NT = g.n16 / 16, NL = NT * (NT + 1) / 2;
+  SOLVE_PROF_T(0);
+  if (t == 0) *fail_p = 0;
+  for (int i = t; i < 2 * g.n16 * kWLs; i += kBlkWG) WL[i] = 0.0;  // WL and LL
+  // this wave's tiles: tl = wid + 8 s -> (I, J), I >= J
+  int tI[kTileMax], tJ[kTileMax];
+  d4 acc[kTileMax];
+#pragma unroll
+  for (int s = 0; s < kTileMax; ++s) {
+    const int tl = wid + kBlkWaves * s;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= tl) ++I;
+    tI[s] = tl < NL ? I : -1;
+    tJ[s] = tl < NL ? tl - I * (I + 1) / 2 : -1;
+    const int col = tJ[s] * 16 + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = tI[s] * 16 + (lane >> 4) + 4 * q;
+      double a = 0.0;
+      if (tl < NL && col < n) {
+        if (row < n) {
+          a = S[(size_t)row * n + col];
+          if (row == col) a += lam * clampd(diagU[row]);
+        } else if (row == n) {
+          a = bvec[col];
+        }
+      }
+      acc[s][q] = a;
+    }
+  }
+  SOLVE_PROF_T(1);
+  bool ok = true;
+  for (int c0 = 0; c0 < n; c0 += kPanelW) {
+#ifdef SLAM_SOLVE_PROFILE_STEP
+    const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
+    // (a) panel columns [c0, c0 + 9), rows c0..n -> Pn[row - c0][col - c0]
+#pragma unroll
+    for (int s = 0; s < kTileMax; ++s) {
+      if (tI[s] < 0 || tJ[s] * 16 + 15 < c0 || tJ[s] * 16 >= c0 + kPanelW || tI[s] * 16 + 15 < c0)
+        continue;  // uniform per wave
+      const int col = tJ[s] * 16 + (lane & 15);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = tI[s] * 16 + (lane >> 4) + 4 * q;
+        if (col >= c0 && col < c0 + kPanelW && col <= row && row >= c0 && row <= n)
+          Pn[(row - c0) * kPanelW + (col - c0)] = acc[s][q];
+      }
+    }
+    __syncthreads();
+#ifdef SLAM_SOLVE_PROFILE_STEP
+    const uint64_t q1 = __builtin_amdgcn_s_memtime();
+#endif
+    // (b) panel factorisation.  Every participating wave factors the 9x9
+    // diagonal block A_KK = L_K D_K L_K^T redundantly (uniform values, no
+    // cross-lane traffic); then each lane takes one panel row r >= c0 and
+    // solves u = a L_K^-T (u_j = A^{(j)}(r, c0+j), the partially eliminated
+    // entry; for a row inside the panel, r = c0 + m, u_j = L(m, j) D_j for
+    // j < m and u_m = D_m) and l = u D_K^-1.  Rows c0+64w .. +63 go to wave w.
+    const int nw = (n - c0 + 1 + 63) >> 6;  // waves with rows (uniform)
+    if (wid < nw) {
+      double A[kPanelW][kPanelW];  // lower triangle of the diagonal block
+#pragma unroll
+      for (int m = 0; m < kPanelW; ++m)
+#pragma unroll
+        for (int i = 0; i <= m; ++i) A[m][i] = Pn[m * kPanelW + i];
+      const int r = c0 + 64 * wid + lane;
+      double u[kPanelW];
+      const double* pr = Pn + (r - c0) * kPanelW;
+#pragma unroll
+      for (int j = 0; j < kPanelW; ++j) u[j] = r <= n ? pr[j] : 0.0;
+      double Dinv[kPanelW];
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < kPanelW; ++j) {
+        const double d = A[j][j];
+        bad |= !(d > 0.0) || !isfinite(d);
+        Dinv[j] = rcp_f64(d);
+#pragma unroll
+        for (int m = j + 1; m < kPanelW; ++m) {
+          const double lmj = A[m][j] * Dinv[j];
+#pragma unroll
+          for (int i = j + 1; i <= m; ++i) A[m][i] = __builtin_fma(-lmj, A[i][j], A[m][i]);
+        }
+#pragma unroll
+        for (int m = j + 1; m < kPanelW; ++m) A[m][j] *= Dinv[j];  // L(m, j)
+      }
+      // right-looking row solve: 9 dependent levels instead of 36
+#pragma unroll
+      for (int i = 0; i < kPanelW; ++i)
+#pragma unroll
+        for (int j = i + 1; j < kPanelW; ++j) u[j] = __builtin_fma(-u[i], A[j][i], u[j]);
+      if (r <= n) {
+        double* wl = WL + r * kWLs;
+        double* ll = LL + r * kWLs;
+#pragma unroll
+        for (int j = 0; j < kPanelW; ++j) {
+          wl[j] = -u[j];
+          ll[j] = u[j] * Dinv[j];
+        }
+        if (r == n) {
+#pragma unroll
+          for (int j = 0; j < kPanelW; ++j) Yy[c0 + j] = u[j];
+        } else {
+          const int m = r - c0;  // >= 9 below the panel
+          double* lf = LF + r * (r - 1) / 2 + c0;
+#pragma unroll
+          for (int j = 0; j < kPanelW; ++j) {
+            if (j < m) lf[j] = u[j] * Dinv[j];
+            if (j == m) Dd[c0 + j] = u[j];
+          }
+        }
+      }
+      if (wid == 0 && lane == 0 && bad) *fail_p = 1;
+    }
+#ifdef SLAM_SOLVE_PROFILE_STEP
+    const uint64_t q2 = __builtin_amdgcn_s_memtime();
+#endif
+    __syncthreads();
+#ifdef SLAM_SOLVE_PROFILE_STEP
+    const uint64_t q3 = __builtin_amdgcn_s_memtime();
+#endif
+    if (*fail_p) {
+      ok = false;
+      break;
+    }
+    // (c) trailing update of the tiles right of / below the panel: operands of
+    // all live tiles loaded first, then the MFMAs interleaved across tiles
+    const int tr = c0 + kPanelW;
+    bool live[kTileMax];
+    double wa[kTileMax][3], lb[kTileMax][3];
+#pragma unroll
+    for (int s = 0; s < kTileMax; ++s) {
+      live[s] = tI[s] >= 0 && tJ[s] * 16 + 15 >= tr;  // uniform (I >= J)
+      if (!live[s]) continue;
+      const double* wrow = WL + (tI[s] * 16 + (lane & 15)) * kWLs + (lane >> 4);
+      const double* lrow = LL + (tJ[s] * 16 + (lane & 15)) * kWLs + (lane >> 4);
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) {
+        wa[s][kk] = wrow[4 * kk];
+        lb[s][kk] = lrow[4 * kk];
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+#pragma unroll
+      for (int s = 0; s < kTileMax; ++s)
+        if (live[s])
+          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[s][kk], lb[s][kk], acc[s], 0, 0, 0);
+    }
+#ifdef SLAM_SOLVE_PROFILE_STEP
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint64_t q4 = __builtin_amdgcn_s_memtime();
+    if (t == 0 && c0 == 9 * (n / 18)) {
+      p.state[12] = (double)(q1 - q0);
+      p.state[13] = (double)(q2 - q1);
+      p.state[14] = (double)(q3 - q2);
+      p.state[15] = (double)(q4 - q3);
+    }
+#endif
+  }
+  SOLVE_PROF_T(2);
+  if (ok && wid == 0) {
+    // z = D^-1 y, then L^T x = z from the bottom; lane l holds rows l, l + 64
+    double x0 = lane < n ? Yy[lane] / Dd[lane] : 0.0;
+    double x1 = lane + 64 < n ? Yy[lane + 64] / Dd[lane + 64] : 0.0;
+    // rows of L are loaded kBackU at a time ahead of the dependent x updates
+    constexpr int kBackU = 8;
+    for (int k = n - 1; k > 0; k -= kBackU) {
+      double l0[kBackU], l1[kBackU];
+#pragma unroll
+      for (int u = 0; u < kBackU; ++u) {
+        const int kk = max(k - u, 1);
+        const double* Lk = LF + kk * (kk - 1) / 2;  // L(kk, i), i < kk
+        l0[u] = lane < kk ? Lk[lane] : 0.0;
+        l1[u] = lane + 64 < kk ? Lk[lane + 64] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kBackU; ++u) {
+        const int kk = k - u;
+        if (kk <= 0) break;  // uniform
+        const double xk = kk < 64 ? readlane_d(x0, kk) : readlane_d(x1, kk - 64);
+        x0 = __builtin_fma(-l0[u], xk, x0);
+        x1 = __builtin_fma(-l1[u], xk, x1);
+      }
+    }
+    if (lane < n) X[lane] = x0;
+    if (lane + 64 < n) X[lane + 64] = x1;
+  }
+  __syncthreads();
+  SOLVE_PROF_T(3);
+  solve_epilogue(p, X, ok, red);
+  SOLVE_PROF_END();
 }
 
 // Back substitution, split for parallelism: per observation dy_o = Y_o^T dc_cam(o)
@@ -780,11 +1079,13 @@ static int solve_step(const slam_ba_problem* prob, bool fuse_decide, void* strea
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
   const int C9 = 9 * p.n_cams;
-  const size_t ne = (size_t)C9 * (C9 + 1) / 2;
-  const size_t lds = sizeof(double) * kSolveHdr +
-                     (C9 <= kLdsMaxN ? sizeof(double) * (ne + C9) + sizeof(uint32_t) * ne : 0);
-  k_solve<<<1, kSolveWG, lds, s>>>(p);
-  SLAM_LAUNCHED("k_solve");
+  if (C9 <= kLdsMaxN) {
+    k_solve_blk<<<1, kBlkWG, sizeof(double) * BlkLds(C9).total, s>>>(p);
+    SLAM_LAUNCHED("k_solve_blk");
+  } else {
+    k_solve<<<1, kSolveWG, sizeof(double) * kSolveHdr, s>>>(p);
+    SLAM_LAUNCHED("k_solve");
+  }
   const int nb_cost = nblk(p.n_obs, kBS), nb_pts = nblk(p.n_pts, kBS);
   double* cost_part = p.red_part;
   double* pred_part = p.red_part + nb_cost;

@@ -86,6 +86,11 @@ def _load():
             f"libslam355.so not found at {LIB_PATH}: build it with "
             "`make -C slam-1_amd` (or __graft_entry__.build()). slam355 has no CPU fallback."
         )
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 and the
+    # dynamic linker binds our DT_NEEDED to whichever copy is loaded first, so
+    # load torch's before ours (torch streams/allocations are passed straight in).
+    import torch  # noqa: F401
+
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -187,6 +187,27 @@ class BAProblem:
         """n LM iterations, no host synchronisation (single rank)."""
         _lib.call("slam_ba_iterate", ctypes.byref(self._s), int(n), self._sp())
 
+    def iterate_graphed(self, n: int = 1):
+        """n LM iterations replayed from a captured HIP graph (one launch for
+        the 13n kernels; captured on first use for each n)."""
+        graphs = self.__dict__.setdefault("_graphs", {})
+        if n not in graphs:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()  # capture needs a non-default stream
+            s.wait_stream(torch.cuda.current_stream())
+            saved = self.stream
+            self.stream = s
+            try:
+                with torch.cuda.graph(g, stream=s):
+                    self.iterate(n)
+            finally:
+                self.stream = saved
+            torch.cuda.current_stream().wait_stream(s)
+            graphs[n] = g
+        with torch.cuda.stream(self.stream if self.stream is not None else
+                               torch.cuda.current_stream()):
+            graphs[n].replay()
+
     def step_distributed(self, group=None):
         """One LM iteration with RCCL all-reduce of the camera system (multi-rank)."""
         import torch.distributed as dist
