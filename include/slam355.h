@@ -217,7 +217,7 @@ typedef struct slam_ba_problem {
   int32_t n_blocks;      /* upper camera-pair blocks of S: C(C+1)/2            */
   int32_t n_pair_chunks; /* Schur work items                                 */
   int32_t n_pairs;
-  int32_t reserved;
+  int32_t n_grps;        /* point groups (>= 1): <= 128 obs each, whole points */
   double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
   double* pts[2];               /* [P][3]                                      */
   const int32_t* obs_cam;       /* [O] (sorted by point, then camera)          */
@@ -232,23 +232,23 @@ typedef struct slam_ba_problem {
   const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2), every upper block */
   const int32_t* block_chunk_ptr; /* [n_blocks+1] (empty range: no common point) */
   const int32_t* obs_campos;    /* [O] position of obs o in cam_obs            */
-  double* rec;                  /* [O][2][16] Jc(9) r u Jp(3) 0 0 (by point)   */
+  const int32_t* grp_ptr;       /* [n_grps+1] point range of each point group  */
   double* recc;                 /* [O][2][16] Jc(9) r u 0.. (camera order)     */
   double* wy;                   /* [O][54] W = Jc^T Jp (9x3), Y = W V*^-1       */
-  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) V*^-1(6) -        */
-  double* dy;                   /* [O][3] Y_o^T dc back-substitution terms     */
+  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) -                 */
   double* cam_part;             /* [n_cam_chunks][256] Gram partials           */
   double* pair_part;            /* [n_pair_chunks][81] Schur partials          */
   double* sys;                  /* S[(9C)^2] b[9C] g[9C] diagU[9C] cost[C]     */
   double* chol;                 /* [slam_ba_chol_len] (9C > 120 only)           */
   double* delta_c;              /* [9C]                                        */
-  double* red_part;             /* [slam_ba_red_slots(P, O)]                   */
+  double* red_part;             /* [slam_ba_red_slots(n_grps)]                 */
   double* small;                /* [4] trial |r|^2, sum pred_p (all-reduced)   */
   double* state;                /* [SLAM_BA_ST_SLOTS]                          */
+  uint32_t* ticket;             /* [1] zero-initialised completion counter     */
 } slam_ba_problem;
 
-/* Number of doubles red_part needs for a problem of P points and O obs. */
-int slam_ba_red_slots(int n_pts, int n_obs);
+/* Number of doubles red_part needs for a problem with n_grps point groups. */
+int slam_ba_red_slots(int n_grps);
 /* Doubles of the factorisation workspace `chol` (needed only when 9C > 120). */
 long long slam_ba_chol_len(int n_cams);
 /* Doubles in the all-reduced system buffer: (9C)^2 + 27C + C. */

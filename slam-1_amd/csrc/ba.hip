@@ -5,19 +5,20 @@
 // and scipy least_squares TRF) with LM on the normal equations, all state on
 // the device so a fixed number of iterations runs with no host round trip.
 //
-// One LM iteration = 10 launches:
-//   k_linearize     obs    -> rec[o] = [Jc(9) r u Jp(3) 0 0] per residual row
-//   k_points        point  -> V*_p, e_p = V*^-1 g_p, W_o = Jc^T Jp, Y_o = W_o V*^-1,
-//                             u_o = Jp e_p (written into rec column 10)
+// One LM iteration = 6 launches (local BA):
+//   k_point_lin     point group -> residuals + Jacobians, camera-ordered Gram
+//                                  record [Jc | r | u], V*_p, e_p = V*^-1 g_p,
+//                                  W_o = Jc^T Jp, Y_o = W_o V*^-1, u_o = Jp e_p
 //   k_cam_gram      chunk  -> f64 MFMA Gram  G = M^T M, M = [Jc | r | u] (2 rows/obs)
 //   k_pair_partials chunk  -> sum over obs pairs of Y_o1 W_o2^T (Schur terms)
 //   k_assemble      block  -> S = blockdiag(U) - sum(Y W^T), b = -Jc^T r - Jc^T u, ...
 //   (all-reduce of sys over ranks happens here for multi-GPU)
-//   k_solve         1 WG   -> damp, Cholesky, camera step, pred_cam, trial cameras
-//   k_backsub       point  -> point step, trial points, pred_p partials
-//   k_trial_cost    obs    -> |r(x+delta)|^2 partials
-//   k_reduce_small  1 WG   -> small = {sum r^2, sum pred_p}
-//   (all-reduce of small over ranks)
+//   k_solve_blk     1 WG   -> damp, blocked LDL^T (MFMA trailing updates), camera
+//                             step, pred_cam, trial cameras (k_solve for 9C > 120)
+//   k_back_trial    point group -> point step, trial points, trial |r|^2 and
+//                                  pred partials; the last group sums them into
+//                                  small (and, single rank, decides)
+//   (all-reduce of small over ranks, then k_decide)
 //   k_decide        1 lane -> rho, accept/reject, lambda update, buffer swap
 #include "common.hpp"
 
@@ -193,116 +194,108 @@ __device__ __forceinline__ int cur_of(const double* state) {
   return state[SLAM_BA_ST_CUR] != 0.0 ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kBS) void k_linearize(slam_ba_problem p) {
-  const int o = blockIdx.x * kBS + threadIdx.x;
-  if (o >= p.n_obs) return;
-  const int cur = cur_of(p.state);
-  double r[2], J[2][12];
-  reproject<true>(p.cams[cur] + 9 * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o], p.obs_q + 2 * o,
-                  r, J);
-  clamp_rows<true>(r, J);
-  // point-ordered record (k_points / k_obs_wy) and camera-ordered record (k_cam_gram)
-  double* rec = p.rec + (size_t)o * 2 * kRecW;
-  double* recc = p.recc + (size_t)p.obs_campos[o] * 2 * kRecW;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    double row[kRecW];
-    for (int k = 0; k < 9; ++k) row[k] = J[a][k];
-    row[9] = r[a];
-    row[10] = 0.0;
-    row[11] = J[a][9];
-    row[12] = J[a][10];
-    row[13] = J[a][11];
-    row[14] = 0.0;
-    row[15] = 0.0;
-    double2* d0 = reinterpret_cast<double2*>(rec + a * kRecW);
-    double2* d1 = reinterpret_cast<double2*>(recc + a * kRecW);
-#pragma unroll
-    for (int k = 0; k < kRecW / 2; ++k) {
-      const double2 v = make_double2(row[2 * k], row[2 * k + 1]);
-      d0[k] = v;
-      d1[k] = k < 5 ? v : make_double2(0.0, 0.0);  // M = [Jc | r | u | 0 ...]
-    }
-  }
-}
-
 __device__ __forceinline__ double clampd(double d) { return fmin(fmax(d, kDiagMin), kDiagMax); }
 
-constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) V*^-1 (6, symmetric) pad
+constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) pad
+// Point groups: a workgroup owns the contiguous observation range of a group
+// of whole points (observations are sorted by point), at most kGrp of them.
+constexpr int kGrp = 128;
 
-// Per point: V = sum Jp^T Jp, g = -Jp^T r, V* = V + lam diag, V*^-1, e = V*^-1 g.
-__global__ __launch_bounds__(kBS) void k_points(slam_ba_problem p) {
-  const int pt = blockIdx.x * kBS + threadIdx.x;
-  if (pt >= p.n_pts) return;
-  const double lam = p.state[SLAM_BA_ST_LAMBDA];
-  const int b = p.pt_ptr[pt], e = p.pt_ptr[pt + 1];
-  double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
-  for (int o = b; o < e; ++o) {
-    const double* rec = p.rec + (size_t)o * 2 * kRecW;
+// Linearisation + point elimination, one workgroup per point group:
+//   per observation: residual and 2x12 Jacobian (BundleAdjustment.py:317-350
+//     + analytic derivative), the camera-ordered Gram record [Jc | r | u];
+//   per point: V = sum Jp^T Jp, g = -sum Jp^T r, V* = V + lam diag(V),
+//     V*^-1 (cofactors), e = V*^-1 g;
+//   per observation: W = Jc^T Jp, Y = W V*^-1, u = Jp e.
+// Jp and r go through LDS between the phases; Jc stays in registers.
+__global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
+  __shared__ double sJ[kGrp][9];   // Jp row 0 (3), Jp row 1 (3), r (2), pad
+  __shared__ double sP[kGrp][10];  // e (3), V*^-1 (6), pad
+  const int g = blockIdx.x;
+  const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
+  const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
+  const int t = threadIdx.x;
+  const int o = o0 + t;
+  const bool has = o < o1;
+  const int cur = cur_of(p.state);
+  double r[2], J[2][12];
+  double* recc = p.recc + (size_t)(has ? p.obs_campos[o] : 0) * 2 * kRecW;
+  if (has) {
+    reproject<true>(p.cams[cur] + 9 * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o],
+                    p.obs_q + 2 * o, r, J);
+    clamp_rows<true>(r, J);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      const double* row = rec + a * kRecW;
-      const double j0 = row[11], j1 = row[12], j2 = row[13], rr = row[9];
-      V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
-      V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
-      g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
+      double2* d = reinterpret_cast<double2*>(recc + a * kRecW);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = make_double2(J[a][2 * k], J[a][2 * k + 1]);
+      d[4] = make_double2(J[a][8], r[a]);
+      // col 10 (u) is written after the point phase; cols 11..15 stay zero
+      d[5] = make_double2(0.0, 0.0);
+      d[6] = make_double2(0.0, 0.0);
+      d[7] = make_double2(0.0, 0.0);
+      sJ[t][3 * a] = J[a][9];
+      sJ[t][3 * a + 1] = J[a][10];
+      sJ[t][3 * a + 2] = J[a][11];
+      sJ[t][6 + a] = r[a];
     }
   }
-  const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
-  const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
-  const double a01 = V01, a02 = V02, a12 = V12;
-  const double c00 = a11 * a22 - a12 * a12;
-  const double c01 = a02 * a12 - a01 * a22;
-  const double c02 = a01 * a12 - a02 * a11;
-  const double c11 = a00 * a22 - a02 * a02;
-  const double c12 = a01 * a02 - a00 * a12;
-  const double c22 = a00 * a11 - a01 * a01;
-  const double det = a00 * c00 + a01 * c01 + a02 * c02;
-  const double id = det != 0.0 ? 1.0 / det : 0.0;
-  const double i00 = c00 * id, i01 = c01 * id, i02 = c02 * id;
-  const double i11 = c11 * id, i12 = c12 * id, i22 = c22 * id;
-  double* pd = p.ptdata + (size_t)pt * kPtData;
-  pd[0] = i00 * g0 + i01 * g1 + i02 * g2;
-  pd[1] = i01 * g0 + i11 * g1 + i12 * g2;
-  pd[2] = i02 * g0 + i12 * g1 + i22 * g2;
-  pd[3] = g0; pd[4] = g1; pd[5] = g2;
-  pd[6] = d0; pd[7] = d1; pd[8] = d2;
-  pd[9] = i00; pd[10] = i01; pd[11] = i02; pd[12] = i11; pd[13] = i12; pd[14] = i22;
-}
-
-// Per observation: W = Jc^T Jp (9x3), Y = W V*^-1, u = Jp e (into both records, col 10).
-__global__ __launch_bounds__(kBS) void k_obs_wy(slam_ba_problem p) {
-  const int o = blockIdx.x * kBS + threadIdx.x;
-  if (o >= p.n_obs) return;
-  double* rec = p.rec + (size_t)o * 2 * kRecW;
-  const double* pd = p.ptdata + (size_t)p.obs_pt[o] * kPtData;
-  const double Vi[3][3] = {{pd[9], pd[10], pd[11]}, {pd[10], pd[12], pd[13]},
-                           {pd[11], pd[13], pd[14]}};
-  const double e0 = pd[0], e1 = pd[1], e2 = pd[2];
-  double r0[kRecW], r1[kRecW];
+  __syncthreads();
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  if (t < p1 - p0) {
+    const int pt = p0 + t;
+    double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+    for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
 #pragma unroll
-  for (int k = 0; k < kRecW; ++k) {
-    r0[k] = rec[k];
-    r1[k] = rec[kRecW + k];
+      for (int a = 0; a < 2; ++a) {
+        const double j0 = sJ[k][3 * a], j1 = sJ[k][3 * a + 1], j2 = sJ[k][3 * a + 2];
+        const double rr = sJ[k][6 + a];
+        V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
+        V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
+        g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
+      }
+    }
+    const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
+    const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
+    const double a01 = V01, a02 = V02, a12 = V12;
+    const double c00 = a11 * a22 - a12 * a12;
+    const double c01 = a02 * a12 - a01 * a22;
+    const double c02 = a01 * a12 - a02 * a11;
+    const double c11 = a00 * a22 - a02 * a02;
+    const double c12 = a01 * a02 - a00 * a12;
+    const double c22 = a00 * a11 - a01 * a01;
+    const double det = a00 * c00 + a01 * c01 + a02 * c02;
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    const double i00 = c00 * id, i01 = c01 * id, i02 = c02 * id;
+    const double i11 = c11 * id, i12 = c12 * id, i22 = c22 * id;
+    const double e0 = i00 * g0 + i01 * g1 + i02 * g2;
+    const double e1 = i01 * g0 + i11 * g1 + i12 * g2;
+    const double e2 = i02 * g0 + i12 * g1 + i22 * g2;
+    double* pd = p.ptdata + (size_t)pt * kPtData;
+    pd[0] = e0; pd[1] = e1; pd[2] = e2;
+    pd[3] = g0; pd[4] = g1; pd[5] = g2;
+    pd[6] = d0; pd[7] = d1; pd[8] = d2;
+    sP[t][0] = e0; sP[t][1] = e1; sP[t][2] = e2;
+    sP[t][3] = i00; sP[t][4] = i01; sP[t][5] = i02;
+    sP[t][6] = i11; sP[t][7] = i12; sP[t][8] = i22;
   }
+  __syncthreads();
+  if (!has) return;
+  const double* sp = sP[p.obs_pt[o] - p0];
+  const double Vi[3][3] = {{sp[3], sp[4], sp[5]}, {sp[4], sp[6], sp[7]}, {sp[5], sp[7], sp[8]}};
   double* wy = p.wy + (size_t)o * 54;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     double W[3];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) W[c] = r0[i] * r0[11 + c] + r1[i] * r1[11 + c];
+    for (int c = 0; c < 3; ++c) W[c] = J[0][i] * J[0][9 + c] + J[1][i] * J[1][9 + c];
 #pragma unroll
     for (int c = 0; c < 3; ++c) wy[i * 3 + c] = W[c];
 #pragma unroll
     for (int c = 0; c < 3; ++c) wy[27 + i * 3 + c] = W[0] * Vi[0][c] + W[1] * Vi[1][c] + W[2] * Vi[2][c];
   }
-  const double u0 = r0[11] * e0 + r0[12] * e1 + r0[13] * e2;
-  const double u1 = r1[11] * e0 + r1[12] * e1 + r1[13] * e2;
-  rec[10] = u0;
-  rec[kRecW + 10] = u1;
-  double* recc = p.recc + (size_t)p.obs_campos[o] * 2 * kRecW;
-  recc[10] = u0;
-  recc[kRecW + 10] = u1;
+  recc[10] = J[0][9] * sp[0] + J[0][10] * sp[1] + J[0][11] * sp[2];
+  recc[kRecW + 10] = J[1][9] * sp[0] + J[1][10] * sp[1] + J[1][11] * sp[2];
 }
 
 // f64 MFMA Gram of M = [Jc | r | u | 0...] over one chunk of a camera's
@@ -851,87 +844,97 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
   SOLVE_PROF_END();
 }
 
-// Back substitution, split for parallelism: per observation dy_o = Y_o^T dc_cam(o)
-// (27 FMA), then per point dp = e - sum_o dy_o over its contiguous observations.
-__global__ __launch_bounds__(kBS) void k_obs_delta(slam_ba_problem p) {
-  const int o = blockIdx.x * kBS + threadIdx.x;
-  if (o >= p.n_obs) return;
-  const double* Y = p.wy + (size_t)o * 54 + 27;
-  const double* dc = p.delta_c + 9 * p.obs_cam[o];
-  double d0 = 0.0, d1 = 0.0, d2 = 0.0;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const double c = dc[i];
-    d0 += Y[3 * i] * c;
-    d1 += Y[3 * i + 1] * c;
-    d2 += Y[3 * i + 2] * c;
-  }
-  p.dy[3 * o] = d0;
-  p.dy[3 * o + 1] = d1;
-  p.dy[3 * o + 2] = d2;
-}
+__device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
 
-__global__ __launch_bounds__(kBS) void k_backsub(slam_ba_problem p, double* __restrict__ part) {
-  __shared__ double red[kBS / 64];
-  const int pt = blockIdx.x * kBS + threadIdx.x;
+// Back substitution + trial cost, one workgroup per point group:
+//   per observation: dy_o = Y_o^T dc_cam(o)                         (-> LDS)
+//   per point: dp = e - sum_o dy_o, trial point x + dp, predicted-reduction term
+//   per observation: trial residual at (cams[next], trial point)   (-> |r|^2)
+// Workgroup partial sums go to part[g] (cost) and part[G + g] (pred); the
+// last workgroup to finish (agent-scope ticket) sums them in a fixed order into
+// small[0..1] and, when DECIDE (single rank), applies the LM decision.
+template <bool DECIDE>
+__global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* __restrict__ part) {
+  __shared__ double sdy[kGrp][3];
+  __shared__ double snp[kGrp][3];
+  __shared__ double red[kGrp / 64];
+  __shared__ int last;
+  const int g = blockIdx.x, G = gridDim.x;
+  const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
+  const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
+  const int t = threadIdx.x;
+  const int o = o0 + t;
+  const bool has = o < o1;
   const int cur = cur_of(p.state);
-  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  const bool fail = p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0;
+  if (has) {
+    const double* Y = p.wy + (size_t)o * 54 + 27;
+    const double* dc = p.delta_c + 9 * p.obs_cam[o];
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const double c = dc[i];
+      d0 += Y[3 * i] * c;
+      d1 += Y[3 * i + 1] * c;
+      d2 += Y[3 * i + 2] * c;
+    }
+    sdy[t][0] = d0;
+    sdy[t][1] = d1;
+    sdy[t][2] = d2;
+  }
+  __syncthreads();
   double pred = 0.0;
-  if (pt < p.n_pts) {
+  if (t < p1 - p0) {
+    const int pt = p0 + t;
+    const double lam = p.state[SLAM_BA_ST_LAMBDA];
     const double* pd = p.ptdata + (size_t)pt * kPtData;
     double d0 = pd[0], d1 = pd[1], d2 = pd[2];
-    for (int o = p.pt_ptr[pt]; o < p.pt_ptr[pt + 1]; ++o) {
-      d0 -= p.dy[3 * o];
-      d1 -= p.dy[3 * o + 1];
-      d2 -= p.dy[3 * o + 2];
+    for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
+      d0 -= sdy[k][0];
+      d1 -= sdy[k][1];
+      d2 -= sdy[k][2];
     }
     const double* x = p.pts[cur] + 3 * pt;
     double* xn = p.pts[1 - cur] + 3 * pt;
-    xn[0] = x[0] + d0;
-    xn[1] = x[1] + d1;
-    xn[2] = x[2] + d2;
+    snp[t][0] = xn[0] = x[0] + d0;
+    snp[t][1] = xn[1] = x[1] + d1;
+    snp[t][2] = xn[2] = x[2] + d2;
     pred = d0 * (lam * pd[6] * d0 + pd[3]) + d1 * (lam * pd[7] * d1 + pd[4]) +
            d2 * (lam * pd[8] * d2 + pd[5]);
-    if (p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0) pred = 0.0;
+    if (fail) pred = 0.0;
   }
-  const double s = block_sum(pred, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
-}
-
-__global__ __launch_bounds__(kBS) void k_trial_cost(slam_ba_problem p, double* __restrict__ part) {
-  __shared__ double red[kBS / 64];
-  const int o = blockIdx.x * kBS + threadIdx.x;
-  const int nxt = 1 - cur_of(p.state);
+  __syncthreads();
   double v = 0.0;
-  if (o < p.n_obs) {
+  if (has) {
     double r[2], J[2][12];
-    reproject<false>(p.cams[nxt] + 9 * p.obs_cam[o], p.pts[nxt] + 3 * p.obs_pt[o],
-                     p.obs_q + 2 * o, r, J);
+    reproject<false>(p.cams[1 - cur] + 9 * p.obs_cam[o], snp[p.obs_pt[o] - p0], p.obs_q + 2 * o,
+                     r, J);
     clamp_rows<false>(r, J);
     v = r[0] * r[0] + r[1] * r[1];
   }
-  const double s = block_sum(v, red);
-  if (threadIdx.x == 0) part[blockIdx.x] = s;
-}
-
-__device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
-
-constexpr int kRedWG = 1024;
-template <bool DECIDE>
-__global__ __launch_bounds__(kRedWG) void k_reduce_small(const double* __restrict__ cost_part,
-                                                         int n_cost, const double* __restrict__ pred_part,
-                                                         int n_pred, double* __restrict__ small,
-                                                         double* __restrict__ state) {
-  __shared__ double red[kRedWG / 64];
+  v = block_sum(v, red);
+  pred = block_sum(pred, red);
+  if (t == 0) {
+    part[g] = v;
+    part[G + g] = pred;
+    __threadfence();  // release the partials (agent scope) before the ticket
+    last = atomicAdd(p.ticket, 1u) == (unsigned)(G - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire the other workgroups' partials
   double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < n_cost; i += kRedWG) a += cost_part[i];
-  for (int i = threadIdx.x; i < n_pred; i += kRedWG) b += pred_part[i];
+  for (int i = t; i < G; i += kGrp) {
+    a += __builtin_nontemporal_load(part + i);
+    b += __builtin_nontemporal_load(part + G + i);
+  }
   a = block_sum(a, red);
   b = block_sum(b, red);
-  if (threadIdx.x == 0) {
-    small[0] = a;
-    small[1] = b;
-    if (DECIDE) lm_decide(state, small);
+  if (t == 0) {
+    p.small[0] = a;
+    p.small[1] = b;
+    *p.ticket = 0u;  // re-arm for the next launch (stream order)
+    if (DECIDE) lm_decide(p.state, p.small);
   }
 }
 
@@ -982,9 +985,11 @@ inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
 int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
   SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
-  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->rec && p->recc && p->wy && p->ptdata && p->dy &&
-                   p->obs_campos && p->sys && p->state && p->small && p->red_part && p->delta_c,
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->recc && p->wy && p->ptdata && p->obs_campos &&
+                   p->grp_ptr && p->ticket && p->sys && p->state && p->small && p->red_part &&
+                   p->delta_c,
                "slam_ba: null buffer");
+  SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
   SLAM_REQUIRE(p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
                "slam_ba: n_blocks must list all C(C+1)/2 upper blocks");
   SLAM_REQUIRE(9 * p->n_cams <= kLdsMaxN || p->chol != nullptr,
@@ -995,9 +1000,7 @@ int check_problem(const slam_ba_problem* p) {
 
 }  // namespace
 
-extern "C" int slam_ba_red_slots(int n_pts, int n_obs) {
-  return nblk(n_obs, kBS) + nblk(n_pts, kBS) + 1;
-}
+extern "C" int slam_ba_red_slots(int n_grps) { return 2 * n_grps; }
 
 extern "C" long long slam_ba_chol_len(int n_cams) {
   const long long c9 = 9ll * n_cams;
@@ -1049,18 +1052,8 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
   // every entry of sys is written by k_assemble (all upper blocks), so no clearing
-  if (p.n_obs > 0) {
-    k_linearize<<<nblk(p.n_obs, kBS), kBS, 0, s>>>(p);
-    SLAM_LAUNCHED("k_linearize");
-  }
-  if (p.n_pts > 0) {
-    k_points<<<nblk(p.n_pts, kBS), kBS, 0, s>>>(p);
-    SLAM_LAUNCHED("k_points");
-  }
-  if (p.n_obs > 0) {
-    k_obs_wy<<<nblk(p.n_obs, kBS), kBS, 0, s>>>(p);
-    SLAM_LAUNCHED("k_obs_wy");
-  }
+  k_point_lin<<<p.n_grps, kGrp, 0, s>>>(p);
+  SLAM_LAUNCHED("k_point_lin");
   if (p.n_cam_chunks > 0) {
     k_cam_gram<<<p.n_cam_chunks, kGramWG, 0, s>>>(p);
     SLAM_LAUNCHED("k_cam_gram");
@@ -1086,28 +1079,11 @@ static int solve_step(const slam_ba_problem* prob, bool fuse_decide, void* strea
     k_solve<<<1, kSolveWG, sizeof(double) * kSolveHdr, s>>>(p);
     SLAM_LAUNCHED("k_solve");
   }
-  const int nb_cost = nblk(p.n_obs, kBS), nb_pts = nblk(p.n_pts, kBS);
-  double* cost_part = p.red_part;
-  double* pred_part = p.red_part + nb_cost;
-  if (p.n_obs > 0) {
-    k_obs_delta<<<nb_cost, kBS, 0, s>>>(p);
-    SLAM_LAUNCHED("k_obs_delta");
-  }
-  if (p.n_pts > 0) {
-    k_backsub<<<nb_pts, kBS, 0, s>>>(p, pred_part);
-    SLAM_LAUNCHED("k_backsub");
-  }
-  if (p.n_obs > 0) {
-    k_trial_cost<<<nb_cost, kBS, 0, s>>>(p, cost_part);
-    SLAM_LAUNCHED("k_trial_cost");
-  }
   if (fuse_decide)
-    k_reduce_small<true><<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small,
-                                              p.state);
+    k_back_trial<true><<<p.n_grps, kGrp, 0, s>>>(p, p.red_part);
   else
-    k_reduce_small<false><<<1, kRedWG, 0, s>>>(cost_part, nb_cost, pred_part, nb_pts, p.small,
-                                               p.state);
-  SLAM_LAUNCHED("k_reduce_small");
+    k_back_trial<false><<<p.n_grps, kGrp, 0, s>>>(p, p.red_part);
+  SLAM_LAUNCHED("k_back_trial");
   return SLAM_OK;
 }
 
@@ -1125,7 +1101,7 @@ extern "C" int slam_ba_decide(const slam_ba_problem* prob, void* stream) {
 extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream) {
   for (int i = 0; i < n_iter; ++i) {
     if (int rc = slam_ba_build_system(prob, stream)) return rc;
-    if (int rc = solve_step(prob, true, stream)) return rc;  // reduce + decide fused
+    if (int rc = solve_step(prob, true, stream)) return rc;  // decide fused into the last group
   }
   return SLAM_OK;
 }

@@ -26,15 +26,15 @@ class BAProblemStruct(ctypes.Structure):
     """Mirror of `slam_ba_problem` (include/slam355.h)."""
     _fields_ = [
         ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_cam_chunks", c_i32),
-        ("n_blocks", c_i32), ("n_pair_chunks", c_i32), ("n_pairs", c_i32), ("reserved", c_i32),
+        ("n_blocks", c_i32), ("n_pair_chunks", c_i32), ("n_pairs", c_i32), ("n_grps", c_i32),
         ("cams", c_p * 2), ("pts", c_p * 2),
         ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p),
         ("cam_obs", c_p), ("cam_chunks", c_p), ("cam_chunk_ptr", c_p),
         ("pair_o", c_p), ("pair_chunks", c_p), ("blocks", c_p), ("block_chunk_ptr", c_p),
-        ("obs_campos", c_p), ("rec", c_p), ("recc", c_p), ("wy", c_p), ("ptdata", c_p),
-        ("dy", c_p), ("cam_part", c_p), ("pair_part", c_p),
+        ("obs_campos", c_p), ("grp_ptr", c_p), ("recc", c_p), ("wy", c_p), ("ptdata", c_p),
+        ("cam_part", c_p), ("pair_part", c_p),
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
-        ("state", c_p),
+        ("state", c_p), ("ticket", c_p),
     ]
 
 
@@ -63,7 +63,7 @@ SIGNATURES = {
     "slam_filter_pairs": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_ba_residual": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p],
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
-    "slam_ba_red_slots": [c_int, c_int],
+    "slam_ba_red_slots": [c_int],
     "slam_ba_sys_len": [c_int],
     "slam_ba_chol_len": [c_int],
     "slam_ba_build_system": [_PROB, c_p],

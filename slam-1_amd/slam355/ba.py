@@ -41,6 +41,31 @@ def _check_indices(n_cams, n_pts, cam_idx, pt_idx, qs):
 
 
 # ----------------------------------------------------------------------------- planner
+GROUP_OBS = 128  # kGrp in csrc/ba.hip: observations (and points) per point group
+
+
+def point_groups(pt_ptr, cap=GROUP_OBS):
+    """Greedy cut of the point-sorted observation list into groups of whole
+    points with <= cap observations each -> grp_ptr [G+1] (point indices).
+    At least one (possibly empty) group."""
+    pt_ptr = np.asarray(pt_ptr, np.int64)
+    P = len(pt_ptr) - 1
+    cnt = np.diff(pt_ptr)
+    if P and cnt.max() > cap:
+        raise ValueError(f"a point has {int(cnt.max())} observations (> {cap} per point group)")
+    starts = [0]
+    base = 0
+    for p in range(P):
+        if pt_ptr[p + 1] - pt_ptr[base] > cap or p - base >= cap:
+            starts.append(p)
+            base = p
+    if P:
+        starts.append(P)
+    else:
+        starts.append(0)
+    return np.asarray(starts, np.int32)
+
+
 def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
     """Index tables for the LM kernels (host numpy, once per problem structure)."""
     O = len(cam_idx)
@@ -96,8 +121,10 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
             for b in range(lo, hi, pair_chunk):
                 pchunks.append((k, b, min(b + pair_chunk, hi)))
         bptr.append(len(pchunks))
+    grp_ptr = point_groups(pt_ptr, GROUP_OBS)
     return dict(
         order=order, obs_cam=obs_cam, obs_pt=obs_pt, pt_ptr=pt_ptr.astype(np.int32),
+        grp_ptr=grp_ptr,
         cam_obs=cam_obs, obs_campos=obs_campos, cam_chunks=cam_chunks, cam_chunk_ptr=np.asarray(cptr, np.int32),
         pair_o=np.stack([o1, o2], 1).astype(np.int32),
         pair_chunks=np.asarray(pchunks, np.int32).reshape(-1, 3), blocks=blocks,
@@ -124,23 +151,24 @@ class BAProblem:
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
         for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "obs_campos", "cam_chunks",
-                  "cam_chunk_ptr", "pair_o", "pair_chunks", "blocks", "block_chunk_ptr"):
+                  "cam_chunk_ptr", "pair_o", "pair_chunks", "blocks", "block_chunk_ptr",
+                  "grp_ptr"):
             arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
             t[k] = T(arr.astype(np.int32))
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
         O, C9 = self.O, 9 * C
-        t["rec"] = z(O * 32)
         t["recc"] = z(O * 32)
         t["wy"] = z(O * 54)
         t["ptdata"] = z(P * 16)
-        t["dy"] = z(O * 3)
         t["cam_part"] = z(len(pl["cam_chunks"]) * 256)
         t["pair_part"] = z(len(pl["pair_chunks"]) * 81)
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C))
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
         t["delta_c"] = z(C9)
-        t["red_part"] = z(_lib.lib.slam_ba_red_slots(P, O))
+        G = len(pl["grp_ptr"]) - 1
+        t["red_part"] = z(_lib.lib.slam_ba_red_slots(G))
+        t["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
         t["small"] = z(4)
         t["state"] = z(N_STATE)
         s = _Prob()
@@ -149,12 +177,13 @@ class BAProblem:
         s.n_blocks = len(pl["blocks"])
         s.n_pair_chunks = len(pl["pair_chunks"])
         s.n_pairs = len(pl["pair_o"])
+        s.n_grps = G
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         for k in ("obs_cam", "obs_pt", "obs_q", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
-                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "obs_campos", "rec",
-                  "recc", "wy", "ptdata", "dy", "cam_part", "pair_part", "sys", "chol", "delta_c",
-                  "red_part", "small", "state"):
+                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "obs_campos", "grp_ptr",
+                  "recc", "wy", "ptdata", "cam_part", "pair_part", "sys", "chol", "delta_c",
+                  "red_part", "small", "state", "ticket"):
             setattr(s, k, t[k].data_ptr())
         self._s = s
         self.reset(lam0)

@@ -108,6 +108,13 @@ def test_planner_pairs_cover_schur_structure():
         for ch in range(bcp[k], bcp[k + 1]):
             lo, hi = pc[ch, 1], pc[ch, 2]
             assert (pl["obs_cam"][o1[lo:hi]] == a).all() and (pl["obs_cam"][o2[lo:hi]] == b).all()
+    # point groups: whole points, <= 128 obs each, covering every point once
+    gp = pl["grp_ptr"]
+    assert gp[0] == 0 and gp[-1] == 200 and (np.diff(gp) > 0).all()
+    assert (pl["pt_ptr"][gp[1:]] - pl["pt_ptr"][gp[:-1]] <= ba.GROUP_OBS).all()
+    assert np.array_equal(ba.point_groups(np.array([0])), [0, 0])
+    with pytest.raises(ValueError):
+        ba.point_groups(np.array([0, 200]))
     # a camera with no observations still plans (sharded problems)
     pl2 = ba.plan(9, 200, ci, pi)
     assert len(pl2["blocks"]) == 45 and pl2["cam_chunk_ptr"][-1] == pl2["cam_chunk_ptr"][-2]
