@@ -48,9 +48,9 @@ int slam_device_count(void);
  *
  * Replaces cv2.FlannBasedMatcher(LSH).knnMatch(des_q, des_t, k=2) followed by
  * the `m.distance < 0.7 * n.distance` loop:
- *   /root/reference/keypoint.py:83-94   (track_keypoints_left_to_right_new)
- *   /root/reference/Point3D.py:199-213  (find_2D_and_3D_correspondenses)
- *   /root/reference/tracking.py:231-247 (get_matches)
+ *   /root/reference/keypoint.py:40-51   (track_keypoints_left_to_right_new)
+ *   /root/reference/Point3D.py:35-49  (find_2D_and_3D_correspondenses)
+ *   /root/reference/tracking.py:14-30 (get_matches)
  * Exact search (FLANN-LSH is approximate).  Ties are broken by
  * the lower train index, as cv::BFMatcher does.
  *
@@ -63,7 +63,7 @@ int slam_device_count(void);
  *   d_good  [batch][q_cap]    u8   1 iff both exist and 10*d1 < 7*d2
  * (`10*d1 < 7*d2` == `d1 < 0.7*d2` for every integer d1, d2 in [0, 256].)
  * A train set with fewer than 2 rows yields no good matches, mirroring the
- * reference's ValueError truncation (keypoint.py:89-94).
+ * reference's ValueError truncation (keypoint.py:46-51).
  * t_cap must be <= 65535.
  * ---------------------------------------------------------------------- */
 int slam_hamming_knn2(const uint8_t* d_q, const int32_t* d_nq, int q_cap,
@@ -73,8 +73,8 @@ int slam_hamming_knn2(const uint8_t* d_q, const int32_t* d_nq, int q_cap,
 
 /* Order-preserving compaction of the good matches of slam_hamming_knn2:
  * d_pairs [batch][q_cap][2] i32 = (queryIdx, trainIdx) of the good rows in
- * query order (the `good` list of keypoint.py:90-92), d_count [batch] i32.
- * Optional extra gate (Point3D.py:209-210): if d_gate_xyz != NULL, a good
+ * query order (the `good` list of keypoint.py:47-49), d_count [batch] i32.
+ * Optional extra gate (Point3D.py:45-46): if d_gate_xyz != NULL, a good
  * row q is kept only if |X[q][k]| < gate for k = 0,1,2, where
  * d_gate_xyz [batch][q_cap][3] f64. */
 int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,
@@ -87,7 +87,7 @@ int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,
  * Geometry of one tracking step (main.py:82-97), batched over frame pairs.
  * ---------------------------------------------------------------------- */
 
-/* Gather of matched keypoints (keypoint.py:96-100, Point3D.py:214-216):
+/* Gather of matched keypoints (keypoint.py:53-57, Point3D.py:50-52):
  * for k < count[b], (qi, ti) = pairs[b][k]:
  *   ptq[b][k] = (double)kpq[b][qi].xy, ptt[b][k] = (double)kpt[b][ti].xy,
  *   dq[b][k] = desq[b][qi], dt[b][k] = dest[b][ti]  (descriptors optional: NULL).
@@ -97,7 +97,7 @@ int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int 
                         const int32_t* d_count, int p_cap, int batch, double* d_ptq,
                         double* d_ptt, uint8_t* d_dq, uint8_t* d_dt, void* stream);
 
-/* 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:214-216):
+/* 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:50-52):
  * for k < count[b], (qi, ti) = pairs[b][k]: Q1[b][k] = X[b][qi], q1[b][k] =
  * ptl[b][qi], q2[b][k] = (double)kp_next[b][ti].xy.  X [batch][xcap][3],
  * ptl [batch][xcap][2] f64; kp_next [batch][kcap][5] f32. */
@@ -105,7 +105,7 @@ int slam_gather_temporal(const double* d_X, const double* d_ptl, int xcap, const
                          int kcap, const int32_t* d_pairs, const int32_t* d_count, int pcap,
                          int batch, double* d_Q1, double* d_q2, double* d_q1, void* stream);
 
-/* cv2.findFundamentalMat(pts_left, pts_right, FM_LMEDS) mask (keypoint.py:102-109),
+/* cv2.findFundamentalMat(pts_left, pts_right, FM_LMEDS) mask (keypoint.py:59-66),
  * deterministic LMedS restated in oracle/fundamental.c: n_hyp seeded 7-point
  * hypotheses (300 = OpenCV's LMeDS count at confidence 0.99), min median of
  * the symmetric epipolar error, inliers err <= sigma^2 with OpenCV's robust
@@ -116,7 +116,7 @@ int slam_fundamental_lmeds(const double* d_m1, const double* d_m2, const int32_t
                            uint8_t* d_mask, double* d_F, int32_t* d_ninliers, void* stream);
 
 /* Order-preserving compaction of pairs[b][k] (k < count[b]) where mask[b][k] != 0
- * (the `pts_left[mask]` of keypoint.py:106-109). d_out must not alias d_pairs. */
+ * (the `pts_left[mask]` of keypoint.py:63-66). d_out must not alias d_pairs. */
 int slam_filter_pairs(const int32_t* d_pairs, const int32_t* d_count, const uint8_t* d_mask,
                       int cap, int batch, int32_t* d_out, int32_t* d_out_count, void* stream);
 

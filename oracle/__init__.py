@@ -5,7 +5,7 @@ this package, and only as the checker / CPU baseline.  The product path
 (slam-1_amd/slam355) never imports it and has no CPU fallback.
 
 Contents:
-  * liboracle.so (C, gcc -ffp-contract=off): hamming.c, orb.c, ba.c
+  * liboracle.so (C, gcc -ffp-contract=off): hamming.c, orb.c, geometry.c (PnP), fundamental.c
   * ba.py        numpy restatement of the BAL objective (BundleAdjustment.py:287-394)
   * geometry.py  numpy restatement of triangulation / PnP / pose chain
 Every function cites the reference file:line it follows.  Pinning: see
@@ -109,7 +109,7 @@ def hamming_knn2_pylist(q: np.ndarray, t: np.ndarray):
     """Pure-Python/numpy restatement for small cases (cross-checks the C oracle).
 
     Sort each query's candidates by (distance, train index) — the order
-    cv::BFMatcher returns — and take the first two (keypoint.py:87).
+    cv::BFMatcher returns — and take the first two (keypoint.py:44).
     """
     q = np.asarray(q, np.uint8).reshape(-1, 32)
     t = np.asarray(t, np.uint8).reshape(-1, 32)

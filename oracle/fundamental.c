@@ -2,7 +2,7 @@
  * ORACLE — test infrastructure only (see oracle/__init__.py).
  *
  * CPU restatement of the stereo outlier filter of the reference:
- *   /root/reference/keypoint.py:102-109
+ *   /root/reference/keypoint.py:59-66
  *     F, mask = cv2.findFundamentalMat(pts_left, pts_right, cv2.FM_LMEDS)
  *     pts_left = pts_left[mask] ...
  * OpenCV (absent here; PARITY UNPINNED vs OpenCV) runs LMeDS over random

@@ -4,13 +4,13 @@
  * CPU baseline, never as the product path.
  *
  * Exact brute-force Hamming kNN-2 + Lowe ratio, a CPU restatement of what
- *   /root/reference/keypoint.py:83-94  (FlannBasedMatcher.knnMatch(k=2) + `m.distance < 0.7*n.distance`)
- *   /root/reference/Point3D.py:199-213 (same, plus the |Q| < max_Distance gate)
+ *   /root/reference/keypoint.py:40-51  (FlannBasedMatcher.knnMatch(k=2) + `m.distance < 0.7*n.distance`)
+ *   /root/reference/Point3D.py:35-49 (same, plus the |Q| < max_Distance gate)
  * compute, with FLANN-LSH replaced by exact search.
  * Tie rule: equal distances are ordered by ascending train index
  * (cv::BFMatcher's stable order), so the best is the lowest-index minimum.
  * A train set with < 2 rows gives no good matches (ValueError truncation,
- * keypoint.py:89-94).
+ * keypoint.py:46-51).
  */
 #include <stdint.h>
 #include <string.h>

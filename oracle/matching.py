@@ -1,10 +1,10 @@
 """ORACLE (test infrastructure only): numpy restatement of the reference's
 post-processing around knnMatch(k=2), driven by the exact C kNN-2 oracle.
 
-  stereo_matches   /root/reference/keypoint.py:78-109 (F-LMedS mask excluded:
+  stereo_matches   /root/reference/keypoint.py:35-66 (F-LMedS mask excluded:
                    pass `mask` explicitly; the golden uses an all-inlier mask)
-  temporal_matches /root/reference/Point3D.py:197-218
-  get_matches      /root/reference/tracking.py:229-251
+  temporal_matches /root/reference/Point3D.py:33-53
+  get_matches      /root/reference/tracking.py:12-34
 """
 from __future__ import annotations
 
@@ -14,7 +14,7 @@ from . import hamming_knn2
 
 
 def good_pairs(des_q, des_t):
-    """The `good` list (keypoint.py:88-94) as an (M, 2) int array of (queryIdx, trainIdx).
+    """The `good` list (keypoint.py:45-51) as an (M, 2) int array of (queryIdx, trainIdx).
 
     With an exact matcher every query has 2 neighbours iff len(des_t) >= 2; with
     fewer, the first `for m, n in matches` unpack raises ValueError and the
@@ -26,7 +26,7 @@ def good_pairs(des_q, des_t):
 
 
 def stereo_matches(pts_l, des_l, pts_r, des_r, mask=None):
-    """keypoint.py:87-109 -> (pts_left f64 [M,2], pts_right, des_left u8 [M,32], des_right)."""
+    """keypoint.py:44-66 -> (pts_left f64 [M,2], pts_right, des_left u8 [M,32], des_right)."""
     p = good_pairs(des_l, des_r)
     pts_left = np.asarray(pts_l, np.float32)[p[:, 0]].astype(np.float64)
     pts_right = np.asarray(pts_r, np.float32)[p[:, 1]].astype(np.float64)
@@ -39,7 +39,7 @@ def stereo_matches(pts_l, des_l, pts_r, des_r, mask=None):
 
 
 def temporal_matches(des_i, pts_i, pts_i1, des_i1, Q, max_Distance=1000):
-    """Point3D.py:197-218 -> (q2 [L,2] f64 from kp_{i+1}.pt, Q1 [L,3], q1 [L,2])."""
+    """Point3D.py:33-53 -> (q2 [L,2] f64 from kp_{i+1}.pt, Q1 [L,3], q1 [L,2])."""
     p = good_pairs(des_i, des_i1)
     Q = np.asarray(Q, np.float64)
     if len(p):
@@ -52,7 +52,7 @@ def temporal_matches(des_i, pts_i, pts_i1, des_i1, Q, max_Distance=1000):
 
 
 def get_matches(pts1, des1, pts2, des2):
-    """tracking.py:229-251 -> float32 (q1, q2)."""
+    """tracking.py:12-34 -> float32 (q1, q2)."""
     p = good_pairs(des1, des2)
     return (np.asarray(pts1, np.float32)[p[:, 0]].reshape(-1, 2),
             np.asarray(pts2, np.float32)[p[:, 1]].reshape(-1, 2))

@@ -1,7 +1,7 @@
 // Fundamental-matrix LMedS outlier mask for gfx950, batched over frame pairs.
 //
 // Replaces cv2.findFundamentalMat(pts_left, pts_right, cv2.FM_LMEDS) and the
-// mask application of /root/reference/keypoint.py:102-109, following the
+// mask application of /root/reference/keypoint.py:59-66, following the
 // deterministic spec of oracle/fundamental.c (300 seeded 7-point hypotheses,
 // Hartley-normalised Gauss-Jordan null space, cubic roots, float errors,
 // min-median selection, OpenCV's robust sigma for the final inlier mask).

@@ -1,7 +1,7 @@
 // Matched-point gather, DLT triangulation and RANSAC + LM PnP for gfx950.
 //
 // Replaces, per frame pair of the tracking loop (/root/reference/main.py:82-97):
-//   keypoint.py:96-100        gather of matched points (f64) and descriptors
+//   keypoint.py:53-57        gather of matched points (f64) and descriptors
 //   Point3D.py:14-19          cv2.triangulatePoints (per-point 4x4 SVD null vector)
 //   transformation.py:5-19    cv2.solvePnPRansac(Q, q, K, 0) (ITERATIVE flavour:
 //                             minimal 5-point LM hypotheses, 8 px reprojection
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kBS) void k_gather(const float* __restrict__ kpq, i
   }
 }
 
-// 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:214-216):
+// 2D-3D correspondences of find_2D_and_3D_correspondenses (Point3D.py:50-52):
 // Q1 = X[qi], q1 = ptl[qi] (tracked left points at t), q2 = kp_next[ti].xy.
 __global__ __launch_bounds__(kBS) void k_gather_temporal(
     const double* __restrict__ X, const double* __restrict__ ptl, int xcap,

@@ -1,7 +1,7 @@
 // Brute-force Hamming kNN-2 matcher + Lowe ratio test, gfx950.
 //
 // Replaces cv2.FlannBasedMatcher(LSH).knnMatch(k=2) + the 0.7 ratio loop of
-// /root/reference/keypoint.py:83-94, Point3D.py:199-213, tracking.py:231-247.
+// /root/reference/keypoint.py:40-51, Point3D.py:35-49, tracking.py:14-30.
 //
 // Design (integer-VALU bound, see DESIGN.md "Hamming matcher"):
 //   * one workgroup = 256 lanes x QPL queries of ONE batch item; each lane keeps

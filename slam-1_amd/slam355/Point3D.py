@@ -45,7 +45,7 @@ def _pts(kps):
 def find_2D_and_3D_correspondenses(descriptors_time_i, keypoints_left_time_i,
                                    keypoints_left_time_i1, descriptors_left_time_i1,
                                    triangulated_3D_points, max_Distance=1000):
-    """(Point3D.py:33-54) -> (q2 [L,2] f64, Q1 [L,3] f64, q1 [L,2])."""
+    """(Point3D.py:33-53) -> (q2 [L,2] f64, Q1 [L,3] f64, q1 [L,2])."""
     dq = np.ascontiguousarray(descriptors_time_i, np.uint8).reshape(-1, 32)
     dt = np.ascontiguousarray(descriptors_left_time_i1, np.uint8).reshape(-1, 32)
     Q = np.asarray(triangulated_3D_points, np.float64).reshape(-1, 3)

@@ -30,7 +30,7 @@ def gather_matches(kpq, kpt, pairs, count, desq=None, dest=None, out=None, strea
 
 
 def gather_temporal(X, ptl, kp_next, pairs, count, out=None, stream=None):
-    """-> (Q1 [B,p,3], q2 [B,p,2], q1 [B,p,2]) f64 (Point3D.py:214-216)."""
+    """-> (Q1 [B,p,3], q2 [B,p,2], q1 [B,p,2]) f64 (Point3D.py:50-52)."""
     B, pcap, _ = pairs.shape
     dev = pairs.device
     if out is None:

@@ -1,7 +1,7 @@
 """Exact Hamming kNN-2 matcher on the GPU (replaces FLANN-LSH knnMatch(k=2)).
 
-Reference call sites: /root/reference/keypoint.py:83-94,
-/root/reference/Point3D.py:199-213, /root/reference/tracking.py:231-247.
+Reference call sites: /root/reference/keypoint.py:40-51,
+/root/reference/Point3D.py:35-49, /root/reference/tracking.py:14-30.
 """
 from __future__ import annotations
 

@@ -20,7 +20,7 @@ from .device import ptr, require_gpu, stream_ptr, to_dev
 
 class KeyPoint:
     """Stand-in for cv2.KeyPoint: the reference reads only `.pt`
-    (keypoint.py:96-97, Point3D.py:216, orb.py:8-9); size/angle/response/octave
+    (keypoint.py:53-54, Point3D.py:52, orb.py:8-9); size/angle/response/octave
     carry the ORB values."""
 
     __slots__ = ("pt", "size", "angle", "response", "octave")

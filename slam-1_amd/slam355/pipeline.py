@@ -3,9 +3,9 @@
 
 The reference processes one frame pair per Python iteration:
   ORB(right_i), ORB(left_{i+1})                       main.py:79-80
-  stereo kNN-2 + ratio + F-LMedS mask                 main.py:82-84 (keypoint.py:78-109)
+  stereo kNN-2 + ratio + F-LMedS mask                 main.py:82-84 (keypoint.py:35-66)
   triangulate                                         main.py:86 (Point3D.py:14-19)
-  temporal kNN-2 + ratio + |Q| gate                   main.py:88-90 (Point3D.py:33-54)
+  temporal kNN-2 + ratio + |Q| gate                   main.py:88-90 (Point3D.py:33-53)
   PnP-RANSAC, sign flip, pose chaining                main.py:94-98, 120-124
 Every step depends only on frames (i, i+1), so `Tracker.track` runs B frame
 pairs per call as 13 kernel launches on one stream, with all intermediate
@@ -99,14 +99,14 @@ class Tracker:
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
         nL, nR = cnt[0:B], cnt[B + 1:2 * B + 1]
         kpL1, dL1, nL1 = kp[1:B + 1], desc[1:B + 1], cnt[1:B + 1]
-        # stereo: kNN-2 + ratio (keypoint.py:87-94), gather (:96-97)
+        # stereo: kNN-2 + ratio (keypoint.py:44-51), gather (:96-97)
         matcher.knn2_batch(dL, nL, dR, nR, out=(self.s_idx2, self.s_dist2, self.s_good), stream=st)
         matcher.compact_matches(self.s_idx2, self.s_good, nL, out=(self.s_pairs, self.s_cnt),
                                 stream=st)
         geometry.gather_matches(kpL, kpR, self.s_pairs, self.s_cnt,
                                 out=(self.s_ptl, self.s_ptr, None, None), stream=st)
         mark("stereo_match")
-        # F-LMedS mask (keypoint.py:102-109), then the surviving pairs with descriptors
+        # F-LMedS mask (keypoint.py:59-66), then the surviving pairs with descriptors
         geometry.fundamental_lmeds(self.s_ptl, self.s_ptr, self.s_cnt, seed=self.seed,
                                    item0=frame0, out=(self.f_mask, self.f_F, self.f_ninl),
                                    stream=st)

@@ -12,8 +12,8 @@ What is pinned, and how:
     `bundle_adjustment_sparsity` pattern (:380-394) and `least_squares`
     results (:397-402) at the reference's settings (ftol=0.1) and at tight
     tolerances (the optimum the GPU LM must reach).
-  * Matching post-processing (/root/reference/Point3D.py:197-218,
-    keypoint.py:78-123, tracking.py:229-251) imported with a stub `cv2`
+  * Matching post-processing (/root/reference/Point3D.py:33-53,
+    keypoint.py:35-80, tracking.py:12-34) imported with a stub `cv2`
     module.  cv2 (OpenCV) is absent from this image (ModuleNotFoundError, not a
     permission denial).  The stub provides an EXACT brute-force knnMatch
     (ties -> lower train index, cv::BFMatcher order), an all-inlier
@@ -165,7 +165,7 @@ def perturb(rng, cams, X, rot_s=1e-3, t_s=1e-2, p_s=0.05):
 def make_matcher_goldens(Point3D, keypoint, tracking):
     rng = np.random.default_rng(20240601)
     out = {}
-    # A: stereo-style L->R (keypoint.py:78) + temporal 2D-3D (Point3D.py:197) + get_matches
+    # A: stereo-style L->R (keypoint.py:35) + temporal 2D-3D (Point3D.py:33) + get_matches
     nL, nR, nN = 300, 320, 400
     desL, desR = descriptor_sets(rng, nL, nR, n_dups=12)
     ptsL = rng.uniform(0, [1280, 720], (nL, 2)).astype(np.float32)

@@ -1,6 +1,6 @@
 """Gather / triangulation / PnP: oracle pinning (CPU) and HIP parity (GPU).
 
-Reference: Point3D.py:5-30, keypoint.py:96-100, transformation.py:5-37.
+Reference: Point3D.py:5-30, keypoint.py:53-57, transformation.py:5-37.
 Tolerances: gather bit-exact; triangulated X rel 1e-9 (GPU one-sided Jacobi vs
 numpy LAPACK SVD, both backward stable on the 4x4 DLT system); PnP: the same
 hypotheses and inlier counts, final pose within 1e-8 (f64 LM on the same

@@ -1,6 +1,6 @@
 """Hamming kNN-2 matcher: oracle pinning (CPU) and HIP parity (GPU).
 
-Reference: keypoint.py:78-109, Point3D.py:197-218, tracking.py:229-251.
+Reference: keypoint.py:35-66, Point3D.py:33-53, tracking.py:12-34.
 The bar is bit-exact: indices, distances and the good mask.
 """
 import os
@@ -29,7 +29,7 @@ def _sets(rng, nq, nt, dup=0, planted=0.6, flip=0.08):
 
 # ----------------------------------------------------------------------------- CPU
 def test_ratio_predicate_integer_form():
-    """`m.distance < 0.7 * n.distance` (keypoint.py:91) == 10*d1 < 7*d2 on [0,256]^2."""
+    """`m.distance < 0.7 * n.distance` (keypoint.py:48) == 10*d1 < 7*d2 on [0,256]^2."""
     d = np.arange(257)
     ref = d[:, None].astype(np.float32).astype(float) < 0.7 * d[None, :].astype(np.float32).astype(float)
     assert np.array_equal(ref, 10 * d[:, None] < 7 * d[None, :])
