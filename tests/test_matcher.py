@@ -150,3 +150,33 @@ def test_gpu_compact_matches_order_and_gate():
             p = p[np.all(np.abs(X[b, p[:, 0]]) < 500.0, axis=1)]
         assert cnt[b] == len(p)
         assert np.array_equal(pairs[b, :cnt[b]], p)
+
+
+@pytest.mark.gpu
+def test_gpu_reference_mirrors_match_goldens(golden_dir):
+    """keypoint.py / tracking.py / Point3D.py mirrors on the GPU reproduce the
+    goldens generated from the reference (exact-BF knnMatch stand-in)."""
+    from slam355 import Point3D, keypoint, tracking
+
+    g = np.load(os.path.join(golden_dir, "matcher_golden.npz"))
+    a1, a2 = tracking.get_matches(g["stereo_ptsL"], g["stereo_desL"], g["stereo_ptsR"],
+                                  g["stereo_desR"])
+    assert a1.dtype == np.float32 and np.array_equal(a1, g["getm_out_q1"])
+    assert np.array_equal(a2, g["getm_out_q2"])
+    q2, Q1, q1 = Point3D.find_2D_and_3D_correspondenses(
+        g["temporal_des_i"], g["temporal_pts_i"], g["temporal_pts_i1"], g["temporal_des_i1"],
+        g["temporal_Q"], max_Distance=500)
+    for a, b in ((q2, "temporal_out_q2"), (Q1, "temporal_out_Q1"), (q1, "temporal_out_q1")):
+        assert np.array_equal(a, g[b]), b
+    # the stereo path adds the F-LMedS mask: pre-mask pairs equal the golden
+    # (all-inlier F stand-in), the mask equals the oracle's seeded LMedS
+    from oracle import geometry as og
+
+    pl, pr, dl, dr = keypoint.track_keypoints_left_to_right_new(
+        g["stereo_ptsL"], g["stereo_desL"], g["stereo_ptsR"], g["stereo_desR"], seed=4, frame=2)
+    mask, _, _, _ = og.fundamental_lmeds(g["stereo_out_ptsL"], g["stereo_out_ptsR"], seed=4,
+                                         item=2)
+    assert np.array_equal(pl, g["stereo_out_ptsL"][mask])
+    assert np.array_equal(pr, g["stereo_out_ptsR"][mask])
+    assert np.array_equal(dl, g["stereo_out_desL"][mask])
+    assert np.array_equal(dr, g["stereo_out_desR"][mask])
