@@ -58,10 +58,32 @@ struct OrbGeom {
 
 __device__ __forceinline__ int rne_f(float v) { return (int)rintf(v); }
 
+// Exact n / d for n >= 0, d >= 1 with n * d < 2^32, by a multiply-high with
+// m = ceil(2^32 / d): the error n (m - 2^32/d) / 2^32 < n / 2^32 < 1/d never
+// crosses an integer.  (Here n < W * H and d <= W <= 1023, so n d < 2^30.)
+// d == 1 gives m == 0 (2^32 does not fit): fdiv then returns n.
+__device__ __forceinline__ uint32_t div_magic(uint32_t d) { return 0xFFFFFFFFu / d + 1u; }
+__device__ __forceinline__ int fdiv(int n, uint32_t m) {
+  return m ? (int)__umulhi((uint32_t)n, m) : n;
+}
+
 // ------------------------------------------------------------------ FAST
 __device__ __forceinline__ int fast_score(const uint8_t* im, int st, int x, int y) {
   const uint8_t* c = im + y * st + x;
   const int v = c[0];
+  // Exact quick reject: any 9 consecutive circle positions contain two
+  // adjacent compass points (0,4,8,12), so a corner needs such a pair to be
+  // darker (or brighter) than v -/+ t.
+  {
+    const int e0 = v - c[3 * st], e4 = v - c[3], e8 = v - c[-3 * st], e12 = v - c[-3];
+    const unsigned dk = (e0 > kFastT ? 1u : 0u) | (e4 > kFastT ? 2u : 0u) |
+                        (e8 > kFastT ? 4u : 0u) | (e12 > kFastT ? 8u : 0u);
+    const unsigned br = (e0 < -kFastT ? 1u : 0u) | (e4 < -kFastT ? 2u : 0u) |
+                        (e8 < -kFastT ? 4u : 0u) | (e12 < -kFastT ? 8u : 0u);
+    const unsigned dk2 = dk & ((dk >> 1) | (dk << 3));  // (0,4) (4,8) (8,12) (12,0)
+    const unsigned br2 = br & ((br >> 1) | (br << 3));
+    if (((dk2 | br2) & 0xFu) == 0u) return 0;
+  }
   int d[16];
   d[0] = v - c[3 * st];
   d[1] = v - c[3 * st + 1];
@@ -167,6 +189,24 @@ __device__ __forceinline__ int lin_coeff(int d, int dsize, int ssize) {
   return 0;  // replicate the first
 }
 
+// -DSLAM_ORB_PROFILE: per-phase shader cycles (s_memtime, thread 0 of every
+// workgroup) accumulated in g_orb_prof and read by slam_orb_profile_read().
+#ifdef SLAM_ORB_PROFILE
+__device__ unsigned long long g_orb_prof[16];
+#define ORB_T0() unsigned long long orb_tp = __builtin_amdgcn_s_memtime()
+#define ORB_T(ph)                                                          \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      const unsigned long long orb_tn = __builtin_amdgcn_s_memtime();      \
+      atomicAdd(&g_orb_prof[ph], orb_tn - orb_tp);                         \
+      orb_tp = orb_tn;                                                     \
+    }                                                                      \
+  } while (0)
+#else
+#define ORB_T0() (void)0
+#define ORB_T(ph) (void)0
+#endif
+
 struct KP {  // one kept keypoint of the current level (LDS)
   int x, y;
   float resp, angle;
@@ -199,6 +239,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   int32_t* ooct = ws_oct + slot * g.tcap;
   uint8_t* odesc = ws_desc + slot * g.tcap * 32;
 
+  ORB_T0();
   // ---- stage the patch (level 0) into LDS, 16 B per lane where aligned
   {
     const uint8_t* src = img + (size_t)b * g.H * g.stride + (size_t)y0 * g.stride + x0;
@@ -218,6 +259,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     }
   }
   __syncthreads();
+  ORB_T(0);
 
   int nout = 0;      // keypoints written for this tile (uniform)
   int overflow = 0;  // uniform
@@ -232,8 +274,9 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
       for (int i = t; i < W; i += kOrbWG) tabx[i] = lin_coeff(i, W, SW);
       for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
       __syncthreads();
+      const uint32_t mW = div_magic(W);
       for (int i = t; i < W * H; i += kOrbWG) {
-        const int y = i / W, x = i - y * W;
+        const int y = fdiv(i, mW), x = i - y * W;
         const int cx = tabx[x], cy = taby[y];
         const int xo = cx >> 9, c1 = cx & 511, c0 = 256 - c1;
         const int yo = cy >> 9, d1 = cy & 511, d0 = 256 - d1;
@@ -248,6 +291,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
         I[i] = (uint8_t)min((v + 32768) >> 16, 255);
       }
       __syncthreads();
+      ORB_T(1);
     }
     const int n_l = g.nl[l];
     if (W <= 2 * kEdge || H <= 2 * kEdge || n_l == 0) continue;  // uniform
@@ -257,18 +301,21 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     uint8_t* Smap = U;
     uint32_t* cand = reinterpret_cast<uint32_t*>(U + ((SWd * SHd + 15) & ~15));
     float* cresp = reinterpret_cast<float*>(cand + g.cand_cap);
+    const uint32_t mS = div_magic(SWd);
     for (int i = t; i < SWd * SHd; i += kOrbWG) {
-      const int y = i / SWd, x = i - y * SWd;
+      const int y = fdiv(i, mS), x = i - y * SWd;
       Smap[i] = (uint8_t)fast_score(I, W, x + kNMS0, y + kNMS0);
     }
     for (int i = t; i < 256; i += kOrbWG) hist[i] = 0;
     if (t < 8) ctr[t] = 0;
     __syncthreads();
+    ORB_T(2);
     // ---- strict 3x3 NMS + border [31, W-32] -> candidates
     {
       const int CW = W - 2 * kEdge, CH = H - 2 * kEdge;
+      const uint32_t mC = div_magic(CW);
       for (int i = t; i < CW * CH; i += kOrbWG) {
-        const int yy = i / CW, xx = i - yy * CW;
+        const int yy = fdiv(i, mC), xx = i - yy * CW;
         const int x = xx + kEdge, y = yy + kEdge;
         const uint8_t* sp = Smap + (y - kNMS0) * SWd + (x - kNMS0);
         const int s = sp[0];
@@ -282,6 +329,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
       }
     }
     __syncthreads();
+    ORB_T(3);
     const int ncand = ctr[0];
     if (ncand > g.cand_cap) {  // cannot happen for strict maxima (density <= 1/4); guard anyway
       overflow = 1;
@@ -337,11 +385,13 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     const int nk = ctr[1];
     for (int i = t; i < nk; i += kOrbWG) cand[i] = reinterpret_cast<uint32_t*>(cresp)[i];
     __syncthreads();
+    ORB_T(4);
     for (int i = t; i < nk; i += kOrbWG) {
       const uint32_t c = cand[i];
       cresp[i] = harris(I, W, (int)(c & 1023u), (int)((c >> 10) & 1023u));
     }
     __syncthreads();
+    ORB_T(5);
     // ---- exact rank by (response desc, y asc, x asc); L[rank] holds the sorted list
     for (int i = t; i < nk; i += kOrbWG) {
       const float ri = cresp[i];
@@ -376,6 +426,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     }
     __syncthreads();
     const int m = ctr[3];
+    ORB_T(6);
     if (m < 0 || nout + m > g.tcap) {
       overflow = 1;
       break;
@@ -406,46 +457,96 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     const int BW = W - 2 * kBl0, BH = H - 2 * kBl0;
     uint8_t* Bl = U;
     __syncthreads();  // Smap/cand/cresp dead from here (L holds the level)
+    ORB_T(7);
     {
+      // 4 adjacent output columns per lane: one aligned 16-byte LDS window per
+      // source row (v_alignbyte to the 10 needed bytes, v_cvt_f32_ubyteN), four
+      // independent FMA chains; rows slide down a per-lane segment.  Every
+      // output keeps the exact operation order of the scalar form (row: fmaf
+      // k0..k6 from 0; column: w3*k3 then fmaf(w[+d]+w[-d], k[3+d])).
       const float k0 = g.gk[0], k1 = g.gk[1], k2 = g.gk[2], k3 = g.gk[3];
       const float k4 = g.gk[4], k5 = g.gk[5], k6 = g.gk[6];
-      const int nseg = (kOrbWG + BW - 1) / BW;
+      const int ncg = (BW + 3) >> 2;
+      const int nseg = max(1, kOrbWG / ncg);
       const int seg = (BH + nseg - 1) / nseg;
-      for (int item = t; item < BW * nseg; item += kOrbWG) {
-        const int s = item / BW, c = item - s * BW;
-        const int r0 = s * seg, r1 = min(BH, r0 + seg);
+      for (int item = t; item < ncg * nseg; item += kOrbWG) {
+        const int sg = item / ncg, cg = item - sg * ncg;
+        const int r0 = sg * seg, r1 = min(BH, r0 + seg);
         if (r0 >= r1) continue;
-        const int x = c + kBl0;
-        auto rowf = [&](int y) {
-          const uint8_t* p = I + y * W + x - 3;
-          float acc = 0.f;
-          acc = fmaf((float)p[0], k0, acc);
-          acc = fmaf((float)p[1], k1, acc);
-          acc = fmaf((float)p[2], k2, acc);
-          acc = fmaf((float)p[3], k3, acc);
-          acc = fmaf((float)p[4], k4, acc);
-          acc = fmaf((float)p[5], k5, acc);
-          acc = fmaf((float)p[6], k6, acc);
-          return acc;
+        const int c4 = 4 * cg, x = c4 + kBl0;
+        auto rowf4 = [&](int y, float4& o) {
+          const int addr = y * W + x - 3;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (addr & ~3));
+          const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3];
+          const int sh = addr & 3;
+          const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+          const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+          const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+          float p[10];
+          p[0] = (float)((q0 >> 0) & 0xFFu);
+          p[1] = (float)((q0 >> 8) & 0xFFu);
+          p[2] = (float)((q0 >> 16) & 0xFFu);
+          p[3] = (float)((q0 >> 24) & 0xFFu);
+          p[4] = (float)((q1 >> 0) & 0xFFu);
+          p[5] = (float)((q1 >> 8) & 0xFFu);
+          p[6] = (float)((q1 >> 16) & 0xFFu);
+          p[7] = (float)((q1 >> 24) & 0xFFu);
+          p[8] = (float)((q2 >> 0) & 0xFFu);
+          p[9] = (float)((q2 >> 8) & 0xFFu);
+          float r[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float acc = 0.f;
+            acc = fmaf(p[j], k0, acc);
+            acc = fmaf(p[j + 1], k1, acc);
+            acc = fmaf(p[j + 2], k2, acc);
+            acc = fmaf(p[j + 3], k3, acc);
+            acc = fmaf(p[j + 4], k4, acc);
+            acc = fmaf(p[j + 5], k5, acc);
+            acc = fmaf(p[j + 6], k6, acc);
+            r[j] = acc;
+          }
+          o = make_float4(r[0], r[1], r[2], r[3]);
         };
         const int yb = r0 + kBl0;  // first output row (image coords)
-        float w0 = rowf(yb - 3), w1 = rowf(yb - 2), w2 = rowf(yb - 1), w3 = rowf(yb);
-        float w4 = rowf(yb + 1), w5 = rowf(yb + 2), w6 = rowf(yb + 3);
+        float4 w0, w1, w2, w3, w4, w5, w6;
+        rowf4(yb - 3, w0);
+        rowf4(yb - 2, w1);
+        rowf4(yb - 1, w2);
+        rowf4(yb, w3);
+        rowf4(yb + 1, w4);
+        rowf4(yb + 2, w5);
+        rowf4(yb + 3, w6);
+        const int nc = min(4, BW - c4);
         for (int r = r0; r < r1; ++r) {
-          float s0 = w3 * k3;
-          s0 = fmaf(w4 + w2, k4, s0);
-          s0 = fmaf(w5 + w1, k5, s0);
-          s0 = fmaf(w6 + w0, k6, s0);
-          const int v = (int)rintf(s0);
-          Bl[r * BW + c] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+          float v4[4];
+          const float a0[4] = {w0.x, w0.y, w0.z, w0.w}, a1[4] = {w1.x, w1.y, w1.z, w1.w};
+          const float a2[4] = {w2.x, w2.y, w2.z, w2.w}, a3[4] = {w3.x, w3.y, w3.z, w3.w};
+          const float a4[4] = {w4.x, w4.y, w4.z, w4.w}, a5[4] = {w5.x, w5.y, w5.z, w5.w};
+          const float a6[4] = {w6.x, w6.y, w6.z, w6.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float s0 = a3[j] * k3;
+            s0 = fmaf(a4[j] + a2[j], k4, s0);
+            s0 = fmaf(a5[j] + a1[j], k5, s0);
+            s0 = fmaf(a6[j] + a0[j], k6, s0);
+            v4[j] = s0;
+          }
+          uint8_t* out = Bl + r * BW + c4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int v = (int)rintf(v4[j]);
+            if (j < nc) out[j] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+          }
           if (r + 1 < r1) {
             w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-            w6 = rowf(r + 1 + kBl0 + 3);
+            rowf4(r + 1 + kBl0 + 3, w6);
           }
         }
       }
     }
     __syncthreads();
+    ORB_T(8);
     // ---- rBRIEF: 32 lanes per keypoint, one byte per lane; write the keypoint
     {
       const float ls = g.ls[l];
@@ -484,6 +585,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     }
     nout += m;
     __syncthreads();
+    ORB_T(9);
   }
   if (t == 0) ws_cnt[slot] = overflow ? -1 : nout;
 }
@@ -638,6 +740,19 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
 bool g_pattern_uploaded[64] = {false};
 
 }  // namespace
+
+#ifdef SLAM_ORB_PROFILE
+// phases: 0 stage, 1 resize, 2 FAST map, 3 NMS, 4 retainBest(2n), 5 Harris,
+// 6 rank + retainBest(n), 7 IC angle, 8 blur, 9 rBRIEF + write (cycles summed
+// over workgroups); reads and clears the counters.
+extern "C" int slam_orb_profile_read(unsigned long long* out16) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_orb_prof), 16 * sizeof(unsigned long long)));
+  unsigned long long z[16] = {};
+  SLAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_orb_prof), z, sizeof(z)));
+  return SLAM_OK;
+}
+#endif
 
 extern "C" int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int overlap_div,
                                         int height_div, int width_div, size_t* bytes) {
