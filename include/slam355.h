@@ -220,6 +220,7 @@ typedef struct slam_ba_problem {
   int32_t n_grps;        /* point groups (>= 1): <= 128 obs each, whole points */
   double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
   double* pts[2];               /* [P][3]                                      */
+  double* camrec[2];            /* [C][32] per-camera projection records of cams[] */
   const int32_t* obs_cam;       /* [O] (sorted by point, then camera)          */
   const int32_t* obs_pt;        /* [O]                                         */
   const double* obs_q;          /* [O][2]                                      */

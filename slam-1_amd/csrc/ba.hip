@@ -37,11 +37,14 @@ constexpr int kBS = 256;   // block size of the element-wise kernels
 // ---------------------------------------------------------------- projection
 // Residual (proj - q) of BundleAdjustment.py:317-337 with the operation order
 // of the numpy code, and optionally its analytic 2x12 Jacobian.
-template <bool JAC>
-__device__ __forceinline__ void reproject(const double* __restrict__ cam,
-                                          const double* __restrict__ X,
-                                          const double* __restrict__ q, double r[2],
-                                          double J[2][12]) {
+// Per-camera part of the projection: everything that depends on the rotation
+// vector only (theta, v, cos, sin, R and the Jacobian's A matrix), computed
+// once per camera by cam_prep and stored as a 32-double record; the per-
+// observation part (reproject_pre) then does no sqrt/sin/cos/division by theta.
+// Both halves keep the operation order of the single-function form, so
+// results are bit-identical to computing everything per observation.
+constexpr int kCamRec = 32;  // c s omc v(3) R(9) A(9) inv small t(3) f k1 k2 pad(0)
+__device__ __forceinline__ void cam_prep(const double* __restrict__ cam, double* __restrict__ o) {
   const double w0 = cam[0], w1 = cam[1], w2 = cam[2];
   const double th = sqrt(w0 * w0 + w1 * w1 + w2 * w2);
   double v0 = 0.0, v1 = 0.0, v2 = 0.0;  // nan_to_num(w / 0) == 0  (:292-293)
@@ -50,54 +53,78 @@ __device__ __forceinline__ void reproject(const double* __restrict__ cam,
     v1 = w1 / th;
     v2 = w2 / th;
   }
-  const double X0 = X[0], X1 = X[1], X2 = X[2];
   const double c = cos(th), s = sin(th);
+  const double omc = 1.0 - c;
+  // R = c I + s [v]x + (1-c) v v^T
+  double R[3][3];
+  R[0][0] = c + omc * v0 * v0; R[0][1] = -s * v2 + omc * v0 * v1; R[0][2] = s * v1 + omc * v0 * v2;
+  R[1][0] = s * v2 + omc * v1 * v0; R[1][1] = c + omc * v1 * v1; R[1][2] = -s * v0 + omc * v1 * v2;
+  R[2][0] = -s * v1 + omc * v2 * v0; R[2][1] = s * v0 + omc * v2 * v1; R[2][2] = c + omc * v2 * v2;
+  // dRX/dw (Gallego & Yezzi): -R [X]x A / |w|^2 with A = w w^T + (R^T - I)[w]x
+  const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
+  const double W[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
+  const double w[3] = {w0, w1, w2};
+  double A[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      double acc = w[i] * w[k];
+      for (int j = 0; j < 3; ++j) acc += R[j][i] * W[j][k];
+      A[i][k] = acc - W[i][k];
+    }
+  o[0] = c; o[1] = s; o[2] = omc;
+  o[3] = v0; o[4] = v1; o[5] = v2;
+  for (int i = 0; i < 9; ++i) o[6 + i] = R[i / 3][i % 3];
+  for (int i = 0; i < 9; ++i) o[15 + i] = A[i / 3][i % 3];
+  o[24] = th2 < 1e-24 ? 0.0 : -1.0 / th2;
+  o[25] = th2 < 1e-24 ? 1.0 : 0.0;
+  for (int i = 0; i < 6; ++i) o[26 + i] = cam[3 + i];
+}
+
+// Residual (proj - q) of BundleAdjustment.py:317-337 with the operation order
+// of the numpy code, and optionally its analytic 2x12 Jacobian, from a camera
+// record of cam_prep.
+template <bool JAC>
+__device__ __forceinline__ void reproject_pre(const double* __restrict__ cr,
+                                              const double* __restrict__ X,
+                                              const double* __restrict__ q, double r[2],
+                                              double J[2][12]) {
+  const double c = cr[0], s = cr[1], omc = cr[2];
+  const double v0 = cr[3], v1 = cr[4], v2 = cr[5];
+  const double X0 = X[0], X1 = X[1], X2 = X[2];
   const double dot = X0 * v0 + X1 * v1 + X2 * v2;
   const double cx0 = v1 * X2 - v2 * X1;
   const double cx1 = v2 * X0 - v0 * X2;
   const double cx2 = v0 * X1 - v1 * X0;
-  const double omc = 1.0 - c;
   const double dk = dot * omc;
   const double RX0 = c * X0 + s * cx0 + dk * v0;
   const double RX1 = c * X1 + s * cx1 + dk * v1;
   const double RX2 = c * X2 + s * cx2 + dk * v2;
-  const double P0 = RX0 + cam[3], P1 = RX1 + cam[4], P2 = RX2 + cam[5];
+  const double P0 = RX0 + cr[26], P1 = RX1 + cr[27], P2 = RX2 + cr[28];
   const double p0 = -P0 / P2, p1 = -P1 / P2;
-  const double f = cam[6], k1 = cam[7], k2 = cam[8];
+  const double f = cr[29], k1 = cr[30], k2 = cr[31];
   const double n = p0 * p0 + p1 * p1;
   const double rad = 1.0 + k1 * n + k2 * (n * n);
   const double sc = rad * f;
   r[0] = p0 * sc - q[0];
   r[1] = p1 * sc - q[1];
   if constexpr (JAC) {
-    // R = c I + s [v]x + (1-c) v v^T
-    double R[3][3];
-    R[0][0] = c + omc * v0 * v0; R[0][1] = -s * v2 + omc * v0 * v1; R[0][2] = s * v1 + omc * v0 * v2;
-    R[1][0] = s * v2 + omc * v1 * v0; R[1][1] = c + omc * v1 * v1; R[1][2] = -s * v0 + omc * v1 * v2;
-    R[2][0] = -s * v1 + omc * v2 * v0; R[2][1] = s * v0 + omc * v2 * v1; R[2][2] = c + omc * v2 * v2;
-    // dRX/dw: Gallego & Yezzi: -R [X]x (w w^T + (R^T - I)[w]x) / |w|^2 ; -[RX]x at w = 0
+    double R[3][3], A[3][3];
+    for (int i = 0; i < 9; ++i) {
+      R[i / 3][i % 3] = cr[6 + i];
+      A[i / 3][i % 3] = cr[15 + i];
+    }
     double dR[3][3];
-    const double th2 = w0 * w0 + w1 * w1 + w2 * w2;
-    if (th2 < 1e-24) {
+    if (cr[25] != 0.0) {  // |w|^2 < 1e-24: -[RX]x
       dR[0][0] = 0.0;  dR[0][1] = RX2;  dR[0][2] = -RX1;
       dR[1][0] = -RX2; dR[1][1] = 0.0;  dR[1][2] = RX0;
       dR[2][0] = RX1;  dR[2][1] = -RX0; dR[2][2] = 0.0;
     } else {
-      const double W[3][3] = {{0.0, -w2, w1}, {w2, 0.0, -w0}, {-w1, w0, 0.0}};
-      const double w[3] = {w0, w1, w2};
-      double A[3][3];
-      for (int i = 0; i < 3; ++i)
-        for (int k = 0; k < 3; ++k) {
-          double acc = w[i] * w[k];
-          for (int j = 0; j < 3; ++j) acc += R[j][i] * W[j][k];
-          A[i][k] = acc - W[i][k];
-        }
       const double Xs[3][3] = {{0.0, -X2, X1}, {X2, 0.0, -X0}, {-X1, X0, 0.0}};
       double B[3][3];
       for (int i = 0; i < 3; ++i)
         for (int k = 0; k < 3; ++k)
           B[i][k] = Xs[i][0] * A[0][k] + Xs[i][1] * A[1][k] + Xs[i][2] * A[2][k];
-      const double inv = -1.0 / th2;
+      const double inv = cr[24];
       for (int i = 0; i < 3; ++i)
         for (int k = 0; k < 3; ++k)
           dR[i][k] = (R[i][0] * B[0][k] + R[i][1] * B[1][k] + R[i][2] * B[2][k]) * inv;
@@ -123,6 +150,17 @@ __device__ __forceinline__ void reproject(const double* __restrict__ cam,
       J[a][8] = pp[a] * (f * n * n);
     }
   }
+}
+
+// Single-call form (standalone residual / Jacobian entry points).
+template <bool JAC>
+__device__ __forceinline__ void reproject(const double* __restrict__ cam,
+                                          const double* __restrict__ X,
+                                          const double* __restrict__ q, double r[2],
+                                          double J[2][12]) {
+  double cr[kCamRec];
+  cam_prep(cam, cr);
+  reproject_pre<JAC>(cr, X, q, r, J);
 }
 
 // The two clamps of BundleAdjustment.py:339-350 (x first, then y on the
@@ -221,8 +259,8 @@ __global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
   double r[2], J[2][12];
   double* recc = p.recc + (size_t)(has ? p.obs_campos[o] : 0) * 2 * kRecW;
   if (has) {
-    reproject<true>(p.cams[cur] + 9 * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o],
-                    p.obs_q + 2 * o, r, J);
+    reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o],
+                        p.obs_q + 2 * o, r, J);
     clamp_rows<true>(r, J);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
@@ -343,12 +381,32 @@ __global__ __launch_bounds__(kPairWG) void k_pair_partials(slam_ba_problem p) {
   __shared__ double red[3][81];
   const int ch = blockIdx.x;
   const int beg = p.pair_chunks[3 * ch + 1], end = p.pair_chunks[3 * ch + 2];
+  __shared__ int so[kPairChunk][2];
   const int n = end - beg;
-  for (int i = threadIdx.x; i < n * 27; i += kPairWG) {
+  // indices first (one round trip), then every lane's rows with all loads in
+  // flight before the LDS stores (one more round trip)
+  if (threadIdx.x < 2 * n) (&so[0][0])[threadIdx.x] = p.pair_o[2 * beg + threadIdx.x];
+  __syncthreads();
+  constexpr int kPer = (kPairChunk * 27 + kPairWG - 1) / kPairWG;  // 7
+  double vy[kPer], vw[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kPairWG;
     const int k = i / 27, e = i - k * 27;
-    const int o1 = p.pair_o[2 * (beg + k)], o2 = p.pair_o[2 * (beg + k) + 1];
-    sy[k][e] = p.wy[(size_t)o1 * 54 + 27 + e];
-    sw[k][e] = p.wy[(size_t)o2 * 54 + e];
+    vy[u] = vw[u] = 0.0;
+    if (k < n) {
+      vy[u] = p.wy[(size_t)so[k][0] * 54 + 27 + e];
+      vw[u] = p.wy[(size_t)so[k][1] * 54 + e];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kPairWG;
+    const int k = i / 27, e = i - k * 27;
+    if (k < n) {
+      sy[k][e] = vy[u];
+      sw[k][e] = vw[u];
+    }
   }
   __syncthreads();
   const int t = threadIdx.x;
@@ -510,7 +568,9 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
     p.cams[1 - cur][i] = p.cams[cur][i] + d;
     pc += d * (lam * clampd(diagU[i]) * d + gvec[i]);
   }
-  pc = block_sum(pc, red);
+  pc = block_sum(pc, red);  // (its barriers also publish the trial cameras to the WG)
+  for (int c = t; c < p.n_cams; c += blockDim.x)
+    cam_prep(p.cams[1 - cur] + 9 * c, p.camrec[1 - cur] + kCamRec * c);
   if (t == 0) {
     double cost = 0.0;
     for (int c = 0; c < p.n_cams; ++c) cost += costc[c];
@@ -907,8 +967,8 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* 
   double v = 0.0;
   if (has) {
     double r[2], J[2][12];
-    reproject<false>(p.cams[1 - cur] + 9 * p.obs_cam[o], snp[p.obs_pt[o] - p0], p.obs_q + 2 * o,
-                     r, J);
+    reproject_pre<false>(p.camrec[1 - cur] + kCamRec * p.obs_cam[o], snp[p.obs_pt[o] - p0],
+                         p.obs_q + 2 * o, r, J);
     clamp_rows<false>(r, J);
     v = r[0] * r[0] + r[1] * r[1];
   }
@@ -971,13 +1031,15 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
   state[SLAM_BA_ST_ITERS] += 1.0;
 }
 
-__global__ void k_reset(double* state, double lam0) {
+__global__ void k_reset(slam_ba_problem p, double lam0) {
   const int t = threadIdx.x;
+  double* state = p.state;
   if (t < SLAM_BA_ST_SLOTS) state[t] = 0.0;
   if (t == 0) {
     state[SLAM_BA_ST_LAMBDA] = lam0;
     state[SLAM_BA_ST_NU] = 2.0;
   }
+  for (int c = t; c < p.n_cams; c += blockDim.x) cam_prep(p.cams[0] + 9 * c, p.camrec[0] + kCamRec * c);
 }
 
 inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
@@ -985,7 +1047,7 @@ inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
 int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
   SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
-  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->recc && p->wy && p->ptdata && p->obs_campos &&
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->camrec[0] && p->camrec[1] && p->recc && p->wy && p->ptdata && p->obs_campos &&
                    p->grp_ptr && p->ticket && p->sys && p->state && p->small && p->red_part &&
                    p->delta_c,
                "slam_ba: null buffer");
@@ -1042,7 +1104,7 @@ extern "C" int slam_ba_jacobian(const double* d_cams, const double* d_pts,
 
 extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream) {
   if (int rc = check_problem(prob)) return rc;
-  k_reset<<<1, 64, 0, slam::as_stream(stream)>>>(prob->state, lambda0);
+  k_reset<<<1, 64, 0, slam::as_stream(stream)>>>(*prob, lambda0);
   SLAM_LAUNCHED("k_reset");
   return SLAM_OK;
 }

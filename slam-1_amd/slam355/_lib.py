@@ -27,7 +27,7 @@ class BAProblemStruct(ctypes.Structure):
     _fields_ = [
         ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_cam_chunks", c_i32),
         ("n_blocks", c_i32), ("n_pair_chunks", c_i32), ("n_pairs", c_i32), ("n_grps", c_i32),
-        ("cams", c_p * 2), ("pts", c_p * 2),
+        ("cams", c_p * 2), ("pts", c_p * 2), ("camrec", c_p * 2),
         ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p),
         ("cam_obs", c_p), ("cam_chunks", c_p), ("cam_chunk_ptr", c_p),
         ("pair_o", c_p), ("pair_chunks", c_p), ("blocks", c_p), ("block_chunk_ptr", c_p),

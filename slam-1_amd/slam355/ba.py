@@ -150,6 +150,7 @@ class BAProblem:
         self.t = t = {}
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
+        t["camrec0"], t["camrec1"] = z(C * 32), z(C * 32)
         for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "obs_campos", "cam_chunks",
                   "cam_chunk_ptr", "pair_o", "pair_chunks", "blocks", "block_chunk_ptr",
                   "grp_ptr"):
@@ -180,6 +181,7 @@ class BAProblem:
         s.n_grps = G
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
+        s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
         for k in ("obs_cam", "obs_pt", "obs_q", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
                   "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "obs_campos", "grp_ptr",
                   "recc", "wy", "ptdata", "cam_part", "pair_part", "sys", "chol", "delta_c",
