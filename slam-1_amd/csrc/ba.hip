@@ -5,12 +5,12 @@
 // and scipy least_squares TRF) with LM on the normal equations, all state on
 // the device so a fixed number of iterations runs with no host round trip.
 //
-// One LM iteration = 6 launches (local BA):
+// One LM iteration = 5 launches (local BA):
 //   k_point_lin     point group -> residuals + Jacobians, camera-ordered Gram
 //                                  record [Jc | r | u], V*_p, e_p = V*^-1 g_p,
 //                                  W_o = Jc^T Jp, Y_o = W_o V*^-1, u_o = Jp e_p
-//   k_cam_gram      chunk  -> f64 MFMA Gram  G = M^T M, M = [Jc | r | u] (2 rows/obs)
-//   k_pair_partials chunk  -> sum over obs pairs of Y_o1 W_o2^T (Schur terms)
+//   k_gram_pairs    chunk  -> camera chunks: f64 MFMA Gram G = M^T M, M = [Jc | r | u]
+//                             (2 rows/obs); pair chunks: sum of Y_o1 W_o2^T (Schur)
 //   k_assemble      block  -> S = blockdiag(U) - sum(Y W^T), b = -Jc^T r - Jc^T u, ...
 //   (all-reduce of sys over ranks happens here for multi-GPU)
 //   k_solve_blk     1 WG   -> damp, blocked LDL^T (MFMA trailing updates), camera
@@ -344,9 +344,7 @@ __global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
 // residual rows = 2 observations.  8 steps are loaded before they are consumed.
 constexpr int kGramWG = 256;
 constexpr int kGramUnroll = 8;
-__global__ __launch_bounds__(kGramWG) void k_cam_gram(slam_ba_problem p) {
-  __shared__ double red[4][256];
-  const int ch = blockIdx.x;
+__device__ __forceinline__ void cam_gram(const slam_ba_problem& p, int ch, double (*red)[256]) {
   const int beg = p.cam_chunks[3 * ch + 1], end = p.cam_chunks[3 * ch + 2];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int krow = lane >> 4, col = lane & 15;
@@ -375,13 +373,19 @@ __global__ __launch_bounds__(kGramWG) void k_cam_gram(slam_ba_problem p) {
 // Schur terms: sum over the chunk's obs pairs of Y_o1 (9x3) W_o2^T (3x9).
 constexpr int kPairChunk = 64;
 constexpr int kPairWG = 256;
-__global__ __launch_bounds__(kPairWG) void k_pair_partials(slam_ba_problem p) {
-  __shared__ double sy[kPairChunk][27];
-  __shared__ double sw[kPairChunk][27];
-  __shared__ double red[3][81];
-  const int ch = blockIdx.x;
+struct PairLds {
+  double sy[kPairChunk][27];
+  double sw[kPairChunk][27];
+  double red[3][81];
+  int so[kPairChunk][2];
+};
+
+__device__ __forceinline__ void pair_partials(const slam_ba_problem& p, int ch, PairLds& L) {
+  auto& sy = L.sy;
+  auto& sw = L.sw;
+  auto& red = L.red;
+  auto& so = L.so;
   const int beg = p.pair_chunks[3 * ch + 1], end = p.pair_chunks[3 * ch + 2];
-  __shared__ int so[kPairChunk][2];
   const int n = end - beg;
   // indices first (one round trip), then every lane's rows with all loads in
   // flight before the LDS stores (one more round trip)
@@ -420,6 +424,21 @@ __global__ __launch_bounds__(kPairWG) void k_pair_partials(slam_ba_problem p) {
   }
   __syncthreads();
   if (t < 81) p.pair_part[(size_t)ch * 81 + t] = (red[0][t] + red[1][t]) + red[2][t];
+}
+
+// Camera Gram chunks and Schur pair chunks are independent: one launch, the
+// workgroup index picks the role (gram chunks first), so the two overlap.
+static_assert(kGramWG == kPairWG, "k_gram_pairs runs both roles with one block size");
+__global__ __launch_bounds__(kGramWG) void k_gram_pairs(slam_ba_problem p) {
+  __shared__ union {
+    double gram[4][256];
+    PairLds pair;
+  } lds;
+  const int b = blockIdx.x;
+  if (b < p.n_cam_chunks)
+    cam_gram(p, b, lds.gram);
+  else
+    pair_partials(p, b - p.n_cam_chunks, lds.pair);
 }
 
 // One workgroup per upper camera-pair block (c1 <= c2), ALL C(C+1)/2 of them:
@@ -1116,13 +1135,9 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
   // every entry of sys is written by k_assemble (all upper blocks), so no clearing
   k_point_lin<<<p.n_grps, kGrp, 0, s>>>(p);
   SLAM_LAUNCHED("k_point_lin");
-  if (p.n_cam_chunks > 0) {
-    k_cam_gram<<<p.n_cam_chunks, kGramWG, 0, s>>>(p);
-    SLAM_LAUNCHED("k_cam_gram");
-  }
-  if (p.n_pair_chunks > 0) {
-    k_pair_partials<<<p.n_pair_chunks, kPairWG, 0, s>>>(p);
-    SLAM_LAUNCHED("k_pair_partials");
+  if (p.n_cam_chunks + p.n_pair_chunks > 0) {
+    k_gram_pairs<<<p.n_cam_chunks + p.n_pair_chunks, kGramWG, 0, s>>>(p);
+    SLAM_LAUNCHED("k_gram_pairs");
   }
   k_assemble<<<p.n_blocks, kBS, 0, s>>>(p);
   SLAM_LAUNCHED("k_assemble");

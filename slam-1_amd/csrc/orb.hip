@@ -42,9 +42,9 @@ struct OrbGeom {
   int H, W, stride;
   int n_tiles, ntx, tile_h, tile_w;
   int tcap;       // keypoint slots per tile in the workspace
-  int cand_cap;   // NMS survivors per level (LDS)
-  int list_cap;   // kept keypoints per level (LDS)
-  int lds_a, lds_b, lds_u, lds_l, lds_m;  // byte offsets of the LDS regions
+  int cand_cap;   // NMS candidates per level (global scratch, worst case 1/4 density)
+  int list_cap;   // kept keypoints / retainBest(2n) survivors per level (LDS)
+  int lds_a, lds_u, lds_l, lds_s, lds_m;  // byte offsets of the LDS regions
   int lds_total;
   float ls[kNLev];  // (float)pow(1.2, l)
   int nl[kNLev];    // per-level budget
@@ -216,7 +216,8 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
                                                      float* __restrict__ ws_kp,
                                                      int32_t* __restrict__ ws_oct,
                                                      uint8_t* __restrict__ ws_desc,
-                                                     int32_t* __restrict__ ws_cnt) {
+                                                     int32_t* __restrict__ ws_cnt,
+                                                     uint32_t* __restrict__ ws_cand) {
   // All LDS is one dynamic region with a 16-byte aligned base (Guideline 17).
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int* hist = reinterpret_cast<int*>(lds + g.lds_m);  // 256 bins of FAST score
@@ -231,19 +232,29 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   const int x0 = tx * g.tile_w, y0 = ty * g.tile_h;
   const int shp = g.tile_shape[tile];
   const int pw = g.sw[shp], ph = g.sh[shp];
-  uint8_t* bufs[2] = {lds + g.lds_a, lds + g.lds_b};
+  // LDS: A = current level image, U = scratch (resize target, FAST score map,
+  // blurred level), L = kept keypoints, S = retainBest(2n) survivors.  Only
+  // one level image is resident: level l is resized from A into U and copied
+  // back, so an ORB workgroup leaves room on its CU for other kernels' groups.
+  uint8_t* A = lds + g.lds_a;
   uint8_t* U = lds + g.lds_u;
   KP* L = reinterpret_cast<KP*>(lds + g.lds_l);
+  uint32_t* svc = reinterpret_cast<uint32_t*>(lds + g.lds_s);
+  float* svr = reinterpret_cast<float*>(svc + g.list_cap);
   const size_t slot = (size_t)b * g.n_tiles + tile;
   float* okp = ws_kp + slot * g.tcap * 5;
   int32_t* ooct = ws_oct + slot * g.tcap;
   uint8_t* odesc = ws_desc + slot * g.tcap * 32;
+  // NMS candidates (and, past list_cap survivors, the survivors) of this tile
+  uint32_t* gcand = ws_cand + slot * 3 * (size_t)g.cand_cap;
+  uint32_t* gsvc = gcand + g.cand_cap;
+  float* gsvr = reinterpret_cast<float*>(gsvc + g.cand_cap);
 
   ORB_T0();
   // ---- stage the patch (level 0) into LDS, 16 B per lane where aligned
   {
     const uint8_t* src = img + (size_t)b * g.H * g.stride + (size_t)y0 * g.stride + x0;
-    uint8_t* dst = bufs[0];
+    uint8_t* dst = A;
     if ((pw & 15) == 0 && (((uintptr_t)src) & 15) == 0 && (g.stride & 15) == 0) {
       const int vpr = pw >> 4;
       for (int i = t; i < vpr * ph; i += kOrbWG) {
@@ -266,11 +277,11 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   const int nlev = g.nlev[shp];
   for (int l = 0; l < nlev; ++l) {
     const int W = g.lw[shp][l], H = g.lh[shp][l];
-    uint8_t* I = bufs[l & 1];
+    uint8_t* I = A;
     if (l > 0) {
-      // ---- resize level l-1 -> l (INTER_LINEAR_EXACT)
+      // ---- resize level l-1 (A) -> l (U, INTER_LINEAR_EXACT), then U -> A
       const int SW = g.lw[shp][l - 1], SH = g.lh[shp][l - 1];
-      const uint8_t* S = bufs[(l - 1) & 1];
+      const uint8_t* S = A;
       for (int i = t; i < W; i += kOrbWG) tabx[i] = lin_coeff(i, W, SW);
       for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
       __syncthreads();
@@ -288,8 +299,11 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
           const int h1 = c0 * r1[0] + (c1 ? c1 * r1[1] : 0);
           v += d1 * h1;
         }
-        I[i] = (uint8_t)min((v + 32768) >> 16, 255);
+        U[i] = (uint8_t)min((v + 32768) >> 16, 255);
       }
+      __syncthreads();
+      for (int i = t; i < (W * H + 15) >> 4; i += kOrbWG)
+        reinterpret_cast<uint4*>(A)[i] = reinterpret_cast<const uint4*>(U)[i];
       __syncthreads();
       ORB_T(1);
     }
@@ -299,8 +313,6 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     // ---- FAST score map over [29, W-30] x [29, H-30]
     const int SWd = W - 2 * kNMS0, SHd = H - 2 * kNMS0;
     uint8_t* Smap = U;
-    uint32_t* cand = reinterpret_cast<uint32_t*>(U + ((SWd * SHd + 15) & ~15));
-    float* cresp = reinterpret_cast<float*>(cand + g.cand_cap);
     const uint32_t mS = div_magic(SWd);
     for (int i = t; i < SWd * SHd; i += kOrbWG) {
       const int y = fdiv(i, mS), x = i - y * SWd;
@@ -323,7 +335,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
         if (s > sp[-1] && s > sp[1] && s > sp[-SWd - 1] && s > sp[-SWd] && s > sp[-SWd + 1] &&
             s > sp[SWd - 1] && s > sp[SWd] && s > sp[SWd + 1]) {
           const int k = atomicAdd(&ctr[0], 1);
-          if (k < g.cand_cap) cand[k] = ((uint32_t)s << 20) | ((uint32_t)y << 10) | (uint32_t)x;
+          if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 20) | ((uint32_t)y << 10) | (uint32_t)x;
           atomicAdd(&hist[s], 1);
         }
       }
@@ -367,24 +379,34 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
         for (int off = 32; off > 0; off >>= 1) tl = max(tl, __shfl_xor(tl, off, 64));
         T = tl;
       }
-      if (lane == 0) ctr[2] = T;
+      // survivors = candidates with score >= T
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cnt += 4 * lane + q >= T ? hist[4 * lane + q] : 0;
+      for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+      if (lane == 0) {
+        ctr[2] = T;
+        ctr[4] = cnt;
+      }
     }
     __syncthreads();
-    // ---- survivors of retainBest(2n) -> front of cand (via cresp as scratch)
+    // ---- survivors of retainBest(2n): LDS when they fit (the normal case),
+    // else this tile's global scratch (same code, slower)
+    const bool sv_lds = ctr[4] <= g.list_cap;  // uniform
+    uint32_t* cand = sv_lds ? svc : gsvc;
+    float* cresp = sv_lds ? svr : gsvr;
     {
       const int T = ctr[2];
       for (int i = t; i < ncand; i += kOrbWG) {
-        const uint32_t c = cand[i];
+        const uint32_t c = gcand[i];
         if ((int)(c >> 20) >= T) {
           const int k = atomicAdd(&ctr[1], 1);
-          reinterpret_cast<uint32_t*>(cresp)[k] = c;
+          cand[k] = c;
         }
       }
     }
     __syncthreads();
     const int nk = ctr[1];
-    for (int i = t; i < nk; i += kOrbWG) cand[i] = reinterpret_cast<uint32_t*>(cresp)[i];
-    __syncthreads();
     ORB_T(4);
     for (int i = t; i < nk; i += kOrbWG) {
       const uint32_t c = cand[i];
@@ -456,7 +478,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     // ---- 7x7 Gaussian (float path) over [9, W-10] x [9, H-10] into U
     const int BW = W - 2 * kBl0, BH = H - 2 * kBl0;
     uint8_t* Bl = U;
-    __syncthreads();  // Smap/cand/cresp dead from here (L holds the level)
+    __syncthreads();  // Smap and the survivor lists are dead from here (L holds the level)
     ORB_T(7);
     {
       // 4 adjacent output columns per lane: one aligned 16-byte LDS window per
@@ -720,16 +742,16 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
       g->tile_shape[ty * ntx + tx] = (uint8_t)s;
     }
   auto al = [](int v) { return (v + 15) & ~15; };
-  const int max_u = max(max_smap + 8 * max_cand, max_bl);
+  const int max_u = max(max(max_smap, max_bl), max_b);
   int nmax = 0;
   for (int l = 0; l < kNLev; ++l) nmax = max(nmax, g->nl[l]);
-  g->cand_cap = max_cand;
+  g->cand_cap = max(max_cand, 1);
   g->list_cap = max(2 * nmax, nmax + 256);
   g->lds_a = 0;
-  g->lds_b = al(max_a);
-  g->lds_u = g->lds_b + al(max_b);
+  g->lds_u = al(max_a);
   g->lds_l = g->lds_u + al(max_u);
-  g->lds_m = g->lds_l + al(g->list_cap * (int)sizeof(KP));
+  g->lds_s = g->lds_l + al(g->list_cap * (int)sizeof(KP));
+  g->lds_m = g->lds_s + al(g->list_cap * 8);
   g->lds_total = g->lds_m + (256 + 16 + 2 * 1024) * 4;
   g->tcap = max_kp + 64;
   SLAM_REQUIRE(g->lds_total <= 160 * 1024,
@@ -760,7 +782,8 @@ extern "C" int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int
   if (int rc = build_geom(H, W, W, max_kp, overlap_div, height_div, width_div, &g)) return rc;
   SLAM_REQUIRE(bytes != nullptr && batch >= 0, "slam_orb_workspace_bytes: bad args");
   const size_t slots = (size_t)batch * g.n_tiles * g.tcap;
-  *bytes = slots * (5 * sizeof(float) + sizeof(int32_t) + 32) + (size_t)batch * g.n_tiles * 4 + 256;
+  *bytes = slots * (5 * sizeof(float) + sizeof(int32_t) + 32) + (size_t)batch * g.n_tiles * 4 +
+           256 + (size_t)batch * g.n_tiles * 3 * g.cand_cap * sizeof(uint32_t);
   return SLAM_OK;
 }
 
@@ -795,9 +818,11 @@ extern "C" int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int
   int32_t* ws_oct = reinterpret_cast<int32_t*>(base + slots * 5 * sizeof(float));
   uint8_t* ws_desc = base + slots * (5 * sizeof(float) + sizeof(int32_t));
   int32_t* ws_cnt = reinterpret_cast<int32_t*>(ws_desc + slots * 32);
+  uint32_t* ws_cand = reinterpret_cast<uint32_t*>(
+      (reinterpret_cast<uintptr_t>(ws_cnt + (size_t)batch * g.n_tiles) + 255) & ~(uintptr_t)255);
   SLAM_REQUIRE(((uintptr_t)ws_cnt & 3) == 0, "slam_orb_tiles: workspace misaligned");
   k_orb_tile<<<dim3(g.n_tiles, batch), kOrbWG, g.lds_total, s>>>(d_img, g, ws_kp, ws_oct,
-                                                                  ws_desc, ws_cnt);
+                                                                  ws_desc, ws_cnt, ws_cand);
   SLAM_LAUNCHED("k_orb_tile");
   k_orb_compact<<<batch, 256, 0, s>>>(ws_kp, ws_oct, ws_desc, ws_cnt, g.n_tiles, g.tcap, d_kp,
                                       d_octave, d_desc, d_count, kp_cap);
