@@ -177,7 +177,7 @@ def run_tracking(args, world, rank):
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration (10 kernels)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration: k_point_lin + k_gram_pairs + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     for r in roof.values():
