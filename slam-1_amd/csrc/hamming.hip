@@ -4,10 +4,13 @@
 // /root/reference/keypoint.py:40-51, Point3D.py:35-49, tracking.py:14-30.
 //
 // Design (integer-VALU bound, see DESIGN.md "Hamming matcher"):
-//   * one workgroup = 256 lanes x QPL queries of ONE batch item; each lane keeps
-//     its QPL query descriptors in VGPRs (8 dwords each);
-//   * the train set streams through LDS in chunks; every lane of a wave reads
-//     the SAME train row (LDS broadcast, conflict-free ds_read_b128);
+//   * one workgroup = 8 waves x 64 lanes x QPL queries of ONE batch item; every
+//     wave holds the same 64 x QPL query descriptors in VGPRs (8 dwords each)
+//     and takes every 8th train row, so a 2000-row train set keeps 8 waves busy
+//     per 128 queries; the 8 partial top-2 lists are merged through LDS;
+//   * a train row is uniform across the wave: it is read with s_load_dwordx8
+//     (scalar cache, 8 rows in flight) straight into SGPR operands -- no LDS
+//     staging and no per-lane vector traffic for the train set;
 //   * per (query, train) pair: 8 v_xor + 8 v_bcnt (popcount with accumulate)
 //     + 1 v_lshl_or to form key = dist<<16 | train_idx, then the running top-2
 //     is k2 = med3(k1, k2, key), k1 = min(k1, key): branch-free, and the
@@ -16,22 +19,30 @@
 
 namespace {
 
-constexpr int kWG = 256;
+constexpr int kWG = 512;
+constexpr int kWaves = kWG / kWave;     // 8: the train rows of a chunk are split over the waves
 constexpr int kQPL = 2;                 // queries per lane
-constexpr int kQPerWG = kWG * kQPL;     // 512 queries per workgroup
-constexpr int kTChunk = 1024;           // train rows per LDS chunk (32 KiB)
+constexpr int kQPerWG = kWave * kQPL;   // 128 queries per workgroup (every wave holds all of them)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// popcount-accumulate: v_bcnt_u32_b32 d, x, acc (one VALU op per dword; the
+// compiler would otherwise split the sum into v_add3 trees)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+  uint32_t d;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(d) : "v"(x), "v"(acc));
+  return d;
+}
 
 __device__ __forceinline__ uint32_t hd8(const uint32_t (&a)[8], const uint4& x,
                                         const uint4& y) {
-  uint32_t d = __popc(a[0] ^ x.x);
-  d += __popc(a[1] ^ x.y);
-  d += __popc(a[2] ^ x.z);
-  d += __popc(a[3] ^ x.w);
-  d += __popc(a[4] ^ y.x);
-  d += __popc(a[5] ^ y.y);
-  d += __popc(a[6] ^ y.z);
-  d += __popc(a[7] ^ y.w);
+  uint32_t d = bcnt_acc(a[0] ^ x.x, 0u);
+  d = bcnt_acc(a[1] ^ x.y, d);
+  d = bcnt_acc(a[2] ^ x.z, d);
+  d = bcnt_acc(a[3] ^ x.w, d);
+  d = bcnt_acc(a[4] ^ y.x, d);
+  d = bcnt_acc(a[5] ^ y.y, d);
+  d = bcnt_acc(a[6] ^ y.z, d);
+  d = bcnt_acc(a[7] ^ y.w, d);
   return d;
 }
 
@@ -40,18 +51,33 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   return max(min(a, b), min(max(a, b), c));
 }
 
+// Top-2 keys (k1 <= k2) merged with another top-2 (a1 <= a2).
+__device__ __forceinline__ void merge2(uint32_t& k1, uint32_t& k2, uint32_t a1, uint32_t a2) {
+  const uint32_t n1 = min(k1, a1);
+  const uint32_t n2 = min(max(k1, a1), min(k2, a2));
+  k1 = n1;
+  k2 = n2;
+}
+
+// Workgroup = 128 queries of one batch item; its 8 waves each take every 8th
+// train row of the LDS chunk (so a 2000-row train set keeps 8 waves busy per
+// 128 queries and a C2 batch fills the chip), then the wave partials are
+// merged through LDS.  Keys dist << 16 | train_idx make the result
+// independent of the processing order (ties -> lower train index).
 __global__ __launch_bounds__(kWG) void knn2_kernel(
     const uint4* __restrict__ q, const int32_t* __restrict__ nq_arr, int q_cap,
     const uint4* __restrict__ t, const int32_t* __restrict__ nt_arr, int t_cap,
     int tiles_per_item, int2* __restrict__ idx2, int2* __restrict__ dist2,
     uint8_t* __restrict__ good) {
-  __shared__ uint4 lds[kTChunk * 2];
+  __shared__ uint32_t part[kWaves][2][kQPerWG];
   const int item = blockIdx.x / tiles_per_item;
   const int tile = blockIdx.x - item * tiles_per_item;
   const int nq = min(max(nq_arr[item], 0), q_cap);
   const int nt = min(max(nt_arr[item], 0), t_cap);
   const int q0 = tile * kQPerWG;
   if (q0 >= nq) return;  // uniform over the workgroup
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);  // uniform: scalar loop
 
   const uint4* qb = q + (size_t)item * q_cap * 2;
   const uint4* tb = t + (size_t)item * t_cap * 2;
@@ -60,7 +86,7 @@ __global__ __launch_bounds__(kWG) void knn2_kernel(
   uint32_t k1[kQPL], k2[kQPL];
 #pragma unroll
   for (int s = 0; s < kQPL; ++s) {
-    const int qi = q0 + s * kWG + threadIdx.x;
+    const int qi = q0 + s * kWave + lane;
     uint4 a = make_uint4(0, 0, 0, 0), b = a;
     if (qi < nq) {
       a = qb[2 * qi];
@@ -72,40 +98,65 @@ __global__ __launch_bounds__(kWG) void knn2_kernel(
     k2[s] = kNone;
   }
 
-  for (int base = 0; base < nt; base += kTChunk) {
-    const int rows = min(kTChunk, nt - base);
-    __syncthreads();
-    for (int i = threadIdx.x; i < rows * 2; i += kWG) lds[i] = tb[2 * base + i];
-    __syncthreads();
-    int j = 0;
-#pragma unroll 2
-    for (; j < rows; ++j) {
-      const uint4 x = lds[2 * j];
-      const uint4 y = lds[2 * j + 1];
-      const uint32_t jj = (uint32_t)(base + j);
+  // Train rows are uniform across the wave: read them with scalar loads
+  // (s_load_dwordx8 through the scalar cache) straight into SGPR operands of
+  // the VALU xors -- no LDS staging and no per-lane vector traffic.
+  // kRowsAhead rows per step, all loads issued before the first use, so the
+  // scalar-cache latency overlaps the previous rows' VALU work.
+  constexpr int kRowsAhead = 8;
+  int j = wid;
+  for (; j + (kRowsAhead - 1) * kWaves < nt; j += kRowsAhead * kWaves) {
+    uint4 x[kRowsAhead], y[kRowsAhead];
+#pragma unroll
+    for (int u = 0; u < kRowsAhead; ++u) {
+      x[u] = tb[2 * (j + u * kWaves)];
+      y[u] = tb[2 * (j + u * kWaves) + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kRowsAhead; ++u) {
+      const uint32_t jj = (uint32_t)(j + u * kWaves);
 #pragma unroll
       for (int s = 0; s < kQPL; ++s) {
-        const uint32_t key = (hd8(qa[s], x, y) << 16) | jj;
+        const uint32_t key = (hd8(qa[s], x[u], y[u]) << 16) | jj;
         k2[s] = umed3(k1[s], k2[s], key);
         k1[s] = min(k1[s], key);
       }
     }
   }
-
+  for (; j < nt; j += kWaves) {
+    const uint4 x = tb[2 * j];
+    const uint4 y = tb[2 * j + 1];
+    const uint32_t jj = (uint32_t)j;
+#pragma unroll
+    for (int s = 0; s < kQPL; ++s) {
+      const uint32_t key = (hd8(qa[s], x, y) << 16) | jj;
+      k2[s] = umed3(k1[s], k2[s], key);
+      k1[s] = min(k1[s], key);
+    }
+  }
+  // merge the wave partials
 #pragma unroll
   for (int s = 0; s < kQPL; ++s) {
-    const int qi = q0 + s * kWG + threadIdx.x;
-    if (qi >= nq) continue;
-    const size_t o = (size_t)item * q_cap + qi;
-    int2 id, ds;
-    id.x = k1[s] == kNone ? -1 : (int)(k1[s] & 0xFFFFu);
-    ds.x = k1[s] == kNone ? -1 : (int)(k1[s] >> 16);
-    id.y = k2[s] == kNone ? -1 : (int)(k2[s] & 0xFFFFu);
-    ds.y = k2[s] == kNone ? -1 : (int)(k2[s] >> 16);
-    idx2[o] = id;
-    dist2[o] = ds;
-    good[o] = (k2[s] != kNone && 10 * ds.x < 7 * ds.y) ? 1 : 0;
+    part[wid][0][s * kWave + lane] = k1[s];
+    part[wid][1][s * kWave + lane] = k2[s];
   }
+  __syncthreads();
+  if (threadIdx.x >= kQPerWG) return;
+  const int ql = threadIdx.x;  // local query of this workgroup
+  uint32_t m1 = part[0][0][ql], m2 = part[0][1][ql];
+#pragma unroll
+  for (int w = 1; w < kWaves; ++w) merge2(m1, m2, part[w][0][ql], part[w][1][ql]);
+  const int qi = q0 + ql;
+  if (qi >= nq) return;
+  const size_t o = (size_t)item * q_cap + qi;
+  int2 id, ds;
+  id.x = m1 == kNone ? -1 : (int)(m1 & 0xFFFFu);
+  ds.x = m1 == kNone ? -1 : (int)(m1 >> 16);
+  id.y = m2 == kNone ? -1 : (int)(m2 & 0xFFFFu);
+  ds.y = m2 == kNone ? -1 : (int)(m2 >> 16);
+  idx2[o] = id;
+  dist2[o] = ds;
+  good[o] = (m2 != kNone && 10 * ds.x < 7 * ds.y) ? 1 : 0;
 }
 
 // One workgroup per batch item: order-preserving compaction of good rows.
