@@ -29,7 +29,7 @@ namespace {
 constexpr int kNLev = 8;
 constexpr int kEdge = 31;
 constexpr int kFastT = 20;
-constexpr int kOrbWG = 1024;
+constexpr int kOrbWG = 512;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxShapes = 4;
 constexpr int kNMS0 = 29;  // score-map region starts here (needs [30, w-31])
