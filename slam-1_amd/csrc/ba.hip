@@ -28,6 +28,23 @@ namespace {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Cross-workgroup hand-off inside one launch (ticket pattern): the partials
+// are stored and loaded with agent-scope relaxed atomics, i.e. write-through
+// `sc1` stores and `sc1` loads that bypass the per-XCD L2, so no L2-wide
+// release/acquire fence is needed (MI355X_MICROARCH.md, correctness table).
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ticket_add(uint32_t* p) {
+  return __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ticket_reset(uint32_t* p) {
+  __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr double kClamp = 5000.0;
 constexpr double kDiagMin = 1e-6, kDiagMax = 1e32;
 constexpr double kLamMin = 1e-16, kLamMax = 1e32;
@@ -929,9 +946,10 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
 //   per observation: dy_o = Y_o^T dc_cam(o)                         (-> LDS)
 //   per point: dp = e - sum_o dy_o, trial point x + dp, predicted-reduction term
 //   per observation: trial residual at (cams[next], trial point)   (-> |r|^2)
-// Workgroup partial sums go to part[g] (cost) and part[G + g] (pred); the
-// last workgroup to finish (agent-scope ticket) sums them in a fixed order into
-// small[0..1] and, when DECIDE (single rank), applies the LM decision.
+// Workgroup partial sums go to part[g] (cost) and part[G + g] (pred) as sc1
+// stores; the last workgroup to finish (agent-scope ticket) sums them in a
+// fixed order into small[0..1] and, when DECIDE (single rank), applies the LM
+// decision.
 template <bool DECIDE>
 __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* __restrict__ part) {
   __shared__ double sdy[kGrp][3];
@@ -994,25 +1012,24 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* 
   v = block_sum(v, red);
   pred = block_sum(pred, red);
   if (t == 0) {
-    part[g] = v;
-    part[G + g] = pred;
-    __threadfence();  // release the partials (agent scope) before the ticket
-    last = atomicAdd(p.ticket, 1u) == (unsigned)(G - 1);
+    st_sc1(part + g, v);
+    st_sc1(part + G + g, pred);
+    __builtin_amdgcn_s_waitcnt(0);  // drained before the ticket
+    last = ticket_add(p.ticket) == (unsigned)(G - 1);
   }
   __syncthreads();
   if (!last) return;
-  __threadfence();  // acquire the other workgroups' partials
   double a = 0.0, b = 0.0;
   for (int i = t; i < G; i += kGrp) {
-    a += __builtin_nontemporal_load(part + i);
-    b += __builtin_nontemporal_load(part + G + i);
+    a += ld_sc1(part + i);
+    b += ld_sc1(part + G + i);
   }
   a = block_sum(a, red);
   b = block_sum(b, red);
   if (t == 0) {
     p.small[0] = a;
     p.small[1] = b;
-    *p.ticket = 0u;  // re-arm for the next launch (stream order)
+    ticket_reset(p.ticket);  // re-arm for the next launch
     if (DECIDE) lm_decide(p.state, p.small);
   }
 }
