@@ -586,14 +586,18 @@ __device__ bool ldl_solve(double* P, uint32_t* tab, int n, double* b, int* fail)
   return true;
 }
 
+// Inputs of the epilogue: camera gradient, Gram diagonal, live cameras and the
+// per-camera cost partials (global memory in k_solve, LDS copies prefetched at
+// kernel start in k_solve_blk so their latency is off the critical path).
+struct EpiSrc {
+  const double *g, *dU, *cam, *costc;
+};
+
 // Shared epilogue: camera step, trial cameras, predicted reduction of the camera
 // part, LM cost at the live parameters.
-__device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool ok, double* red) {
+__device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool ok, double* red,
+                               const EpiSrc& e) {
   const int C9 = 9 * p.n_cams, t = threadIdx.x;
-  const double* bvec = p.sys + (size_t)C9 * C9;
-  const double* gvec = bvec + C9;
-  const double* diagU = gvec + C9;
-  const double* costc = diagU + C9;
   double* state = p.state;
   const double lam = state[SLAM_BA_ST_LAMBDA];
   const int cur = cur_of(state);
@@ -601,15 +605,15 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
   for (int i = t; i < C9; i += blockDim.x) {
     const double d = ok ? x[i] : 0.0;
     p.delta_c[i] = d;
-    p.cams[1 - cur][i] = p.cams[cur][i] + d;
-    pc += d * (lam * clampd(diagU[i]) * d + gvec[i]);
+    p.cams[1 - cur][i] = e.cam[i] + d;
+    pc += d * (lam * clampd(e.dU[i]) * d + e.g[i]);
   }
   pc = block_sum(pc, red);  // (its barriers also publish the trial cameras to the WG)
   for (int c = t; c < p.n_cams; c += blockDim.x)
     cam_prep(p.cams[1 - cur] + 9 * c, p.camrec[1 - cur] + kCamRec * c);
   if (t == 0) {
     double cost = 0.0;
-    for (int c = 0; c < p.n_cams; ++c) cost += costc[c];
+    for (int c = 0; c < p.n_cams; ++c) cost += e.costc[c];
     state[SLAM_BA_ST_COST] = 0.5 * cost;
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
     state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : 1.0;
@@ -645,7 +649,9 @@ __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
   __syncthreads();
   const bool ok = ldl_solve<kSolveWG>(P, tab, C9, x, fail_p);
   __syncthreads();
-  solve_epilogue(p, x, ok, red);
+  const double* gvec = bvec + C9;
+  solve_epilogue(p, x, ok, red,
+                 EpiSrc{gvec, diagU, p.cams[cur_of(p.state)], gvec + 2 * C9});
 }
 
 // -DSLAM_SOLVE_PROFILE: phase timestamps (wall_clock64, 100 MHz) of k_solve_blk
@@ -688,7 +694,8 @@ constexpr int kBlkWG = 256;   // 4 waves, one per SIMD: 512 registers per lane
 constexpr int kBlkWaves = kBlkWG / 64;
 constexpr int kTileMax = 9;   // lower 16x16 tiles per wave: 4 * 9 >= 36
 constexpr int kPanelW = 9;    // columns per block step (one camera)
-constexpr int kWLs = 12;      // W/L row stride: K = 9 padded to 3 MFMA steps of 4
+constexpr int kWLs = 13;      // W/L row stride: K = 9 padded to 3 MFMA steps of 4 (odd: no LDS bank conflicts)
+static_assert(kLdsMaxN <= kBlkWG, "k_solve_blk prefetch assumes one element per thread");
 static_assert(kBlkWaves * kTileMax >= ((kLdsMaxN + 16) / 16) * ((kLdsMaxN + 16) / 16 + 1) / 2,
               "kTileMax too small");
 
@@ -712,7 +719,7 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 // LDS layout of k_solve_blk (doubles, after the kSolveHdr header)
 struct BlkLds {
   int n16;        // rows rounded up to a tile multiple (>= n + 1)
-  int pn, wl, ll, lf, dd, yy, xx, total;
+  int pn, wl, ll, lf, dd, yy, xx, ep, total;
   __host__ __device__ explicit BlkLds(int n) {
     n16 = ((n + 1 + 15) / 16) * 16;
     pn = kSolveHdr;                       // [n16][kPanelW] panel copy
@@ -722,7 +729,8 @@ struct BlkLds {
     dd = lf + ((n * (n - 1) / 2 + 1) & ~1);  // [n] D
     yy = dd + ((n + 1) & ~1);             // [n] y = L^-1 b
     xx = yy + ((n + 1) & ~1);             // [n] solution
-    total = xx + ((n + 1) & ~1);
+    ep = xx + ((n + 1) & ~1);             // [5][n] b, g, diagU, live cameras, cost partials
+    total = ep + 5 * ((n + 1) & ~1);
   }
 };
 
@@ -747,9 +755,11 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int NT = g.n16 / 16, NL = NT * (NT + 1) / 2;
   SOLVE_PROF_T(0);
+  const int n2 = (n + 1) & ~1;
   if (t == 0) *fail_p = 0;
   for (int i = t; i < 2 * g.n16 * kWLs; i += kBlkWG) WL[i] = 0.0;  // WL and LL
-  // this wave's tiles: tl = wid + 8 s -> (I, J), I >= J
+  // this wave's tiles: tl = wid + 4 s -> (I, J), I >= J.  All S loads are
+  // issued unconditionally (clamped addresses) before any is used.
   int tI[kTileMax], tJ[kTileMax];
   d4 acc[kTileMax];
 #pragma unroll
@@ -759,19 +769,35 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
     while ((I + 1) * (I + 2) / 2 <= tl) ++I;
     tI[s] = tl < NL ? I : -1;
     tJ[s] = tl < NL ? tl - I * (I + 1) / 2 : -1;
+    const int col = min(max(tJ[s], 0) * 16 + (lane & 15), n - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = min(max(tI[s], 0) * 16 + (lane >> 4) + 4 * q, n - 1);
+      acc[s][q] = S[(size_t)row * n + col];
+    }
+  }
+  double* Eb = lds + g.ep;  // prefetch: b, g, diagU, live cameras, cost partials
+  {
+    const double* src[5] = {bvec, bvec + n, diagU, p.cams[cur_of(p.state)], diagU + n};
+    const int len[5] = {n, n, n, n, p.n_cams};
+    double v[5];  // n <= kLdsMaxN < kBlkWG: one element per thread, loads issued together
+#pragma unroll
+    for (int a = 0; a < 5; ++a) v[a] = src[a][min(t, len[a] - 1)];
+#pragma unroll
+    for (int a = 0; a < 5; ++a)
+      if (t < len[a]) Eb[a * n2 + t] = v[a];
+  }
+  __syncthreads();  // prefetched b and diagU
+#pragma unroll
+  for (int s = 0; s < kTileMax; ++s) {
     const int col = tJ[s] * 16 + (lane & 15);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = tI[s] * 16 + (lane >> 4) + 4 * q;
-      double a = 0.0;
-      if (tl < NL && col < n) {
-        if (row < n) {
-          a = S[(size_t)row * n + col];
-          if (row == col) a += lam * clampd(diagU[row]);
-        } else if (row == n) {
-          a = bvec[col];
-        }
-      }
+      double a = acc[s][q];
+      if (row == col) a += lam * clampd(Eb[2 * n2 + col]);
+      if (row == n) a = Eb[min(col, n - 1)];
+      if (tI[s] < 0 || col >= n || row > n) a = 0.0;
       acc[s][q] = a;
     }
   }
@@ -848,14 +874,21 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
         if (r == n) {
 #pragma unroll
           for (int j = 0; j < kPanelW; ++j) Yy[c0 + j] = u[j];
-        } else {
-          const int m = r - c0;  // >= 9 below the panel
+        } else if (r >= c0 + kPanelW) {
           double* lf = LF + r * (r - 1) / 2 + c0;
 #pragma unroll
-          for (int j = 0; j < kPanelW; ++j) {
-            if (j < m) lf[j] = u[j] * Dinv[j];
-            if (j == m) Dd[c0 + j] = u[j];
-          }
+          for (int j = 0; j < kPanelW; ++j) lf[j] = u[j] * Dinv[j];
+        }
+      }
+      // the panel's own factor rows and D from the diagonal-block factor every
+      // lane holds (one lane stores them: no per-column divergent branches)
+      if (t == 0) {
+#pragma unroll
+        for (int m = 0; m < kPanelW; ++m) {
+          Dd[c0 + m] = A[m][m];
+          double* lf = LF + (c0 + m) * (c0 + m - 1) / 2 + c0;
+#pragma unroll
+          for (int j = 0; j < m; ++j) lf[j] = A[m][j];
         }
       }
       if (wid == 0 && lane == 0 && bad) *fail_p = 1;
@@ -908,35 +941,60 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
   }
   SOLVE_PROF_T(2);
   if (ok && wid == 0) {
-    // z = D^-1 y, then L^T x = z from the bottom; lane l holds rows l, l + 64
+    // z = D^-1 y, then L^T x = z from the bottom; lane l holds rows l, l + 64.
+    // Step k: x_i -= L(k, i) x_k for i < k, x_k broadcast by v_readlane.  Rows
+    // k >= 64 update every x0 (i = lane < 64 <= k, no mask) and the x1 rows
+    // below k; rows k < 64 update x0 only.  The L rows of kBackU steps are
+    // loaded (clamped, then masked by a select) ahead of the dependent chain.
     double x0 = lane < n ? Yy[lane] / Dd[lane] : 0.0;
     double x1 = lane + 64 < n ? Yy[lane + 64] / Dd[lane + 64] : 0.0;
-    // rows of L are loaded kBackU at a time ahead of the dependent x updates
     constexpr int kBackU = 8;
-    for (int k = n - 1; k > 0; k -= kBackU) {
+    int k = n - 1;
+    for (; k - kBackU + 1 >= 64; k -= kBackU) {
       double l0[kBackU], l1[kBackU];
 #pragma unroll
       for (int u = 0; u < kBackU; ++u) {
-        const int kk = max(k - u, 1);
-        const double* Lk = LF + kk * (kk - 1) / 2;  // L(kk, i), i < kk
-        l0[u] = lane < kk ? Lk[lane] : 0.0;
-        l1[u] = lane + 64 < kk ? Lk[lane + 64] : 0.0;
+        const int kk = k - u;
+        const double* Lk = LF + kk * (kk - 1) / 2;
+        l0[u] = Lk[lane];
+        const double v = Lk[min(lane + 64, kk - 1)];
+        l1[u] = lane + 64 < kk ? v : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < kBackU; ++u) {
-        const int kk = k - u;
-        if (kk <= 0) break;  // uniform
-        const double xk = kk < 64 ? readlane_d(x0, kk) : readlane_d(x1, kk - 64);
+        const double xk = readlane_d(x1, k - u - 64);
         x0 = __builtin_fma(-l0[u], xk, x0);
         x1 = __builtin_fma(-l1[u], xk, x1);
       }
+    }
+    for (; k >= 64; --k) {
+      const double* Lk = LF + k * (k - 1) / 2;
+      const double v = Lk[min(lane + 64, k - 1)];
+      const double xk = readlane_d(x1, k - 64);
+      x0 = __builtin_fma(-Lk[lane], xk, x0);
+      x1 = __builtin_fma(-(lane + 64 < k ? v : 0.0), xk, x1);
+    }
+    for (; k - kBackU + 1 >= 1; k -= kBackU) {
+      double l0[kBackU];
+#pragma unroll
+      for (int u = 0; u < kBackU; ++u) {
+        const int kk = k - u;
+        const double v = LF[kk * (kk - 1) / 2 + min(lane, kk - 1)];
+        l0[u] = lane < kk ? v : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kBackU; ++u) x0 = __builtin_fma(-l0[u], readlane_d(x0, k - u), x0);
+    }
+    for (; k >= 1; --k) {
+      const double v = LF[k * (k - 1) / 2 + min(lane, k - 1)];
+      x0 = __builtin_fma(-(lane < k ? v : 0.0), readlane_d(x0, k), x0);
     }
     if (lane < n) X[lane] = x0;
     if (lane + 64 < n) X[lane + 64] = x1;
   }
   __syncthreads();
   SOLVE_PROF_T(3);
-  solve_epilogue(p, X, ok, red);
+  solve_epilogue(p, X, ok, red, EpiSrc{Eb + n2, Eb + 2 * n2, Eb + 3 * n2, Eb + 4 * n2});
   SOLVE_PROF_END();
 }
 
