@@ -142,6 +142,33 @@ int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count
                     double reproj_thresh, int hyp_iters, int refine_iters, double* d_rvec,
                     double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, void* stream);
 
+/* The reference's stereo visual-odometry pose estimator
+ * (visual_odometry.py:135-157 estimate_pose over the residuals of :65-81),
+ * restated deterministically (oracle/vo.c): dof = (rotvec, t), T = [R | t];
+ * residuals f (4N) = [proj(P T, Q2) - q1 (x row, y row), proj(P T^-1, Q1) - q2
+ * (x row, y row)]; max_iter hypotheses of 6 points drawn WITH replacement from
+ * splitmix64(seed, item0 + b, h) (np.random.choice(range(n), 6), :139), LM from
+ * dof = 0 (lm_iters; least_squares(method='lm') at :142), error = sum over k of
+ * |(f[2k], f[2k+1])| (the reshape((2N, 2)) of :144-146), sequential early stop
+ * after early_stop non-improving hypotheses (:147-154; 5 in the reference).
+ * One workgroup per item, one lane per hypothesis (max_iter <= 128).
+ * d_q1/d_q2 [batch][cap][2], d_Q1/d_Q2 [batch][cap][3] f64, d_P 3x4 row-major.
+ * Outputs: d_pose [batch][6] (rotvec, t) of the selected hypothesis (zeros when
+ * none improved), d_best [batch] its index (-1 if none), d_ntried [batch]
+ * hypotheses the sequential loop evaluates, d_err [batch] its error. */
+int slam_vo_estimate_pose(const double* d_q1, const double* d_q2, const double* d_Q1,
+                          const double* d_Q2, const int32_t* d_count, int cap, int batch,
+                          const double* d_P, uint64_t seed, int item0, int max_iter,
+                          int lm_iters, int early_stop, double* d_pose, int32_t* d_best,
+                          int32_t* d_ntried, double* d_err, void* stream);
+
+/* reprojection_residuals(dof, q1, q2, Q1, Q2) (visual_odometry.py:65-81) for
+ * one dof per item: d_dof [batch][6]; d_res [batch][4 * cap], the first
+ * 4 * count[b] entries in the reference's flattened order. */
+int slam_vo_residuals(const double* d_dof, const double* d_q1, const double* d_q2,
+                      const double* d_Q1, const double* d_Q2, const int32_t* d_count, int cap,
+                      int batch, const double* d_P, double* d_res, void* stream);
+
 /* ------------------------------------------------------------------------
  * Tiled ORB detector + rBRIEF descriptor.
  *

@@ -8,6 +8,9 @@
   rodrigues / form_transf / calculate_transformation_matrix
                             transformation.py:5-37 (incl. the r, t sign flip)
   pnp_ransac                oracle/geometry.c (seeded RANSAC + LM spec)
+  vo_residuals / vo_estimate_pose
+                            visual_odometry.py:65-81, 135-157 -> oracle/vo.c
+                            (seeded 6-point samples + analytic-Jacobian LM spec)
 """
 from __future__ import annotations
 
@@ -126,3 +129,62 @@ def pnp_ransac(Q, q, K, seed=0, item=0, n_hyp=100, thresh=8.0, hyp_iters=10, ref
                   hyp_iters, refine_iters, _ptr(rvec), _ptr(tvec), _ptr(mask), _ptr(hyp), _ptr(hc))
     out = (rvec, tvec, n, mask[:L].astype(bool))
     return out + (hyp, hc) if return_hypotheses else out
+
+
+_VO = None
+
+
+def _vo_fns():
+    global _VO
+    if _VO is None:
+        L = lib()
+        p, i, u = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+        L.oracle_vo_residuals.argtypes = [p, p, p, p, p, i, p, p]
+        L.oracle_vo_residuals.restype = None
+        L.oracle_vo_hypothesis.argtypes = [p, p, p, p, i, p, u, i, i, i, p, p]
+        L.oracle_vo_hypothesis.restype = None
+        L.oracle_vo_estimate_pose.argtypes = [p, p, p, p, i, p, u, i, i, i, i, p, p, p, p]
+        L.oracle_vo_estimate_pose.restype = ctypes.c_int
+        _VO = L
+    return _VO
+
+
+def _vo_in(q1, q2, Q1, Q2, P):
+    return (np.ascontiguousarray(q1, np.float64).reshape(-1, 2),
+            np.ascontiguousarray(q2, np.float64).reshape(-1, 2),
+            np.ascontiguousarray(Q1, np.float64).reshape(-1, 3),
+            np.ascontiguousarray(Q2, np.float64).reshape(-1, 3),
+            np.ascontiguousarray(P, np.float64).reshape(3, 4))
+
+
+def vo_residuals(dof, q1, q2, Q1, Q2, P):
+    """reprojection_residuals (visual_odometry.py:65-81): flat (4N,)."""
+    q1, q2, Q1, Q2, P = _vo_in(q1, q2, Q1, Q2, P)
+    N = len(q1)
+    f = np.zeros(max(4 * N, 1))
+    d = np.ascontiguousarray(dof, np.float64).reshape(6)
+    _vo_fns().oracle_vo_residuals(_ptr(d), _ptr(q1), _ptr(q2), _ptr(Q1), _ptr(Q2), N, _ptr(P), _ptr(f))
+    return f[:4 * N]
+
+
+def vo_hypothesis(q1, q2, Q1, Q2, P, seed=0, item=0, h=0, lm_iters=20):
+    """One hypothesis of estimate_pose: (dof after LM, its 6 sample indices)."""
+    q1, q2, Q1, Q2, P = _vo_in(q1, q2, Q1, Q2, P)
+    dof = np.zeros(6)
+    idx = np.zeros(6, np.int32)
+    _vo_fns().oracle_vo_hypothesis(_ptr(q1), _ptr(q2), _ptr(Q1), _ptr(Q2), len(q1), _ptr(P),
+                                   seed & ((1 << 64) - 1), item, h, lm_iters, _ptr(dof), _ptr(idx))
+    return dof, idx
+
+
+def vo_estimate_pose(q1, q2, Q1, Q2, P, seed=0, item=0, max_iter=100, lm_iters=20, early_stop=5):
+    """estimate_pose (visual_odometry.py:135-157) -> (dof, best, ntried, error, errs[max_iter])."""
+    q1, q2, Q1, Q2, P = _vo_in(q1, q2, Q1, Q2, P)
+    dof = np.zeros(6)
+    nt = ctypes.c_int(0)
+    err = ctypes.c_double(0.0)
+    errs = np.zeros(max_iter)
+    best = _vo_fns().oracle_vo_estimate_pose(
+        _ptr(q1), _ptr(q2), _ptr(Q1), _ptr(Q2), len(q1), _ptr(P), seed & ((1 << 64) - 1), item,
+        max_iter, lm_iters, early_stop, _ptr(dof), ctypes.byref(nt), ctypes.byref(err), _ptr(errs))
+    return dof, best, nt.value, err.value, errs

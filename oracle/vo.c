@@ -1,0 +1,227 @@
+/*
+ * ORACLE — test infrastructure only (see oracle/__init__.py).
+ *
+ * CPU restatement of the reference's stereo visual-odometry pose estimator:
+ *   /root/reference/visual_odometry.py:65-81   reprojection_residuals(dof, q1, q2, Q1, Q2)
+ *   /root/reference/visual_odometry.py:135-157 estimate_pose(q1, q2, Q1, Q2, max_iter=100)
+ * dof = (rotvec r, t), T = [R(r) | t] (_form_transf, :57-63);
+ *   f = [proj(P_l T, Q2) - q1 (x row, y row), proj(P_l T^-1, Q1) - q2 (x row, y row)]
+ * (np.vstack(...).flatten(), :81).  The reference samples with NumPy's global
+ * RNG and solves each sample with scipy least_squares(method='lm') (MINPACK,
+ * finite differences); neither sequence is reproducible, so PARITY IS UNPINNED
+ * against them and the spec both this oracle and the HIP kernel follow is:
+ *   - hypothesis h draws 6 indices WITH replacement (np.random.choice(range(n), 6))
+ *     from splitmix64 seeded with seed ^ (item * C1) ^ (h * C2);
+ *   - LM with the analytic Jacobian from dof = 0 on the sample (lambda 1e-3,
+ *     x0.1 / x10, Marquardt diagonal), lm_iters iterations;
+ *   - error = sum_k sqrt(f[2k]^2 + f[2k+1]^2), k ascending: the reshape((2N, 2))
+ *     of :144-145 pairs CONSECUTIVE entries of the flat f;
+ *   - the sequential selection of :147-154 (strict <, early stop after
+ *     early_stop non-improving hypotheses); no improvement -> dof = 0.
+ * The converged LM optimum is cross-checked against scipy least_squares(lm)
+ * in tests/test_geometry.py.  Operation order matches csrc/geometry.hip.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "pose_util.h"
+
+#define VO_SAMPLE 6
+
+static void project(const double* P, const double X[3], int jac, double uv[2], double a[2][3]) {
+  const double x0 = P[0] * X[0] + P[1] * X[1] + P[2] * X[2] + P[3];
+  const double x1 = P[4] * X[0] + P[5] * X[1] + P[6] * X[2] + P[7];
+  const double x2 = P[8] * X[0] + P[9] * X[1] + P[10] * X[2] + P[11];
+  const double iz = 1.0 / x2;
+  uv[0] = x0 * iz;
+  uv[1] = x1 * iz;
+  if (jac)
+    for (int k = 0; k < 3; ++k) {
+      a[0][k] = (P[k] - uv[0] * P[8 + k]) * iz;
+      a[1][k] = (P[4 + k] - uv[1] * P[8 + k]) * iz;
+    }
+}
+
+/* d(R X)/dw (sgn +1) and d(R^T X)/dw (sgn -1), Gallego & Yezzi 2015 */
+static void drot(const double w[3], const double R[9], const double X[3], int sgn, double D[3][3]) {
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (th2 < 1e-24) {
+    const double s = sgn > 0 ? -1.0 : 1.0;
+    D[0][0] = 0.0; D[0][1] = -s * X[2]; D[0][2] = s * X[1];
+    D[1][0] = s * X[2]; D[1][1] = 0.0; D[1][2] = -s * X[0];
+    D[2][0] = -s * X[1]; D[2][1] = s * X[0]; D[2][2] = 0.0;
+    return;
+  }
+  const double W[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+  double Am[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      double acc = w[i] * w[k];
+      if (sgn > 0) {
+        for (int j = 0; j < 3; ++j) acc += R[3 * j + i] * W[j][k];
+        Am[i][k] = acc - W[i][k];
+      } else {
+        for (int j = 0; j < 3; ++j) acc -= R[3 * i + j] * W[j][k];
+        Am[i][k] = acc + W[i][k];
+      }
+    }
+  const double Xs[3][3] = {{0.0, -X[2], X[1]}, {X[2], 0.0, -X[0]}, {-X[1], X[0], 0.0}};
+  double B[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k)
+      B[i][k] = Xs[i][0] * Am[0][k] + Xs[i][1] * Am[1][k] + Xs[i][2] * Am[2][k];
+  const double inv = (sgn > 0 ? -1.0 : 1.0) / th2;
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      const double m0 = sgn > 0 ? R[3 * i] : R[i], m1 = sgn > 0 ? R[3 * i + 1] : R[3 + i],
+                   m2 = sgn > 0 ? R[3 * i + 2] : R[6 + i];
+      D[i][k] = (m0 * B[0][k] + m1 * B[1][k] + m2 * B[2][k]) * inv;
+    }
+}
+
+/* the 4 residuals of one point pair and optionally the 4x6 Jacobian */
+static void residual4(const double p[6], const double R[9], const double* P, const double* Q1,
+                      const double* Q2, const double* q1, const double* q2, double r[4],
+                      double J[4][6]) {
+  double X[3], Y[3], Z[3], uv[2], a[2][3], D[3][3];
+  for (int i = 0; i < 3; ++i) X[i] = R[3 * i] * Q2[0] + R[3 * i + 1] * Q2[1] + R[3 * i + 2] * Q2[2] + p[3 + i];
+  for (int i = 0; i < 3; ++i) Z[i] = Q1[i] - p[3 + i];
+  for (int i = 0; i < 3; ++i) Y[i] = R[i] * Z[0] + R[3 + i] * Z[1] + R[6 + i] * Z[2];
+  project(P, X, J != NULL, uv, a);
+  r[0] = uv[0] - q1[0];
+  r[1] = uv[1] - q1[1];
+  if (J) {
+    drot(p, R, Q2, +1, D);
+    for (int c = 0; c < 2; ++c)
+      for (int k = 0; k < 3; ++k) {
+        J[c][k] = a[c][0] * D[0][k] + a[c][1] * D[1][k] + a[c][2] * D[2][k];
+        J[c][3 + k] = a[c][k];
+      }
+  }
+  project(P, Y, J != NULL, uv, a);
+  r[2] = uv[0] - q2[0];
+  r[3] = uv[1] - q2[1];
+  if (J) {
+    drot(p, R, Z, -1, D);
+    for (int c = 0; c < 2; ++c)
+      for (int k = 0; k < 3; ++k) {
+        J[2 + c][k] = a[c][0] * D[0][k] + a[c][1] * D[1][k] + a[c][2] * D[2][k];
+        J[2 + c][3 + k] = -(a[c][0] * R[3 * k] + a[c][1] * R[3 * k + 1] + a[c][2] * R[3 * k + 2]);
+      }
+  }
+}
+
+/* element i of the flat residual vector (one projection) */
+static double elem(const double p[6], const double R[9], const double* P, const double* Q1,
+                   const double* Q2, const double* q1, const double* q2, int N, int i) {
+  const int row = i / N, col = i - row * N;
+  double X[3], uv[2], a[2][3];
+  if (row < 2) {
+    const double* Q = Q2 + 3 * col;
+    for (int k = 0; k < 3; ++k) X[k] = R[3 * k] * Q[0] + R[3 * k + 1] * Q[1] + R[3 * k + 2] * Q[2] + p[3 + k];
+    project(P, X, 0, uv, a);
+    return uv[row] - q1[2 * col + row];
+  }
+  const double* Q = Q1 + 3 * col;
+  const double Z[3] = {Q[0] - p[3], Q[1] - p[4], Q[2] - p[5]};
+  for (int k = 0; k < 3; ++k) X[k] = R[k] * Z[0] + R[3 + k] * Z[1] + R[6 + k] * Z[2];
+  project(P, X, 0, uv, a);
+  return uv[row - 2] - q2[2 * col + row - 2];
+}
+
+/* reprojection_residuals (:65-81): f[4N] */
+void oracle_vo_residuals(const double* dof, const double* q1, const double* q2, const double* Q1,
+                         const double* Q2, int N, const double* P, double* f) {
+  double R[9];
+  rodrigues(dof, R);
+  for (int i = 0; i < 4 * N; ++i) f[i] = elem(dof, R, P, Q1, Q2, q1, q2, N, i);
+}
+
+/* LM of one hypothesis on its 6-point sample; returns the sample indices too */
+void oracle_vo_hypothesis(const double* q1, const double* q2, const double* Q1, const double* Q2,
+                          int N, const double* P, uint64_t seed, int item, int h, int lm_iters,
+                          double pp[6], int idx[VO_SAMPLE]) {
+  uint64_t s = seed ^ ((uint64_t)item * 0xD1B54A32D192ED03ull) ^ ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+  for (int k = 0; k < VO_SAMPLE; ++k) idx[k] = (int)((splitmix64(&s) >> 32) % (uint64_t)N);
+  double lam = 1e-3, R[9];
+  memset(pp, 0, 6 * sizeof(double));
+  for (int it = 0; it < lm_iters; ++it) {
+    rodrigues(pp, R);
+    double H[21] = {0}, g[6] = {0}, cost = 0.0;
+    for (int k = 0; k < VO_SAMPLE; ++k) {
+      const int v = idx[k];
+      double r[4], J[4][6];
+      residual4(pp, R, P, Q1 + 3 * v, Q2 + 3 * v, q1 + 2 * v, q2 + 2 * v, r, J);
+      for (int a = 0; a < 4; ++a) {
+        int m = 0;
+        for (int i = 0; i < 6; ++i) {
+          for (int j = 0; j <= i; ++j) H[m++] += J[a][i] * J[a][j];
+          g[i] += J[a][i] * r[a];
+        }
+        cost += r[a] * r[a];
+      }
+    }
+    double d[6], pn[6], Rn[9];
+    if (!solve6(H, g, lam, d)) {
+      lam = fmin(lam * 10.0, 1e12);
+      continue;
+    }
+    for (int i = 0; i < 6; ++i) pn[i] = pp[i] + d[i];
+    rodrigues(pn, Rn);
+    double cn = 0.0;
+    for (int k = 0; k < VO_SAMPLE; ++k) {
+      const int v = idx[k];
+      double r[4];
+      residual4(pn, Rn, P, Q1 + 3 * v, Q2 + 3 * v, q1 + 2 * v, q2 + 2 * v, r, NULL);
+      cn += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    }
+    if (cn < cost) {
+      memcpy(pp, pn, sizeof(pn));
+      lam = fmax(lam * 0.1, 1e-12);
+    } else {
+      lam = fmin(lam * 10.0, 1e12);
+    }
+  }
+}
+
+/* estimate_pose (:135-157).  Returns the selected hypothesis index (-1 if none);
+ * pose <- its dof; *ntried <- hypotheses the sequential loop evaluates;
+ * errs[h] (optional, max_iter) <- every hypothesis' error. */
+int oracle_vo_estimate_pose(const double* q1, const double* q2, const double* Q1, const double* Q2,
+                            int N, const double* P, uint64_t seed, int item, int max_iter,
+                            int lm_iters, int early_stop, double* pose, int* ntried, double* err,
+                            double* errs) {
+  memset(pose, 0, 6 * sizeof(double));
+  *ntried = 0;
+  *err = INFINITY;
+  if (N <= 0) return -1;
+  double mn = INFINITY;
+  int best = -1, early = 0;
+  for (int h = 0; h < max_iter; ++h) {
+    double pp[6], R[9];
+    int idx[VO_SAMPLE];
+    oracle_vo_hypothesis(q1, q2, Q1, Q2, N, P, seed, item, h, lm_iters, pp, idx);
+    rodrigues(pp, R);
+    double e = 0.0;
+    for (int k = 0; k < 2 * N; ++k) {
+      const double f0 = elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k);
+      const double f1 = elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k + 1);
+      e += sqrt(f0 * f0 + f1 * f1);
+    }
+    if (errs) errs[h] = e;
+    if (*ntried) continue;  /* sequential loop already stopped: only record errs */
+    if (e < mn) {
+      mn = e;
+      best = h;
+      early = 0;
+      memcpy(pose, pp, sizeof(pp));
+    } else {
+      ++early;
+    }
+    if (early == early_stop) *ntried = h + 1;
+  }
+  if (!*ntried) *ntried = max_iter;
+  *err = mn;
+  return best;
+}

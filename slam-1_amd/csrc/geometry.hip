@@ -480,6 +480,260 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
   if (t == 0) ninl[b] = hcnt[bh];
 }
 
+
+// --------------------------------------------------------------- stereo VO pose
+// The reference's second pose estimator (visual_odometry.py:65-81, 135-157):
+// dof = (rotvec r, t), T = [R(r) | t];
+//   forward  q1_pred = proj(P_l T,      Q2)   vs q1
+//   backward q2_pred = proj(P_l T^-1,   Q1)   vs q2
+// residual vector f (4N) = [fwd x (N), fwd y (N), bwd x (N), bwd y (N)]
+// (np.vstack([q1_pred - q1.T, q2_pred - q2.T]).flatten(), :81).
+// estimate_pose: max_iter hypotheses of 6 points drawn WITH replacement
+// (np.random.choice(range(n), 6), :139), LM from dof = 0 on the sample (:142),
+// error = sum of the norms of CONSECUTIVE PAIRS of f (the reshape((2N, 2)) of
+// :144-146 pairs f[2k], f[2k+1]), sequential early termination after 5
+// non-improving hypotheses (:147-154).  All hypotheses run in parallel (one per
+// lane) and the sequential rule is applied to their errors in order, which
+// selects exactly what the sequential loop would.
+constexpr int kVoWG = 128;
+constexpr int kVoSample = 6;
+
+// X -> (u, v) with P (3x4 row-major); a0/a1: d(u, v)/dX when JAC
+template <bool JAC>
+__device__ inline void vo_project(const double* P, const double X[3], double uv[2], double a[2][3]) {
+  const double x0 = P[0] * X[0] + P[1] * X[1] + P[2] * X[2] + P[3];
+  const double x1 = P[4] * X[0] + P[5] * X[1] + P[6] * X[2] + P[7];
+  const double x2 = P[8] * X[0] + P[9] * X[1] + P[10] * X[2] + P[11];
+  const double iz = 1.0 / x2;
+  uv[0] = x0 * iz;
+  uv[1] = x1 * iz;
+  if constexpr (JAC) {
+    for (int k = 0; k < 3; ++k) {
+      a[0][k] = (P[k] - uv[0] * P[8 + k]) * iz;
+      a[1][k] = (P[4 + k] - uv[1] * P[8 + k]) * iz;
+    }
+  }
+}
+
+// d(R(w) X)/dw (sgn = +1) and d(R(w)^T X)/dw (sgn = -1), Gallego & Yezzi 2015:
+//   d(R X)/dw   = -R  [X]x (w w^T + (R^T - I)[w]x) / |w|^2
+//   d(R^T X)/dw =  R^T [X]x (w w^T - (R - I)[w]x) / |w|^2
+// with the first-order forms -[RX]x and [X]x at w = 0.
+__device__ inline void vo_drot(const double w[3], const double R[9], const double X[3], int sgn,
+                               double D[3][3]) {
+  const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  if (th2 < 1e-24) {
+    // sgn > 0: -[R X]x = -[X]x (R = I); sgn < 0: [X]x
+    const double s = sgn > 0 ? -1.0 : 1.0;
+    D[0][0] = 0.0; D[0][1] = -s * X[2]; D[0][2] = s * X[1];
+    D[1][0] = s * X[2]; D[1][1] = 0.0; D[1][2] = -s * X[0];
+    D[2][0] = -s * X[1]; D[2][1] = s * X[0]; D[2][2] = 0.0;
+    return;
+  }
+  const double W[3][3] = {{0.0, -w[2], w[1]}, {w[2], 0.0, -w[0]}, {-w[1], w[0], 0.0}};
+  double Am[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      double acc = w[i] * w[k];
+      if (sgn > 0) {
+        for (int j = 0; j < 3; ++j) acc += R[3 * j + i] * W[j][k];  // R^T W
+        Am[i][k] = acc - W[i][k];
+      } else {
+        for (int j = 0; j < 3; ++j) acc -= R[3 * i + j] * W[j][k];  // - R W
+        Am[i][k] = acc + W[i][k];
+      }
+    }
+  const double Xs[3][3] = {{0.0, -X[2], X[1]}, {X[2], 0.0, -X[0]}, {-X[1], X[0], 0.0}};
+  double B[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k)
+      B[i][k] = Xs[i][0] * Am[0][k] + Xs[i][1] * Am[1][k] + Xs[i][2] * Am[2][k];
+  const double inv = (sgn > 0 ? -1.0 : 1.0) / th2;
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) {
+      // sgn > 0: R B; sgn < 0: R^T B
+      const double m0 = sgn > 0 ? R[3 * i] : R[i], m1 = sgn > 0 ? R[3 * i + 1] : R[3 + i],
+                   m2 = sgn > 0 ? R[3 * i + 2] : R[6 + i];
+      D[i][k] = (m0 * B[0][k] + m1 * B[1][k] + m2 * B[2][k]) * inv;
+    }
+}
+
+// the 4 residuals of point pair (Q1, Q2, q1, q2) and optionally the 4x6 Jacobian
+template <bool JAC>
+__device__ inline void vo_residual(const double p[6], const double R[9], const double* P,
+                                   const double* Q1, const double* Q2, const double* q1,
+                                   const double* q2, double r[4], double J[4][6]) {
+  double X[3], Y[3], Z[3], uv[2], a[2][3];
+  for (int i = 0; i < 3; ++i) X[i] = R[3 * i] * Q2[0] + R[3 * i + 1] * Q2[1] + R[3 * i + 2] * Q2[2] + p[3 + i];
+  for (int i = 0; i < 3; ++i) Z[i] = Q1[i] - p[3 + i];
+  for (int i = 0; i < 3; ++i) Y[i] = R[i] * Z[0] + R[3 + i] * Z[1] + R[6 + i] * Z[2];
+  vo_project<JAC>(P, X, uv, a);
+  r[0] = uv[0] - q1[0];
+  r[1] = uv[1] - q1[1];
+  if constexpr (JAC) {
+    double D[3][3];
+    vo_drot(p, R, Q2, +1, D);
+    for (int c = 0; c < 2; ++c)
+      for (int k = 0; k < 3; ++k) {
+        J[c][k] = a[c][0] * D[0][k] + a[c][1] * D[1][k] + a[c][2] * D[2][k];
+        J[c][3 + k] = a[c][k];
+      }
+  }
+  vo_project<JAC>(P, Y, uv, a);
+  r[2] = uv[0] - q2[0];
+  r[3] = uv[1] - q2[1];
+  if constexpr (JAC) {
+    double D[3][3];
+    vo_drot(p, R, Z, -1, D);
+    for (int c = 0; c < 2; ++c)
+      for (int k = 0; k < 3; ++k) {
+        J[2 + c][k] = a[c][0] * D[0][k] + a[c][1] * D[1][k] + a[c][2] * D[2][k];
+        // dY/dt = -R^T
+        J[2 + c][3 + k] = -(a[c][0] * R[3 * k] + a[c][1] * R[3 * k + 1] + a[c][2] * R[3 * k + 2]);
+      }
+  }
+}
+
+// element i of the flat residual vector f (one projection)
+__device__ inline double vo_elem(const double p[6], const double R[9], const double* P,
+                                 const double* Q1, const double* Q2, const double* q1,
+                                 const double* q2, int N, int i) {
+  const int row = i / N, col = i - row * N;
+  double X[3], uv[2], a[2][3];
+  if (row < 2) {
+    const double* Q = Q2 + 3 * col;
+    for (int k = 0; k < 3; ++k) X[k] = R[3 * k] * Q[0] + R[3 * k + 1] * Q[1] + R[3 * k + 2] * Q[2] + p[3 + k];
+    vo_project<false>(P, X, uv, a);
+    return uv[row] - q1[2 * col + row];
+  }
+  const double* Q = Q1 + 3 * col;
+  const double Z[3] = {Q[0] - p[3], Q[1] - p[4], Q[2] - p[5]};
+  for (int k = 0; k < 3; ++k) X[k] = R[k] * Z[0] + R[3 + k] * Z[1] + R[6 + k] * Z[2];
+  vo_project<false>(P, X, uv, a);
+  return uv[row - 2] - q2[2 * col + row - 2];
+}
+
+__global__ __launch_bounds__(kVoWG) void k_vo_pose(
+    const double* __restrict__ q1a, const double* __restrict__ q2a, const double* __restrict__ Q1a,
+    const double* __restrict__ Q2a, const int32_t* __restrict__ count, int cap,
+    const double* __restrict__ Pg, uint64_t seed, int item0, int max_iter, int lm_iters,
+    int early_stop, double* __restrict__ pose, int32_t* __restrict__ best_out,
+    int32_t* __restrict__ ntried, double* __restrict__ err_out) {
+  __shared__ double hp[kVoWG][6];
+  __shared__ double herr[kVoWG];
+  const int b = blockIdx.x, h = threadIdx.x;
+  const int N = min(max(count[b], 0), cap);
+  const double* q1 = q1a + (size_t)b * cap * 2;
+  const double* q2 = q2a + (size_t)b * cap * 2;
+  const double* Q1 = Q1a + (size_t)b * cap * 3;
+  const double* Q2 = Q2a + (size_t)b * cap * 3;
+  double P[12];
+  for (int i = 0; i < 12; ++i) P[i] = Pg[i];
+  if (N > 0 && h < max_iter) {
+    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+    double sQ1[kVoSample][3], sQ2[kVoSample][3], sq1[kVoSample][2], sq2[kVoSample][2];
+    for (int k = 0; k < kVoSample; ++k) {
+      const int v = (int)((splitmix64(s) >> 32) % (uint64_t)N);  // with replacement
+      for (int c = 0; c < 3; ++c) {
+        sQ1[k][c] = Q1[3 * v + c];
+        sQ2[k][c] = Q2[3 * v + c];
+      }
+      for (int c = 0; c < 2; ++c) {
+        sq1[k][c] = q1[2 * v + c];
+        sq2[k][c] = q2[2 * v + c];
+      }
+    }
+    // LM on the sample from dof = 0 (Marquardt diagonal, lambda x0.1 / x10)
+    double pp[6] = {0, 0, 0, 0, 0, 0}, lam = 1e-3, R[9];
+    for (int it = 0; it < lm_iters; ++it) {
+      rodrigues(pp, R);
+      double H[21] = {0}, g[6] = {0}, cost = 0.0;
+      for (int k = 0; k < kVoSample; ++k) {
+        double r[4], J[4][6];
+        vo_residual<true>(pp, R, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+        for (int a = 0; a < 4; ++a) {
+          int m = 0;
+          for (int i = 0; i < 6; ++i) {
+            for (int j = 0; j <= i; ++j) H[m++] += J[a][i] * J[a][j];
+            g[i] += J[a][i] * r[a];
+          }
+          cost += r[a] * r[a];
+        }
+      }
+      double d[6], pn[6], Rn[9];
+      if (!solve6(H, g, lam, d)) {
+        lam = fmin(lam * 10.0, 1e12);
+        continue;
+      }
+      for (int i = 0; i < 6; ++i) pn[i] = pp[i] + d[i];
+      rodrigues(pn, Rn);
+      double cn = 0.0;
+      for (int k = 0; k < kVoSample; ++k) {
+        double r[4], J[4][6];
+        vo_residual<false>(pn, Rn, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+        cn += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+      }
+      if (cn < cost) {
+        for (int i = 0; i < 6; ++i) pp[i] = pn[i];
+        lam = fmax(lam * 0.1, 1e-12);
+      } else {
+        lam = fmin(lam * 10.0, 1e12);
+      }
+    }
+    // error over all points: sum_k |(f[2k], f[2k+1])| in order
+    rodrigues(pp, R);
+    double e = 0.0;
+    for (int k = 0; k < 2 * N; ++k) {
+      const double f0 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k);
+      const double f1 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k + 1);
+      e += sqrt(f0 * f0 + f1 * f1);
+    }
+    for (int i = 0; i < 6; ++i) hp[h][i] = pp[i];
+    herr[h] = e;
+  }
+  __syncthreads();
+  if (h == 0) {
+    // the sequential loop of :138-154 over the hypotheses in order
+    double mn = INFINITY;
+    int best = -1, tried = 0, early = 0;
+    if (N > 0)
+      for (int k = 0; k < max_iter; ++k) {
+        tried = k + 1;
+        if (herr[k] < mn) {
+          mn = herr[k];
+          best = k;
+          early = 0;
+        } else {
+          ++early;
+        }
+        if (early == early_stop) break;
+      }
+    for (int i = 0; i < 6; ++i) pose[6 * b + i] = best >= 0 ? hp[best][i] : 0.0;
+    best_out[b] = best;
+    ntried[b] = tried;
+    err_out[b] = mn;
+  }
+}
+
+// reprojection_residuals(dof, q1, q2, Q1, Q2) (:65-81): f [batch][4 cap], the
+// first 4 count[b] entries of item b in the reference's flat order
+__global__ __launch_bounds__(kBS) void k_vo_residuals(
+    const double* __restrict__ dof, const double* __restrict__ q1a, const double* __restrict__ q2a,
+    const double* __restrict__ Q1a, const double* __restrict__ Q2a,
+    const int32_t* __restrict__ count, int cap, const double* __restrict__ Pg,
+    double* __restrict__ out) {
+  const int b = blockIdx.y, i = blockIdx.x * kBS + threadIdx.x;
+  const int N = min(max(count[b], 0), cap);
+  if (i >= 4 * N) return;
+  double p[6], P[12], R[9];
+  for (int k = 0; k < 6; ++k) p[k] = dof[6 * b + k];
+  for (int k = 0; k < 12; ++k) P[k] = Pg[k];
+  rodrigues(p, R);
+  out[(size_t)b * 4 * cap + i] =
+      vo_elem(p, R, P, Q1a + (size_t)b * cap * 3, Q2a + (size_t)b * cap * 3,
+              q1a + (size_t)b * cap * 2, q2a + (size_t)b * cap * 2, N, i);
+}
 }  // namespace
 
 extern "C" int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int kt_cap,
@@ -550,5 +804,42 @@ extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32
                                                       refine_iters, d_rvec, d_tvec, d_ninliers,
                                                       d_mask);
   SLAM_LAUNCHED("k_pnp");
+  return SLAM_OK;
+}
+
+extern "C" int slam_vo_estimate_pose(const double* d_q1, const double* d_q2, const double* d_Q1,
+                                     const double* d_Q2, const int32_t* d_count, int cap,
+                                     int batch, const double* d_P, uint64_t seed, int item0,
+                                     int max_iter, int lm_iters, int early_stop, double* d_pose,
+                                     int32_t* d_best, int32_t* d_ntried, double* d_err,
+                                     void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_vo_estimate_pose: bad shape");
+  SLAM_REQUIRE(max_iter >= 1 && max_iter <= kVoWG, "slam_vo_estimate_pose: max_iter in [1, %d]",
+               kVoWG);
+  SLAM_REQUIRE(lm_iters >= 0 && early_stop >= 1, "slam_vo_estimate_pose: bad lm_iters/early_stop");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_q1 && d_q2 && d_Q1 && d_Q2 && d_count && d_P && d_pose && d_best && d_ntried &&
+                   d_err,
+               "slam_vo_estimate_pose: null pointer");
+  k_vo_pose<<<batch, kVoWG, 0, slam::as_stream(stream)>>>(d_q1, d_q2, d_Q1, d_Q2, d_count, cap,
+                                                         d_P, seed, item0, max_iter, lm_iters,
+                                                         early_stop, d_pose, d_best, d_ntried,
+                                                         d_err);
+  SLAM_LAUNCHED("k_vo_pose");
+  return SLAM_OK;
+}
+
+extern "C" int slam_vo_residuals(const double* d_dof, const double* d_q1, const double* d_q2,
+                                 const double* d_Q1, const double* d_Q2, const int32_t* d_count,
+                                 int cap, int batch, const double* d_P, double* d_res,
+                                 void* stream) {
+  SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_vo_residuals: bad shape");
+  if (batch == 0 || cap == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_dof && d_q1 && d_q2 && d_Q1 && d_Q2 && d_count && d_P && d_res,
+               "slam_vo_residuals: null pointer");
+  dim3 grid((4 * cap + kBS - 1) / kBS, batch);
+  k_vo_residuals<<<grid, kBS, 0, slam::as_stream(stream)>>>(d_dof, d_q1, d_q2, d_Q1, d_Q2,
+                                                           d_count, cap, d_P, d_res);
+  SLAM_LAUNCHED("k_vo_residuals");
   return SLAM_OK;
 }

@@ -58,6 +58,9 @@ SIGNATURES = {
     "slam_triangulate": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "slam_pnp_ransac": [c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int, c_double, c_int,
                         c_int, c_p, c_p, c_p, c_p, c_p],
+    "slam_vo_estimate_pose": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int,
+                              c_int, c_int, c_p, c_p, c_p, c_p, c_p],
+    "slam_vo_residuals": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_fundamental_lmeds": [c_p, c_p, c_p, c_int, c_int, c_uint64, c_int, c_int, c_p, c_p, c_p,
                                c_p],
     "slam_filter_pairs": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p],

@@ -106,3 +106,39 @@ def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, **kw):
               prm["hyp_iters"], prm["refine_iters"], ptr(rvec), ptr(tvec), ptr(ninl), ptr(mask),
               stream_ptr(stream))
     return rvec, tvec, ninl, mask
+
+
+VO_DEFAULTS = dict(max_iter=100, lm_iters=20, early_stop=5)
+
+
+def vo_estimate_pose(q1, q2, Q1, Q2, count, P, seed=0, item0=0, out=None, stream=None, **kw):
+    """visual_odometry.py:135-157 batched: q1, q2 [B,cap,2], Q1, Q2 [B,cap,3] f64,
+    P 3x4 -> (pose [B,6] (rotvec, t), best [B], ntried [B], err [B])."""
+    prm = dict(VO_DEFAULTS, **kw)
+    B, cap, _ = Q1.shape
+    dev = Q1.device
+    Pt = P if isinstance(P, torch.Tensor) else torch.as_tensor(np.asarray(P, np.float64), device=dev)
+    if out is None:
+        pose = torch.zeros((B, 6), dtype=torch.float64, device=dev)
+        best = torch.zeros((B,), dtype=torch.int32, device=dev)
+        ntried = torch.zeros((B,), dtype=torch.int32, device=dev)
+        err = torch.zeros((B,), dtype=torch.float64, device=dev)
+    else:
+        pose, best, ntried, err = out
+    _lib.call("slam_vo_estimate_pose", ptr(q1), ptr(q2), ptr(Q1), ptr(Q2), ptr(count), cap, B,
+              ptr(Pt.contiguous()), int(seed) & ((1 << 64) - 1), int(item0), prm["max_iter"],
+              prm["lm_iters"], prm["early_stop"], ptr(pose), ptr(best), ptr(ntried), ptr(err),
+              stream_ptr(stream))
+    return pose, best, ntried, err
+
+
+def vo_residuals(dof, q1, q2, Q1, Q2, count, P, out=None, stream=None):
+    """visual_odometry.py:65-81 batched: dof [B,6] -> f [B, 4 cap] (first 4 count[b] valid)."""
+    B, cap, _ = Q1.shape
+    dev = Q1.device
+    Pt = P if isinstance(P, torch.Tensor) else torch.as_tensor(np.asarray(P, np.float64), device=dev)
+    f = out if out is not None else torch.zeros((B, 4 * max(cap, 1)), dtype=torch.float64,
+                                                device=dev)
+    _lib.call("slam_vo_residuals", ptr(dof), ptr(q1), ptr(q2), ptr(Q1), ptr(Q2), ptr(count), cap,
+              B, ptr(Pt.contiguous()), ptr(f), stream_ptr(stream))
+    return f
