@@ -170,6 +170,28 @@ int slam_vo_residuals(const double* d_dof, const double* d_q1, const double* d_q
                       int batch, const double* d_P, double* d_res, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Map association: appendKeyPoints (keypoint.py:101-122).
+ *
+ * For each of the N new absolute points (d_abs [N][3] f64, camera-frame
+ * d_rel [N][3], image coordinates d_pts2d [N][2]) the exact nearest map point
+ * (the reference's KDTree(Qs).query(k=1); squared distance summed x, y, z in
+ * f64, ties -> lowest index) is taken as the landmark when its distance is
+ * below threshold * |rel| (:113-115); otherwise the point is appended to the
+ * map with the next index (:117-118).  Queries use the map as it was before
+ * the call (the tree is built first, :109).  d_map [map_cap][3] f64 and the map
+ * size d_M (device int32, updated in place: sequences of frames need no host
+ * synchronisation).  M_bound is any host-side upper bound of *d_M (grid
+ * sizing); M_bound + N <= map_cap is required.  d_n (nullable): device count
+ * of valid points (<= N).  d_rows [N][4] f64 = [frame_index, landmark index,
+ * u, v] (the reference's full_index_array rows).  Workspace from
+ * slam_map_workspace_bytes(N, M_bound or map_cap). */
+int slam_map_workspace_bytes(int max_queries, int map_cap, size_t* bytes);
+int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int M_bound,
+                       const double* d_abs, const double* d_rel, const double* d_pts2d,
+                       const int32_t* d_n, int N, double threshold, int frame_index,
+                       double* d_rows, void* d_ws, size_t ws_size, void* stream);
+
+/* ------------------------------------------------------------------------
  * Tiled ORB detector + rBRIEF descriptor.
  *
  * Replaces orb_detector_using_tiles (/root/reference/orb.py:4-25), i.e. the

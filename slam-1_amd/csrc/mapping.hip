@@ -1,0 +1,152 @@
+// Map association: appendKeyPoints (/root/reference/keypoint.py:101-122).
+//
+// The reference builds a scipy KDTree over the map Qs every frame, queries the
+// nearest map point of every new absolute point, and walks the points in
+// order: a point whose nearest distance is below threshold * |rel_point| is
+// an observation of that landmark; any other point is appended to the map
+// (index len(Qs) - 1 at the time).  The tree is built before the walk, so the
+// new points never match each other, and the walk is a prefix count:
+//   index(d) = nn(d)                       if dist(d) < threshold |rel(d)|
+//            = M + #(new points before d)  otherwise.
+// Two kernels: k_map_nn (exact brute-force nearest neighbour, queries one per
+// lane, the map streamed through LDS in chunks; one workgroup per (query block,
+// map chunk)) and k_map_assoc (per query: fold the chunk partials in chunk
+// order, the gate, a workgroup prefix scan, the appends and the output rows).
+// Distances are squared sums in x, y, z order in f64 (KDTree's p = 2 sum), ties
+// resolve to the lowest map index.  The map size M lives on the device, so a
+// sequence of frames runs without host synchronisation.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kNnWG = 256;      // queries per workgroup (one per lane)
+constexpr int kNnChunk = 1024;  // map points per workgroup, staged in LDS (24 KiB)
+constexpr int kAssocWG = 1024;
+
+__global__ __launch_bounds__(kNnWG) void k_map_nn(const double* __restrict__ map,
+                                                  const int32_t* __restrict__ d_M,
+                                                  const double* __restrict__ X,
+                                                  const int32_t* __restrict__ d_n, int N,
+                                                  double* __restrict__ part_d2,
+                                                  int32_t* __restrict__ part_idx) {
+  __shared__ double sm[3 * kNnChunk];
+  const int M = *d_M;
+  const int n = d_n ? min(max(*d_n, 0), N) : N;
+  const int base = blockIdx.y * kNnChunk;
+  if (base >= M || (int)(blockIdx.x * kNnWG) >= n) return;  // uniform
+  const int cnt = min(kNnChunk, M - base);
+  for (int i = threadIdx.x; i < 3 * cnt; i += kNnWG) sm[i] = map[(size_t)3 * base + i];
+  __syncthreads();
+  const int q = blockIdx.x * kNnWG + threadIdx.x;
+  if (q >= n) return;
+  const double x = X[3 * q], y = X[3 * q + 1], z = X[3 * q + 2];
+  double best = INFINITY;
+  int bi = -1;
+  for (int j = 0; j < cnt; ++j) {
+    const double dx = x - sm[3 * j], dy = y - sm[3 * j + 1], dz = z - sm[3 * j + 2];
+    const double d2 = (dx * dx + dy * dy) + dz * dz;
+    if (d2 < best) {
+      best = d2;
+      bi = base + j;
+    }
+  }
+  part_d2[(size_t)blockIdx.y * N + q] = best;
+  part_idx[(size_t)blockIdx.y * N + q] = bi;
+}
+
+__global__ __launch_bounds__(kAssocWG) void k_map_assoc(
+    double* __restrict__ map, int32_t* __restrict__ d_M, const double* __restrict__ X,
+    const double* __restrict__ rel, const double* __restrict__ pts2d,
+    const int32_t* __restrict__ d_n, int N, double threshold, int frame,
+    const double* __restrict__ part_d2, const int32_t* __restrict__ part_idx,
+    double* __restrict__ rows) {
+  __shared__ int wsum[kAssocWG / 64];
+  const int M = *d_M;
+  const int n = d_n ? min(max(*d_n, 0), N) : N;
+  const int nch = (M + kNnChunk - 1) / kNnChunk;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  int run = 0;  // new points appended so far (uniform)
+  for (int t0 = 0; t0 < n; t0 += kAssocWG) {
+    const int q = t0 + t;
+    bool isnew = false;
+    int idx = -1;
+    if (q < n) {
+      double best = INFINITY;
+      for (int c = 0; c < nch; ++c) {
+        const double d2 = part_d2[(size_t)c * N + q];
+        if (d2 < best) {
+          best = d2;
+          idx = part_idx[(size_t)c * N + q];
+        }
+      }
+      const double r0 = rel[3 * q], r1 = rel[3 * q + 1], r2 = rel[3 * q + 2];
+      const double gate = threshold * sqrt((r0 * r0 + r1 * r1) + r2 * r2);
+      isnew = !(sqrt(best) < gate);  // empty map: best = inf -> new
+    }
+    // workgroup exclusive scan of isnew (ballot per wave, then the wave totals)
+    const unsigned long long bal = __ballot(isnew);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wid] = __popcll(bal);
+    __syncthreads();
+    int wbase = 0, total = 0;
+    for (int w = 0; w < kAssocWG / 64; ++w) {
+      wbase += w < wid ? wsum[w] : 0;
+      total += wsum[w];
+    }
+    if (q < n) {
+      if (isnew) {
+        idx = M + run + wbase + pre;
+        map[3 * (size_t)idx] = X[3 * q];
+        map[3 * (size_t)idx + 1] = X[3 * q + 1];
+        map[3 * (size_t)idx + 2] = X[3 * q + 2];
+      }
+      rows[4 * (size_t)q] = (double)frame;
+      rows[4 * (size_t)q + 1] = (double)idx;
+      rows[4 * (size_t)q + 2] = pts2d[2 * q];
+      rows[4 * (size_t)q + 3] = pts2d[2 * q + 1];
+    }
+    run += total;
+    __syncthreads();  // wsum reuse
+  }
+  if (t == 0) *d_M = M + run;
+}
+
+size_t ws_bytes(int max_queries, int map_cap) {
+  const size_t nch = (size_t)(map_cap + kNnChunk - 1) / kNnChunk;
+  return nch * (size_t)max_queries * (sizeof(double) + sizeof(int32_t)) + 256;
+}
+
+}  // namespace
+
+extern "C" int slam_map_workspace_bytes(int max_queries, int map_cap, size_t* bytes) {
+  SLAM_REQUIRE(max_queries >= 0 && map_cap >= 0 && bytes, "slam_map_workspace_bytes: bad args");
+  *bytes = ws_bytes(max_queries, map_cap);
+  return SLAM_OK;
+}
+
+extern "C" int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int M_bound,
+                                  const double* d_abs, const double* d_rel, const double* d_pts2d,
+                                  const int32_t* d_n, int N, double threshold, int frame_index,
+                                  double* d_rows, void* d_ws, size_t ws_size, void* stream) {
+  SLAM_REQUIRE(N >= 0 && map_cap >= 0 && M_bound >= 0, "slam_map_associate: bad shape");
+  SLAM_REQUIRE(M_bound + N <= map_cap,
+               "slam_map_associate: map capacity %d < M_bound %d + N %d (grow the map first)",
+               map_cap, M_bound, N);
+  SLAM_REQUIRE(ws_size >= ws_bytes(N, M_bound), "slam_map_associate: workspace too small");
+  if (N == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_map && d_M && d_abs && d_rel && d_pts2d && d_rows && d_ws,
+               "slam_map_associate: null pointer");
+  const int nch = (M_bound + kNnChunk - 1) / kNnChunk;
+  double* part_d2 = static_cast<double*>(d_ws);
+  int32_t* part_idx = reinterpret_cast<int32_t*>(part_d2 + (size_t)nch * N);
+  hipStream_t s = slam::as_stream(stream);
+  if (nch > 0) {
+    dim3 grid((N + kNnWG - 1) / kNnWG, nch);
+    k_map_nn<<<grid, kNnWG, 0, s>>>(d_map, d_M, d_abs, d_n, N, part_d2, part_idx);
+    SLAM_LAUNCHED("k_map_nn");
+  }
+  k_map_assoc<<<1, kAssocWG, 0, s>>>(d_map, d_M, d_abs, d_rel, d_pts2d, d_n, N, threshold,
+                                     frame_index, part_d2, part_idx, d_rows);
+  SLAM_LAUNCHED("k_map_assoc");
+  return SLAM_OK;
+}

@@ -6,6 +6,9 @@ matched points as float64 and descriptors (:53-57), the F-LMedS inlier mask
 (:59-66).  The GUI block (:68-78) is not part of the hot path and is dropped.
 FLANN-LSH is replaced by exact brute force (Oracle); the F-LMedS
 fit is the seeded deterministic one of csrc/fundamental.hip.
+
+appendKeyPoints (keypoint.py:101-122, map association) is re-exported from
+slam355.mapping (GPU nearest-neighbour association, device-resident map).
 """
 from __future__ import annotations
 
@@ -14,6 +17,7 @@ import torch
 
 from . import geometry, matcher
 from .device import require_gpu, to_dev
+from .mapping import appendKeyPoints  # noqa: F401  (keypoint.py:101)
 
 
 def _pts(kps):

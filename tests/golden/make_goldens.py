@@ -22,6 +22,11 @@ What is pinned, and how:
     semantics of the reference around an exact matcher.  FLANN-LSH itself
     (approximate, randomised) and OpenCV's ORB / F-LMedS / PnP are NOT pinned
     here ("parity unpinned").
+  * Map association and BA-problem export (/root/reference/keypoint.py:101-122
+    appendKeyPoints over a growing map, Point3D.py:22-30
+    relative_to_abs3DPoints, XXXport_files.py:16-64 make_cam_params /
+    make_Qs_for_BA / export_data), run on a seeded synthetic sequence; the
+    BA_file.txt that export_data writes is recorded byte for byte.
 Only data (inputs + outputs) is written; no reference source is copied.
 """
 from __future__ import annotations
@@ -89,6 +94,12 @@ def import_reference():
     import keypoint  # noqa: E402
     import tracking  # noqa: E402
     return Point3D, keypoint, tracking
+
+
+def import_export_modules():
+    import XXXport_files  # noqa: E402  (numpy + scipy Rotation only)
+    import keyframe  # noqa: E402
+    return XXXport_files, keyframe
 
 
 def bal_namespace():
@@ -255,9 +266,64 @@ def make_ba_goldens(ns):
     return {k: np.shape(v) for k, v in out.items()}
 
 
+def make_mapping_goldens(Point3D, keypoint, xport, keyframe):
+    """A 6-frame sequence through appendKeyPoints (threshold 0.01, main.py:125)
+    with re-observed landmarks (inside and outside the 1 % gate) and new ones,
+    then export_data of the accumulated problem."""
+    import tempfile
+
+    rng = np.random.default_rng(31)
+    world = np.stack([rng.uniform(-15, 15, 400), rng.uniform(-3, 3, 400), rng.uniform(8, 60, 400)], 1)
+    out = {}
+    Qs = np.empty((0, 3))
+    opt = np.empty((0, 4))
+    frames = [keyframe.KeyFrame(np.eye(4))]
+    for i in range(6):
+        yaw = 0.01 * i
+        pose = np.eye(4)
+        pose[:3, :3] = np.array([[np.cos(yaw), 0, np.sin(yaw)], [0, 1, 0], [-np.sin(yaw), 0, np.cos(yaw)]])
+        pose[:3, 3] = [0.1 * i, 0.0, 1.0 * i]
+        n = 70 + 5 * i
+        pick = rng.choice(len(world), n, replace=False)
+        Xw = world[pick] + rng.normal(0, 1, (n, 1)) * rng.choice([0.002, 0.05, 2.0], (n, 1)) * 0.1
+        rel = (Xw - pose[:3, 3]) @ pose[:3, :3]  # camera coordinates of frame i
+        absP = Point3D.relative_to_abs3DPoints(rel, pose)
+        pts2d = rng.uniform([0, 0], [1226, 370], (n, 2))
+        out[f"f{i}_Qs_in"] = Qs.copy()
+        out[f"f{i}_rel"] = rel
+        out[f"f{i}_pose"] = pose
+        out[f"f{i}_abs"] = absP
+        out[f"f{i}_pts2d"] = pts2d
+        Qs, rows = keypoint.appendKeyPoints(Qs, absP, 0.01, pts2d, i, rel)
+        out[f"f{i}_Qs_out"] = Qs
+        out[f"f{i}_rows"] = rows
+        opt = np.vstack((opt, rows))
+        frames.append(keyframe.KeyFrame(pose))
+    P_left = np.array([[718.856, 0, 607.1928, 0], [0, 718.856, 185.2157, 0], [0, 0, 1, 0]])
+    out["P_left"] = P_left
+    out["frame_poses"] = np.stack([f.pose for f in frames])
+    out["cam_params"] = xport.make_cam_params(frames, P_left)
+    out["Qs_for_BA"] = xport.make_Qs_for_BA(Qs)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            os.mkdir("ourCache")
+            xport.export_data(opt, frames, Qs, P_left)
+            out["ba_file"] = np.frombuffer(open("ourCache/BA_file.txt", "rb").read(), np.uint8)
+            out["cam_frames_file"] = np.frombuffer(open("ourCache/cam_frames.txt", "rb").read(),
+                                                   np.uint8)
+        finally:
+            os.chdir(cwd)
+    np.savez_compressed(os.path.join(OUT, "mapping_golden.npz"), **out)
+    return {"frames": 6, "map": len(Qs), "obs": len(opt)}
+
+
 def main():
     Point3D, keypoint, tracking = import_reference()
     print("matcher:", make_matcher_goldens(Point3D, keypoint, tracking))
+    xport, keyframe = import_export_modules()
+    print("mapping:", make_mapping_goldens(Point3D, keypoint, xport, keyframe))
     print("ba:", make_ba_goldens(bal_namespace()))
 
 
