@@ -109,6 +109,24 @@ def ba_flops_per_iter(C, P, O, n_per_pt):
 
 
 # ---------------------------------------------------------------------------- tracking
+def pmc_traffic():
+    """Per-kernel HBM bytes per dispatch from the committed PMC summary
+    profiles/pmc_traffic.json (scripts/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE
+    in separate rocprofv3 --pmc passes of this bench), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    d["path"] = os.path.relpath(path, ROOT)
+    return d
+
+
+def pmc_bytes(pmc, kernels):
+    if pmc is None or not all(k in pmc["kernels"] for k in kernels):
+        return None
+    return float(sum(pmc["kernels"][k]["hbm_bytes"] for k in kernels))
+
+
 def run_tracking(args, world, rank):
     from slam355.ba import BAProblem
     from slam355.pipeline import Tracker, chain_poses
@@ -177,12 +195,18 @@ def run_tracking(args, world, rank):
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration: k_point_lin + k_gram_pairs + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration: k_linearize + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
+    pmc = pmc_traffic()
+    roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile", "k_orb_compact"))
+    roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_linearize", "k_assemble", "k_solve_blk",
+                                                  "k_back_trial<true>"))
     for r in roof.values():
         r["frac"] = r["achieved"] / r["peak"]
-        r["traffic"] = None
+        if r["traffic"] is not None:
+            r["traffic_unit"] = "bytes per launch (LM iteration for local_ba), HBM, from PMC"
+            r["traffic_source"] = pmc["path"]
     per_step = {k: v for k, v in stages.items()}
     dominant = max(("orb", orb_ms), ("local_ba", stages.get("local_ba", 0.0)), key=lambda kv: kv[1])[0]
     rec = {

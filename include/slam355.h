@@ -222,9 +222,12 @@ int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int stride, in
  * Bundle adjustment (BAL model) — replaces the reference's BAL block
  * /root/reference/BundleAdjustment.py:287-402 (rotate / project / objective /
  * bundle_adjustment_sparsity / least_squares TRF) with Levenberg-Marquardt on
- * the normal equations: analytic 2x12 Jacobian per observation, f64 MFMA Gram
- * [J_c | r | u]^T [J_c | r | u] per camera, point-block Schur complement,
- * Cholesky of the reduced camera system.
+ * the normal equations: analytic 2x12 Jacobian per observation; per point
+ * group (whole points, <= 128 observations) the point blocks are eliminated and
+ * the group's share of the reduced camera system (camera Grams U - sum Y W^T,
+ * off-diagonal sums Y W^T, Jc^T r, Jc^T u) is written as slot partials that a
+ * second launch sums per block in group order (deterministic); blocked LDL^T
+ * of the reduced camera system.
  *
  * Camera layout per row: [r0 r1 r2 t0 t1 t2 f k1 k2] (BundleAdjustment.py:324).
  * ---------------------------------------------------------------------- */
@@ -262,11 +265,11 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
  * (point, camera); index tables are fixed for the life of a problem. */
 typedef struct slam_ba_problem {
   int32_t n_cams, n_pts, n_obs;
-  int32_t n_cam_chunks;  /* camera-Gram work items                          */
+  int32_t n_grps;        /* point groups (>= 1): <= 128 obs / points each     */
   int32_t n_blocks;      /* upper camera-pair blocks of S: C(C+1)/2            */
-  int32_t n_pair_chunks; /* Schur work items                                 */
-  int32_t n_pairs;
-  int32_t n_grps;        /* point groups (>= 1): <= 128 obs each, whole points */
+  int32_t n_cslots;      /* (group, camera) slots                             */
+  int32_t n_bslots;      /* (group, camera-pair block) slots                  */
+  int32_t reserved;
   double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
   double* pts[2];               /* [P][3]                                      */
   double* camrec[2];            /* [C][32] per-camera projection records of cams[] */
@@ -274,20 +277,23 @@ typedef struct slam_ba_problem {
   const int32_t* obs_pt;        /* [O]                                         */
   const double* obs_q;          /* [O][2]                                      */
   const int32_t* pt_ptr;        /* [P+1] CSR point -> obs                      */
-  const int32_t* cam_obs;       /* [O] obs ids grouped by camera               */
-  const int32_t* cam_chunks;    /* [n_cam_chunks][3] (cam, begin, end) in cam_obs */
-  const int32_t* cam_chunk_ptr; /* [C+1] chunk range of each camera            */
-  const int32_t* pair_o;        /* [n_pairs][2] (o1 in c1, o2 in c2), by block */
-  const int32_t* pair_chunks;   /* [n_pair_chunks][3] (block, begin, end)      */
-  const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2), every upper block */
-  const int32_t* block_chunk_ptr; /* [n_blocks+1] (empty range: no common point) */
-  const int32_t* obs_campos;    /* [O] position of obs o in cam_obs            */
   const int32_t* grp_ptr;       /* [n_grps+1] point range of each point group  */
-  double* recc;                 /* [O][2][16] Jc(9) r u 0.. (camera order)     */
-  double* wy;                   /* [O][54] W = Jc^T Jp (9x3), Y = W V*^-1       */
-  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) -                 */
-  double* cam_part;             /* [n_cam_chunks][256] Gram partials           */
-  double* pair_part;            /* [n_pair_chunks][81] Schur partials          */
+  const int32_t* grp_cslot;     /* [n_grps+1] camera-slot range of each group  */
+  const int32_t* cslot_cam;     /* [n_cslots] camera of each slot              */
+  const int32_t* cslot_obs_ptr; /* [n_cslots+1] range in cslot_obs             */
+  const int32_t* cslot_obs;     /* [O] group-local obs indices, slot by slot   */
+  const int32_t* grp_bslot;     /* [n_grps+1] block-slot range of each group   */
+  const int32_t* bslot_blk;     /* [n_bslots] upper block index (c1 <= c2)     */
+  const int32_t* bslot_pair_ptr;/* [n_bslots+1] range in bslot_pairs           */
+  const int32_t* bslot_pairs;   /* group-local o1 | o2 << 16, o1 < o2 of one point */
+  const int32_t* blocks;        /* [n_blocks][2] (c1 <= c2), every upper block */
+  const int32_t* cam_cslot_ptr; /* [C+1] camera -> its rows of cpart            */
+  const int32_t* cslot_row;     /* [n_cslots] row of a camera slot in cpart (camera-major, group order) */
+  const int32_t* blk_bslot_ptr; /* [n_blocks+1] block -> its rows of bpart (empty: no common point) */
+  const int32_t* bslot_row;     /* [n_bslots] row of a block slot in bpart (block-major, group order) */
+  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) V*^-1(6) -       */
+  double* cpart;                /* [n_cslots][112] U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2 */
+  double* bpart;                /* [n_bslots][81] sum Y W^T                    */
   double* sys;                  /* S[(9C)^2] b[9C] g[9C] diagU[9C] cost[C]     */
   double* chol;                 /* [slam_ba_chol_len] (9C > 120 only)           */
   double* delta_c;              /* [9C]                                        */

@@ -5,13 +5,14 @@
 // and scipy least_squares TRF) with LM on the normal equations, all state on
 // the device so a fixed number of iterations runs with no host round trip.
 //
-// One LM iteration = 5 launches (local BA):
-//   k_point_lin     point group -> residuals + Jacobians, camera-ordered Gram
-//                                  record [Jc | r | u], V*_p, e_p = V*^-1 g_p,
-//                                  W_o = Jc^T Jp, Y_o = W_o V*^-1, u_o = Jp e_p
-//   k_gram_pairs    chunk  -> camera chunks: f64 MFMA Gram G = M^T M, M = [Jc | r | u]
-//                             (2 rows/obs); pair chunks: sum of Y_o1 W_o2^T (Schur)
-//   k_assemble      block  -> S = blockdiag(U) - sum(Y W^T), b = -Jc^T r - Jc^T u, ...
+// One LM iteration = 4 launches (local BA):
+//   k_linearize     point group -> residuals + Jacobians, V*_p, e_p = V*^-1 g_p,
+//                                  W_o = Jc^T Jp, u_o = Jp e_p, and the group's
+//                                  slot partials of the reduced camera system:
+//                                  per camera U - sum Y W^T, Jc^T r, Jc^T u;
+//                                  per camera pair sum Y_o1 W_o2^T
+//   k_assemble      block  -> S = sum of its slot partials in group order,
+//                             b = -Jc^T r - Jc^T u, g, diag U, cost
 //   (all-reduce of sys over ranks happens here for multi-GPU)
 //   k_solve_blk     1 WG   -> damp, blocked LDL^T (MFMA trailing updates), camera
 //                             step, pred_cam, trial cameras (k_solve for 9C > 120)
@@ -48,7 +49,6 @@ __device__ __forceinline__ void ticket_reset(uint32_t* p) {
 constexpr double kClamp = 5000.0;
 constexpr double kDiagMin = 1e-6, kDiagMax = 1e32;
 constexpr double kLamMin = 1e-16, kLamMax = 1e32;
-constexpr int kRecW = 16;  // doubles per residual row in rec
 constexpr int kBS = 256;   // block size of the element-wise kernels
 
 // ---------------------------------------------------------------- projection
@@ -251,51 +251,167 @@ __device__ __forceinline__ int cur_of(const double* state) {
 
 __device__ __forceinline__ double clampd(double d) { return fmin(fmax(d, kDiagMin), kDiagMax); }
 
-constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) pad
+constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) V*^-1(6) pad
+constexpr int kCPart = 112;  // per camera slot: U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2, pad
 // Point groups: a workgroup owns the contiguous observation range of a group
 // of whole points (observations are sorted by point), at most kGrp of them.
 constexpr int kGrp = 128;
+constexpr int kLinWG = 256;  // k_linearize: obs / point phases use kGrp lanes, slot phase all
+constexpr int kSlotLds = 128;  // slot ranges staged in LDS (larger groups read them from memory)
+constexpr int kPairLds = 1024; // observation pairs staged in LDS (ditto)
 
-// Linearisation + point elimination, one workgroup per point group:
+// LDS of k_linearize (65 KB: leaves room for a co-resident ORB workgroup)
+struct LinLds {
+  double jc[kGrp][18];  // Jc rows (2 x 9)
+  double w[kGrp][27];   // W = Jc^T Jp [i][c]; before phase 3: Jp (6), r (2)
+  double ru[kGrp][4];   // r0 r1 u0 u1
+  double pt[kGrp][9];   // per group point: e (3), V*^-1 (i00 i01 i02 i11 i12 i22)
+  int lpt[kGrp];        // group-local point of each observation
+  int cobs[kGrp];       // the group's camera-slot observation lists
+  int cptr[kSlotLds];   // camera-slot ranges in cobs (when the group has < kSlotLds slots)
+  int bptr[kSlotLds];   // block-slot ranges in pairs
+  int pairs[kPairLds];  // the group's observation pairs (when <= kPairLds)
+};
+
+// Y_o row i (= W_o row i times V*^-1, V*^-1 symmetric) of a group observation
+__device__ __forceinline__ void y_row(const double* W, const double* Vi, int i, double y[3]) {
+  const double a = W[3 * i], b = W[3 * i + 1], c = W[3 * i + 2];
+  y[0] = a * Vi[0] + b * Vi[1] + c * Vi[2];
+  y[1] = a * Vi[1] + b * Vi[3] + c * Vi[4];
+  y[2] = a * Vi[2] + b * Vi[4] + c * Vi[5];
+}
+
+// Linearisation, point elimination and the group's share of the reduced camera
+// system, one workgroup per point group:
 //   per observation: residual and 2x12 Jacobian (BundleAdjustment.py:317-350
-//     + analytic derivative), the camera-ordered Gram record [Jc | r | u];
+//     + analytic derivative) -> LDS;
 //   per point: V = sum Jp^T Jp, g = -sum Jp^T r, V* = V + lam diag(V),
 //     V*^-1 (cofactors), e = V*^-1 g;
-//   per observation: W = Jc^T Jp, Y = W V*^-1, u = Jp e.
-// Jp and r go through LDS between the phases; Jc stays in registers.
-__global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
-  __shared__ double sJ[kGrp][9];   // Jp row 0 (3), Jp row 1 (3), r (2), pad
-  __shared__ double sP[kGrp][10];  // e (3), V*^-1 (6), pad
+//   per observation: W = Jc^T Jp, u = Jp e -> LDS;
+//   per slot row (a lane owns row i of one slot; slots from the planner):
+//     camera slot (c):      U - sum_o Y_o W_o^T, Jc^T r, Jc^T u, diag U, |r|^2
+//                           over the group's observations of camera c;
+//     block slot (c1 <= c2): sum Y_o1 W_o2^T over the group's observation pairs
+//                           o1 < o2 of one point with cameras c1, c2.
+// Everything stays in LDS between the phases; only the slot partials (and the
+// per-point data the back substitution needs) are written.
+// Slot partials of one group (see k_linearize): a lane owns row i of one slot
+// (405 lanes' worth at C3: two rounds of the workgroup).
+// cptr / bptr: slot ranges (minus coff / boff) into the group's camera-slot
+// observations (L.cobs) and observation pairs.
+__device__ __forceinline__ void lin_slots(const slam_ba_problem& p, LinLds& L, int cs0, int ncs,
+                                          int bs0, int nbs, const int* cptr, int coff,
+                                          const int* bptr, int boff, const int* pairs) {
+  const int t = threadIdx.x;
+  const int* cobs = L.cobs;
+  for (int item = t; item < 9 * (ncs + nbs); item += kLinWG) {
+    const int sl = item / 9, i = item - 9 * sl;
+    double acc[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[j] = 0.0;
+    if (sl < ncs) {
+      const int s = cs0 + sl;
+      double vr = 0.0, vu = 0.0, vd = 0.0, cost = 0.0;
+      // the next observation's index and point are fetched one iteration
+      // ahead, so each iteration waits on one LDS round trip, not three
+      const int qb = cptr[sl] - coff, qe = cptr[sl + 1] - coff;
+      int k = cobs[qb < qe ? qb : 0], lk = L.lpt[k];
+      for (int q = qb; q < qe; ++q) {
+        const int kn = cobs[q + 1 < qe ? q + 1 : q], lkn = L.lpt[kn];
+        const double* jc = L.jc[k];
+        const double* W = L.w[k];
+        double y[3];
+        y_row(W, L.pt[lk] + 3, i, y);
+        const double a0 = jc[i], a1 = jc[9 + i];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          const double u = __builtin_fma(a0, jc[j], a1 * jc[9 + j]);
+          const double v = __builtin_fma(y[0], W[3 * j], __builtin_fma(y[1], W[3 * j + 1], y[2] * W[3 * j + 2]));
+          acc[j] += u - v;
+        }
+        const double r0 = L.ru[k][0], r1 = L.ru[k][1];
+        vr = __builtin_fma(a0, r0, __builtin_fma(a1, r1, vr));
+        vu = __builtin_fma(a0, L.ru[k][2], __builtin_fma(a1, L.ru[k][3], vu));
+        vd = __builtin_fma(a0, a0, __builtin_fma(a1, a1, vd));
+        cost = __builtin_fma(r0, r0, __builtin_fma(r1, r1, cost));
+        k = kn;
+        lk = lkn;
+      }
+      double* out = p.cpart + (size_t)p.cslot_row[s] * kCPart;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) out[9 * i + j] = acc[j];
+      out[81 + i] = vr;
+      out[90 + i] = vu;
+      out[99 + i] = vd;
+      if (i == 0) out[108] = cost;
+    } else {
+      const int sb = sl - ncs, s = bs0 + sb;
+      const int qb = bptr[sb] - boff, qe = bptr[sb + 1] - boff;
+      int pr = pairs[qb < qe ? qb : 0], lk = L.lpt[pr & 0xffff];
+      for (int q = qb; q < qe; ++q) {
+        const int prn = pairs[q + 1 < qe ? q + 1 : q], lkn = L.lpt[prn & 0xffff];
+        const int k1 = pr & 0xffff, k2 = pr >> 16;
+        double y[3];
+        y_row(L.w[k1], L.pt[lk] + 3, i, y);
+        const double* W2 = L.w[k2];
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+          acc[j] = __builtin_fma(y[0], W2[3 * j], __builtin_fma(y[1], W2[3 * j + 1], __builtin_fma(y[2], W2[3 * j + 2], acc[j])));
+        pr = prn;
+        lk = lkn;
+      }
+      double* out = p.bpart + (size_t)p.bslot_row[s] * 81;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) out[9 * i + j] = acc[j];
+    }
+  }
+}
+
+#ifdef SLAM_LIN_PROFILE
+#define LIN_T(i) const uint64_t lin_t##i = __builtin_amdgcn_s_memtime()
+#else
+#define LIN_T(i) (void)0
+#endif
+__global__ __launch_bounds__(kLinWG) void k_linearize(slam_ba_problem p) {
+  __shared__ LinLds L;
+  LIN_T(0);
   const int g = blockIdx.x;
   const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
   const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
   const int t = threadIdx.x;
   const int o = o0 + t;
-  const bool has = o < o1;
+  const bool has = t < kGrp && o < o1;
   const int cur = cur_of(p.state);
+  // slot lists of this group -> LDS (their loads overlap the projections)
+  const int cs0 = p.grp_cslot[g], ncs = p.grp_cslot[g + 1] - cs0;
+  const int bs0 = p.grp_bslot[g], nbs = p.grp_bslot[g + 1] - bs0;
+  const int cb0 = p.cslot_obs_ptr[cs0], pb0 = p.bslot_pair_ptr[bs0];
+  const int npairs = p.bslot_pair_ptr[bs0 + nbs] - pb0;
+  const bool fit_c = ncs < kSlotLds, fit_b = nbs < kSlotLds, fit_p = npairs <= kPairLds;
+  if (fit_c && t <= ncs) L.cptr[t] = p.cslot_obs_ptr[cs0 + t] - cb0;
+  if (fit_b && t <= nbs) L.bptr[t] = p.bslot_pair_ptr[bs0 + t] - pb0;
+  if (t < kGrp && t < o1 - o0) L.cobs[t] = p.cslot_obs[cb0 + t];
+  if (fit_p)
+    for (int q = t; q < npairs; q += kLinWG) L.pairs[q] = p.bslot_pairs[pb0 + q];
   double r[2], J[2][12];
-  double* recc = p.recc + (size_t)(has ? p.obs_campos[o] : 0) * 2 * kRecW;
   if (has) {
-    reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * p.obs_pt[o],
+    const int pt = p.obs_pt[o];
+    reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
                         p.obs_q + 2 * o, r, J);
     clamp_rows<true>(r, J);
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
-      double2* d = reinterpret_cast<double2*>(recc + a * kRecW);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) d[k] = make_double2(J[a][2 * k], J[a][2 * k + 1]);
-      d[4] = make_double2(J[a][8], r[a]);
-      // col 10 (u) is written after the point phase; cols 11..15 stay zero
-      d[5] = make_double2(0.0, 0.0);
-      d[6] = make_double2(0.0, 0.0);
-      d[7] = make_double2(0.0, 0.0);
-      sJ[t][3 * a] = J[a][9];
-      sJ[t][3 * a + 1] = J[a][10];
-      sJ[t][3 * a + 2] = J[a][11];
-      sJ[t][6 + a] = r[a];
+      for (int i = 0; i < 9; ++i) L.jc[t][9 * a + i] = J[a][i];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) L.w[t][3 * a + c] = J[a][9 + c];
+      L.w[t][6 + a] = r[a];
+      L.ru[t][a] = r[a];
     }
+    L.lpt[t] = pt - p0;
   }
   __syncthreads();
+  LIN_T(1);
   const double lam = p.state[SLAM_BA_ST_LAMBDA];
   if (t < p1 - p0) {
     const int pt = p0 + t;
@@ -303,8 +419,8 @@ __global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
     for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
-        const double j0 = sJ[k][3 * a], j1 = sJ[k][3 * a + 1], j2 = sJ[k][3 * a + 2];
-        const double rr = sJ[k][6 + a];
+        const double j0 = L.w[k][3 * a], j1 = L.w[k][3 * a + 1], j2 = L.w[k][3 * a + 2];
+        const double rr = L.w[k][6 + a];
         V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
         V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
         g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
@@ -321,149 +437,98 @@ __global__ __launch_bounds__(kGrp) void k_point_lin(slam_ba_problem p) {
     const double c22 = a00 * a11 - a01 * a01;
     const double det = a00 * c00 + a01 * c01 + a02 * c02;
     const double id = det != 0.0 ? 1.0 / det : 0.0;
-    const double i00 = c00 * id, i01 = c01 * id, i02 = c02 * id;
-    const double i11 = c11 * id, i12 = c12 * id, i22 = c22 * id;
-    const double e0 = i00 * g0 + i01 * g1 + i02 * g2;
-    const double e1 = i01 * g0 + i11 * g1 + i12 * g2;
-    const double e2 = i02 * g0 + i12 * g1 + i22 * g2;
+    const double iv[6] = {c00 * id, c01 * id, c02 * id, c11 * id, c12 * id, c22 * id};
+    const double e0 = iv[0] * g0 + iv[1] * g1 + iv[2] * g2;
+    const double e1 = iv[1] * g0 + iv[3] * g1 + iv[4] * g2;
+    const double e2 = iv[2] * g0 + iv[4] * g1 + iv[5] * g2;
     double* pd = p.ptdata + (size_t)pt * kPtData;
     pd[0] = e0; pd[1] = e1; pd[2] = e2;
     pd[3] = g0; pd[4] = g1; pd[5] = g2;
     pd[6] = d0; pd[7] = d1; pd[8] = d2;
-    sP[t][0] = e0; sP[t][1] = e1; sP[t][2] = e2;
-    sP[t][3] = i00; sP[t][4] = i01; sP[t][5] = i02;
-    sP[t][6] = i11; sP[t][7] = i12; sP[t][8] = i22;
-  }
-  __syncthreads();
-  if (!has) return;
-  const double* sp = sP[p.obs_pt[o] - p0];
-  const double Vi[3][3] = {{sp[3], sp[4], sp[5]}, {sp[4], sp[6], sp[7]}, {sp[5], sp[7], sp[8]}};
-  double* wy = p.wy + (size_t)o * 54;
+    L.pt[t][0] = e0; L.pt[t][1] = e1; L.pt[t][2] = e2;
 #pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    double W[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) W[c] = J[0][i] * J[0][9 + c] + J[1][i] * J[1][9 + c];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) wy[i * 3 + c] = W[c];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) wy[27 + i * 3 + c] = W[0] * Vi[0][c] + W[1] * Vi[1][c] + W[2] * Vi[2][c];
-  }
-  recc[10] = J[0][9] * sp[0] + J[0][10] * sp[1] + J[0][11] * sp[2];
-  recc[kRecW + 10] = J[1][9] * sp[0] + J[1][10] * sp[1] + J[1][11] * sp[2];
-}
-
-// f64 MFMA Gram of M = [Jc | r | u | 0...] over one chunk of a camera's
-// observations (camera-ordered record: contiguous rows, no gather): G = M^T M.
-// v_mfma_f64_16x16x4_f64: lane l holds A[i = l&15][k = l>>4] and
-// B[k = l>>4][j = l&15]; with A = M^T, B = M both are the same element
-// M[k][l&15], so each lane loads one double per MFMA and one MFMA consumes 4
-// residual rows = 2 observations.  8 steps are loaded before they are consumed.
-constexpr int kGramWG = 256;
-constexpr int kGramUnroll = 8;
-__device__ __forceinline__ void cam_gram(const slam_ba_problem& p, int ch, double (*red)[256]) {
-  const int beg = p.cam_chunks[3 * ch + 1], end = p.cam_chunks[3 * ch + 2];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int krow = lane >> 4, col = lane & 15;
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-  // rows of the chunk: 2 per observation; each MFMA step takes 4 rows
-  const int row0 = 2 * beg, row1 = 2 * end;
-  const double* M = p.recc;
-  for (int base = row0 + 4 * wid; base < row1; base += 16 * kGramUnroll) {
-    double v[kGramUnroll];
-#pragma unroll
-    for (int u = 0; u < kGramUnroll; ++u) {
-      const int r = base + 16 * u + krow;
-      v[u] = r < row1 ? M[(size_t)r * kRecW + col] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kGramUnroll; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v[u], v[u], acc, 0, 0, 0);
-  }
-  // D layout (f64): col = lane&15, row = (lane>>4) + 4*reg
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[wid][(krow + 4 * r) * 16 + col] = acc[r];
-  __syncthreads();
-  const int t = threadIdx.x;
-  p.cam_part[(size_t)ch * 256 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
-}
-
-// Schur terms: sum over the chunk's obs pairs of Y_o1 (9x3) W_o2^T (3x9).
-constexpr int kPairChunk = 64;
-constexpr int kPairWG = 256;
-struct PairLds {
-  double sy[kPairChunk][27];
-  double sw[kPairChunk][27];
-  double red[3][81];
-  int so[kPairChunk][2];
-};
-
-__device__ __forceinline__ void pair_partials(const slam_ba_problem& p, int ch, PairLds& L) {
-  auto& sy = L.sy;
-  auto& sw = L.sw;
-  auto& red = L.red;
-  auto& so = L.so;
-  const int beg = p.pair_chunks[3 * ch + 1], end = p.pair_chunks[3 * ch + 2];
-  const int n = end - beg;
-  // indices first (one round trip), then every lane's rows with all loads in
-  // flight before the LDS stores (one more round trip)
-  if (threadIdx.x < 2 * n) (&so[0][0])[threadIdx.x] = p.pair_o[2 * beg + threadIdx.x];
-  __syncthreads();
-  constexpr int kPer = (kPairChunk * 27 + kPairWG - 1) / kPairWG;  // 7
-  double vy[kPer], vw[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int i = threadIdx.x + u * kPairWG;
-    const int k = i / 27, e = i - k * 27;
-    vy[u] = vw[u] = 0.0;
-    if (k < n) {
-      vy[u] = p.wy[(size_t)so[k][0] * 54 + 27 + e];
-      vw[u] = p.wy[(size_t)so[k][1] * 54 + e];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int i = threadIdx.x + u * kPairWG;
-    const int k = i / 27, e = i - k * 27;
-    if (k < n) {
-      sy[k][e] = vy[u];
-      sw[k][e] = vw[u];
+    for (int k = 0; k < 6; ++k) {
+      pd[9 + k] = iv[k];
+      L.pt[t][3 + k] = iv[k];
     }
   }
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t < 243) {
-    const int g = t / 81, ent = t - g * 81, i = ent / 9, j = ent - i * 9;
-    double acc = 0.0;
-    for (int k = g; k < n; k += 3)
-      acc += sy[k][3 * i] * sw[k][3 * j] + sy[k][3 * i + 1] * sw[k][3 * j + 1] +
-             sy[k][3 * i + 2] * sw[k][3 * j + 2];
-    red[g][ent] = acc;
+  if (has) {
+    const double* e = L.pt[L.lpt[t]];
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) L.w[t][3 * i + c] = J[0][i] * J[0][9 + c] + J[1][i] * J[1][9 + c];
+    L.ru[t][2] = J[0][9] * e[0] + J[0][10] * e[1] + J[0][11] * e[2];
+    L.ru[t][3] = J[1][9] * e[0] + J[1][10] * e[1] + J[1][11] * e[2];
   }
   __syncthreads();
-  if (t < 81) p.pair_part[(size_t)ch * 81 + t] = (red[0][t] + red[1][t]) + red[2][t];
-}
-
-// Camera Gram chunks and Schur pair chunks are independent: one launch, the
-// workgroup index picks the role (gram chunks first), so the two overlap.
-static_assert(kGramWG == kPairWG, "k_gram_pairs runs both roles with one block size");
-__global__ __launch_bounds__(kGramWG) void k_gram_pairs(slam_ba_problem p) {
-  __shared__ union {
-    double gram[4][256];
-    PairLds pair;
-  } lds;
-  const int b = blockIdx.x;
-  if (b < p.n_cam_chunks)
-    cam_gram(p, b, lds.gram);
+  LIN_T(2);
+  // the group's slot lists (staged in LDS at kernel start: see below)
+  // slot phase: LDS-staged lists when they fit (always at C3), else from memory
+  // (two inlined copies, so every list access is a plain ds_read or global load)
+  if (fit_c && fit_b && fit_p)
+    lin_slots(p, L, cs0, ncs, bs0, nbs, L.cptr, 0, L.bptr, 0, L.pairs);
   else
-    pair_partials(p, b - p.n_cam_chunks, lds.pair);
+    lin_slots(p, L, cs0, ncs, bs0, nbs, p.cslot_obs_ptr + cs0, cb0, p.bslot_pair_ptr + bs0, pb0,
+              p.bslot_pairs + pb0);
+#ifdef SLAM_LIN_PROFILE
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  LIN_T(3);
+  if (g == 7 && t == 0) {
+    p.state[12] = (double)(lin_t1 - lin_t0);
+    p.state[13] = (double)(lin_t2 - lin_t1);
+    p.state[14] = (double)(lin_t3 - lin_t2);
+    p.state[15] = (double)(ncs * 100 + nbs);
+  }
+#endif
 }
 
-// One workgroup per upper camera-pair block (c1 <= c2), ALL C(C+1)/2 of them:
-// S block = [U_c] - sum(Y W^T); blocks without common points are written as
-// zeros, so sys needs no separate clearing.  Partial sums are read 4 at a time.
-__global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
-  __shared__ double G[256];
-  __shared__ double T3[3][81];
+// Column sums of the n-wide rows [rb, re) of part (row stride `stride`): the
+// workgroup's lanes are (part k, column e) pairs; part k takes rows rb + k,
+// rb + k + nparts, ... with 8 loads in flight, then the parts are added in
+// order k = 0, 1, ... (deterministic).  Result in out[0..n).
+constexpr int kAsmWG = 1024;
+__device__ void rows_sum(const double* __restrict__ part, int stride, int rb, int re, int n,
+                         double (*red)[kCPart], double* out) {
+  const int t = threadIdx.x;
+  const int nparts = kAsmWG / n, k = t / n, e = t - k * n;
+  if (k < nparts) {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int r = rb + k;
+    for (; r + 7 * nparts < re; r += 8 * nparts) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(size_t)(r + u * nparts) * stride + e];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += v[u];
+    }
+    for (int u = 0; r < re; r += nparts, ++u) a[u] += part[(size_t)r * stride + e];
+    red[k][e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  }
+  __syncthreads();
+  if (t < n) {
+    double v = 0.0;
+    for (int q = 0; q < nparts; ++q) v += red[q][t];
+    out[t] = v;
+  }
+  __syncthreads();
+}
+
+// One workgroup per upper camera-pair block (c1 <= c2), ALL C(C+1)/2 of them.
+// The slot partials of a camera / block are contiguous rows (the planner's
+// camera- / block-major row order), summed in group order (deterministic):
+//   diagonal block c:  S = sum (U - Y W^T) over the camera rows of c, minus
+//                      B + B^T for the block rows of (c, c) (a point observed
+//                      twice by c); b = -Jc^T r - Jc^T u, g = -Jc^T r, diag U, cost;
+//   block c1 < c2:     S = -sum Y W^T (and its transpose) over the block rows.
+// Blocks without observations / common points are written as zeros, so sys
+// needs no separate clearing.
+__global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
+  __shared__ double red[kAsmWG / 81][kCPart];
+  __shared__ double sh[kCPart];
+  __shared__ double sb[81];
   const int blk = blockIdx.x;
   const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
   const int C9 = 9 * p.n_cams;
@@ -473,51 +538,30 @@ __global__ __launch_bounds__(kBS) void k_assemble(slam_ba_problem p) {
   double* diagU = gvec + C9;
   double* costc = diagU + C9;
   const int t = threadIdx.x;
-  if (c1 == c2) {
-    const int cb = p.cam_chunk_ptr[c1], ce = p.cam_chunk_ptr[c1 + 1];
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    int ch = cb;
-    for (; ch + 3 < ce; ch += 4) {
-      a0 += p.cam_part[(size_t)ch * 256 + t];
-      a1 += p.cam_part[(size_t)(ch + 1) * 256 + t];
-      a2 += p.cam_part[(size_t)(ch + 2) * 256 + t];
-      a3 += p.cam_part[(size_t)(ch + 3) * 256 + t];
-    }
-    for (; ch < ce; ++ch) a0 += p.cam_part[(size_t)ch * 256 + t];
-    G[t] = (a0 + a1) + (a2 + a3);
-  }
-  {
-    const int g = t / 81, ent = t - g * 81;
-    if (g < 3) {
-      const int pb = p.block_chunk_ptr[blk], pe = p.block_chunk_ptr[blk + 1];
-      double a0 = 0.0, a1 = 0.0;
-      int ch = pb + g;
-      for (; ch + 3 < pe; ch += 6) {
-        a0 += p.pair_part[(size_t)ch * 81 + ent];
-        a1 += p.pair_part[(size_t)(ch + 3) * 81 + ent];
-      }
-      for (; ch < pe; ch += 3) a0 += p.pair_part[(size_t)ch * 81 + ent];
-      T3[g][ent] = a0 + a1;
-    }
+  const bool diag = c1 == c2;
+  const int bb = p.blk_bslot_ptr[blk], be = p.blk_bslot_ptr[blk + 1];
+  if (diag) rows_sum(p.cpart, kCPart, p.cam_cslot_ptr[c1], p.cam_cslot_ptr[c1 + 1], 109, red, sh);
+  if (!diag || be > bb) {
+    rows_sum(p.bpart, 81, bb, be, 81, red, sb);
+  } else if (t < 81) {
+    sb[t] = 0.0;
   }
   __syncthreads();
   if (t < 81) {
-    const double acc = (T3[0][t] + T3[1][t]) + T3[2][t];
-    const int i = t / 9, j = t - i * 9;
-    if (c1 == c2) {
-      S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = G[i * 16 + j] - acc;
+    const int i = t / 9, j = t - 9 * (t / 9);
+    if (diag) {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = sh[t] - (sb[t] + sb[9 * j + i]);
     } else {
-      S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = -acc;
-      S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = -acc;
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = -sb[t];
+      S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = -sb[t];
     }
   }
-  if (c1 == c2 && t < 9) {
-    // G row i: [.. U .. | col 9 = Jc^T r | col 10 = Jc^T u]
-    gvec[9 * c1 + t] = -G[t * 16 + 9];
-    bvec[9 * c1 + t] = -G[t * 16 + 9] - G[t * 16 + 10];
-    diagU[9 * c1 + t] = G[t * 16 + t];
+  if (diag && t < 9) {
+    gvec[9 * c1 + t] = -sh[81 + t];
+    bvec[9 * c1 + t] = -sh[81 + t] - sh[90 + t];
+    diagU[9 * c1 + t] = sh[99 + t];
   }
-  if (c1 == c2 && t == 0) costc[c1] = G[9 * 16 + 9];
+  if (diag && t == 0) costc[c1] = sh[108];
 }
 
 // ---------------------------------------------------------------- solve
@@ -1001,7 +1045,7 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
 __device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
 
 // Back substitution + trial cost, one workgroup per point group:
-//   per observation: dy_o = Y_o^T dc_cam(o)                         (-> LDS)
+//   per observation: dy_o = Y_o^T dc_cam(o) = V*^-1 W_o^T dc         (-> LDS)
 //   per point: dp = e - sum_o dy_o, trial point x + dp, predicted-reduction term
 //   per observation: trial residual at (cams[next], trial point)   (-> |r|^2)
 // Workgroup partial sums go to part[g] (cost) and part[G + g] (pred) as sc1
@@ -1023,19 +1067,26 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* 
   const int cur = cur_of(p.state);
   const bool fail = p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0;
   if (has) {
-    const double* Y = p.wy + (size_t)o * 54 + 27;
+    // dy_o = Y_o^T dc = V*^-1 (W_o^T dc), W_o = Jc^T Jp re-derived from the
+    // Jacobian at the live parameters (the one k_linearize used)
+    double r[2], J[2][12];
+    const int pt = p.obs_pt[o];
+    reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
+                        p.obs_q + 2 * o, r, J);
+    clamp_rows<true>(r, J);
     const double* dc = p.delta_c + 9 * p.obs_cam[o];
-    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const double c = dc[i];
-      d0 += Y[3 * i] * c;
-      d1 += Y[3 * i + 1] * c;
-      d2 += Y[3 * i + 2] * c;
+      w0 += (J[0][i] * J[0][9] + J[1][i] * J[1][9]) * c;
+      w1 += (J[0][i] * J[0][10] + J[1][i] * J[1][10]) * c;
+      w2 += (J[0][i] * J[0][11] + J[1][i] * J[1][11]) * c;
     }
-    sdy[t][0] = d0;
-    sdy[t][1] = d1;
-    sdy[t][2] = d2;
+    const double* vi = p.ptdata + (size_t)pt * kPtData + 9;
+    sdy[t][0] = vi[0] * w0 + vi[1] * w1 + vi[2] * w2;
+    sdy[t][1] = vi[1] * w0 + vi[3] * w1 + vi[4] * w2;
+    sdy[t][2] = vi[2] * w0 + vi[4] * w1 + vi[5] * w2;
   }
   __syncthreads();
   double pred = 0.0;
@@ -1141,9 +1192,11 @@ inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
 int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
   SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
-  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->camrec[0] && p->camrec[1] && p->recc && p->wy && p->ptdata && p->obs_campos &&
-                   p->grp_ptr && p->ticket && p->sys && p->state && p->small && p->red_part &&
-                   p->delta_c,
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->camrec[0] && p->camrec[1] && p->ptdata &&
+                   p->cpart && p->bpart && p->grp_ptr && p->grp_cslot && p->grp_bslot &&
+                   p->cslot_obs_ptr && p->bslot_pair_ptr && p->cam_cslot_ptr && p->cslot_row && p->bslot_row &&
+                   p->blk_bslot_ptr && p->blocks && p->ticket && p->sys && p->state &&
+                   p->small && p->red_part && p->delta_c,
                "slam_ba: null buffer");
   SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
   SLAM_REQUIRE(p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
@@ -1208,13 +1261,9 @@ extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
   // every entry of sys is written by k_assemble (all upper blocks), so no clearing
-  k_point_lin<<<p.n_grps, kGrp, 0, s>>>(p);
-  SLAM_LAUNCHED("k_point_lin");
-  if (p.n_cam_chunks + p.n_pair_chunks > 0) {
-    k_gram_pairs<<<p.n_cam_chunks + p.n_pair_chunks, kGramWG, 0, s>>>(p);
-    SLAM_LAUNCHED("k_gram_pairs");
-  }
-  k_assemble<<<p.n_blocks, kBS, 0, s>>>(p);
+  k_linearize<<<p.n_grps, kLinWG, 0, s>>>(p);
+  SLAM_LAUNCHED("k_linearize");
+  k_assemble<<<p.n_blocks, kAsmWG, 0, s>>>(p);
   SLAM_LAUNCHED("k_assemble");
   return SLAM_OK;
 }

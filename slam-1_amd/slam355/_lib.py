@@ -25,14 +25,14 @@ c_i32 = ctypes.c_int32
 class BAProblemStruct(ctypes.Structure):
     """Mirror of `slam_ba_problem` (include/slam355.h)."""
     _fields_ = [
-        ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_cam_chunks", c_i32),
-        ("n_blocks", c_i32), ("n_pair_chunks", c_i32), ("n_pairs", c_i32), ("n_grps", c_i32),
+        ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_grps", c_i32),
+        ("n_blocks", c_i32), ("n_cslots", c_i32), ("n_bslots", c_i32), ("reserved", c_i32),
         ("cams", c_p * 2), ("pts", c_p * 2), ("camrec", c_p * 2),
-        ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p),
-        ("cam_obs", c_p), ("cam_chunks", c_p), ("cam_chunk_ptr", c_p),
-        ("pair_o", c_p), ("pair_chunks", c_p), ("blocks", c_p), ("block_chunk_ptr", c_p),
-        ("obs_campos", c_p), ("grp_ptr", c_p), ("recc", c_p), ("wy", c_p), ("ptdata", c_p),
-        ("cam_part", c_p), ("pair_part", c_p),
+        ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p), ("grp_ptr", c_p),
+        ("grp_cslot", c_p), ("cslot_cam", c_p), ("cslot_obs_ptr", c_p), ("cslot_obs", c_p),
+        ("grp_bslot", c_p), ("bslot_blk", c_p), ("bslot_pair_ptr", c_p), ("bslot_pairs", c_p),
+        ("blocks", c_p), ("cam_cslot_ptr", c_p), ("cslot_row", c_p), ("blk_bslot_ptr", c_p),
+        ("bslot_row", c_p), ("ptdata", c_p), ("cpart", c_p), ("bpart", c_p),
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
         ("state", c_p), ("ticket", c_p),
     ]

@@ -66,82 +66,104 @@ def point_groups(pt_ptr, cap=GROUP_OBS):
     return np.asarray(starts, np.int32)
 
 
-def plan(n_cams, n_pts, cam_idx, pt_idx, cam_chunk=512, pair_chunk=64):
-    """Index tables for the LM kernels (host numpy, once per problem structure)."""
+def block_index(c1, c2, n_cams):
+    """Index of the upper block (c1 <= c2) in np.triu_indices(n_cams) order."""
+    c1 = np.asarray(c1, np.int64)
+    return c1 * n_cams - c1 * (c1 - 1) // 2 + (np.asarray(c2, np.int64) - c1)
+
+
+def plan(n_cams, n_pts, cam_idx, pt_idx):
+    """Index tables for the LM kernels (host numpy, once per problem structure).
+
+    Observations are sorted by (point, camera) and cut into point groups
+    (whole points, <= GROUP_OBS observations).  Each group gets
+      camera slots (g, c): its observations of camera c (group-local indices);
+      block slots (g, c1 <= c2): its points' observation pairs o1 < o2 (cameras
+        c1 <= c2; c1 == c2 only for a point observed twice by one camera);
+    and each slot's partial row sits in camera- / block-major order (rows of
+    one camera / block contiguous, in group order) for the assembly."""
     O = len(cam_idx)
+    C = n_cams
     order = np.lexsort((cam_idx, pt_idx))  # by point, then camera
-    obs_cam = cam_idx[order].astype(np.int32)
-    obs_pt = pt_idx[order].astype(np.int32)
+    obs_cam = cam_idx[order].astype(np.int64)
+    obs_pt = pt_idx[order].astype(np.int64)
     pt_ptr = np.zeros(n_pts + 1, np.int64)
     np.cumsum(np.bincount(obs_pt, minlength=n_pts), out=pt_ptr[1:])
-    cam_obs = np.argsort(obs_cam, kind="stable").astype(np.int32)
-    obs_campos = np.empty(O, np.int32)
-    obs_campos[cam_obs] = np.arange(O, dtype=np.int32)
-    # cameras without observations are allowed (a rank's shard may not see every
-    # camera); their blocks assemble to zeros and the damping keeps S definite
-    cam_cnt = np.bincount(obs_cam, minlength=n_cams)
-    cam_ptr = np.concatenate([[0], np.cumsum(cam_cnt)])
-    chunks, cptr = [], [0]
-    for c in range(n_cams):
-        for b in range(cam_ptr[c], cam_ptr[c + 1], cam_chunk):
-            chunks.append((c, b, min(b + cam_chunk, cam_ptr[c + 1])))
-        cptr.append(len(chunks))
-    cam_chunks = np.asarray(chunks, np.int32).reshape(-1, 3)
+    grp_ptr = point_groups(pt_ptr, GROUP_OBS)
+    G = len(grp_ptr) - 1
+    pt_grp = np.repeat(np.arange(G), np.diff(grp_ptr))
+    obs_grp = pt_grp[obs_pt] if O else np.zeros(0, np.int64)
+    loc = np.arange(O) - pt_ptr[grp_ptr[:-1]][obs_grp] if O else np.zeros(0, np.int64)
 
-    # Schur pairs: per point, ordered obs pairs (i, j) with cam_i <= cam_j
+    # camera slots: (group, camera), observations in group order
+    ck = obs_grp * C + obs_cam
+    so = np.lexsort((np.arange(O), ck))
+    ukey, ustart = np.unique(ck[so], return_index=True)
+    cslot_grp, cslot_cam = ukey // C, ukey % C
+    cslot_obs_ptr = np.append(ustart, O)
+    cslot_obs = loc[so]
+    grp_cslot = np.searchsorted(cslot_grp, np.arange(G + 1))
+    cam_cslots = np.lexsort((cslot_grp, cslot_cam))
+    cslot_row = np.empty(len(cam_cslots), np.int64)
+    cslot_row[cam_cslots] = np.arange(len(cam_cslots))
+    cam_cslot_ptr = np.zeros(C + 1, np.int64)
+    np.cumsum(np.bincount(cslot_cam, minlength=C), out=cam_cslot_ptr[1:])
+
+    # block slots: per point, observation pairs (i < j) -> cameras c_i <= c_j
     cnt = np.diff(pt_ptr)
     o1s, o2s = [], []
     for n in np.unique(cnt):
-        if n == 0:
+        if n < 2:
             continue
-        pts_n = np.nonzero(cnt == n)[0]
-        base = pt_ptr[pts_n][:, None, None]
-        ii, jj = np.meshgrid(np.arange(n), np.arange(n), indexing="ij")
-        a = (base + ii[None]).reshape(len(pts_n), -1)
-        b = (base + jj[None]).reshape(len(pts_n), -1)
-        keep = obs_cam[a] <= obs_cam[b]
-        o1s.append(a[keep])
-        o2s.append(b[keep])
+        base = pt_ptr[np.nonzero(cnt == n)[0]][:, None]
+        ii, jj = np.triu_indices(n, 1)
+        o1s.append((base + ii[None]).ravel())
+        o2s.append((base + jj[None]).ravel())
     o1 = np.concatenate(o1s) if o1s else np.zeros(0, np.int64)
     o2 = np.concatenate(o2s) if o2s else np.zeros(0, np.int64)
-    bid = obs_cam[o1].astype(np.int64) * n_cams + obs_cam[o2]
-    so = np.lexsort((o1, bid))
-    o1, o2, bid = o1[so], o2[so], bid[so]
-    ub, bstart = np.unique(bid, return_index=True)
-    bend = np.append(bstart[1:], len(bid))
-    # every upper block (c1 <= c2) gets a workgroup in k_assemble, so the whole
-    # of S is written each iteration; blocks with no common point have no chunks
-    c1, c2 = np.triu_indices(n_cams)
-    blocks = np.stack([c1, c2], 1).astype(np.int32)
-    span = dict(zip(ub.tolist(), zip(bstart.tolist(), bend.tolist())))
-    pchunks, bptr = [], [0]
-    for k, key in enumerate((c1.astype(np.int64) * n_cams + c2).tolist()):
-        if key in span:
-            lo, hi = span[key]
-            for b in range(lo, hi, pair_chunk):
-                pchunks.append((k, b, min(b + pair_chunk, hi)))
-        bptr.append(len(pchunks))
-    grp_ptr = point_groups(pt_ptr, GROUP_OBS)
+    NB = C * (C + 1) // 2
+    blk = block_index(obs_cam[o1], obs_cam[o2], C)
+    bk = obs_grp[o1] * NB + blk
+    sp = np.lexsort((o2, o1, bk))
+    bkey, bstart = np.unique(bk[sp], return_index=True)
+    bslot_grp, bslot_blk = bkey // NB, bkey % NB
+    bslot_pair_ptr = np.append(bstart, len(sp))
+    bslot_pairs = loc[o1[sp]] | (loc[o2[sp]] << 16)
+    grp_bslot = np.searchsorted(bslot_grp, np.arange(G + 1))
+    blk_bslots = np.lexsort((bslot_grp, bslot_blk))
+    bslot_row = np.empty(len(blk_bslots), np.int64)
+    bslot_row[blk_bslots] = np.arange(len(blk_bslots))
+    blk_bslot_ptr = np.zeros(NB + 1, np.int64)
+    np.cumsum(np.bincount(bslot_blk, minlength=NB), out=blk_bslot_ptr[1:])
+
+    c1, c2 = np.triu_indices(C)
+    i32 = lambda a: np.asarray(a, np.int32)  # noqa: E731
     return dict(
-        order=order, obs_cam=obs_cam, obs_pt=obs_pt, pt_ptr=pt_ptr.astype(np.int32),
-        grp_ptr=grp_ptr,
-        cam_obs=cam_obs, obs_campos=obs_campos, cam_chunks=cam_chunks, cam_chunk_ptr=np.asarray(cptr, np.int32),
-        pair_o=np.stack([o1, o2], 1).astype(np.int32),
-        pair_chunks=np.asarray(pchunks, np.int32).reshape(-1, 3), blocks=blocks,
-        block_chunk_ptr=np.asarray(bptr, np.int32), n_obs=O)
+        order=order, obs_cam=i32(obs_cam), obs_pt=i32(obs_pt), pt_ptr=i32(pt_ptr),
+        grp_ptr=i32(grp_ptr), grp_cslot=i32(grp_cslot), cslot_cam=i32(cslot_cam),
+        cslot_obs_ptr=i32(cslot_obs_ptr), cslot_obs=i32(cslot_obs), grp_bslot=i32(grp_bslot),
+        bslot_blk=i32(bslot_blk), bslot_pair_ptr=i32(bslot_pair_ptr), bslot_pairs=i32(bslot_pairs),
+        blocks=i32(np.stack([c1, c2], 1)), cam_cslot_ptr=i32(cam_cslot_ptr),
+        cslot_row=i32(cslot_row), blk_bslot_ptr=i32(blk_bslot_ptr), bslot_row=i32(bslot_row),
+        n_obs=O)
+
+
+_INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
+                 "cslot_obs_ptr", "cslot_obs", "grp_bslot", "bslot_blk", "bslot_pair_ptr",
+                 "bslot_pairs", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
+                 "bslot_row")
 
 
 class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
-    def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, cam_chunk=512,
-                 pair_chunk=64, stream=None):
+    def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None):
         dev = require_gpu()
         cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
         C, P = len(cams), len(pts)
         cam_idx, pt_idx, qs = _check_indices(C, P, cam_idx, pt_idx, qs)
-        pl = plan(C, P, cam_idx, pt_idx, cam_chunk, pair_chunk)
+        pl = plan(C, P, cam_idx, pt_idx)
         self.plan = pl
         self.C, self.P, self.O = C, P, pl["n_obs"]
         self.stream = stream
@@ -151,18 +173,15 @@ class BAProblem:
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
         t["camrec0"], t["camrec1"] = z(C * 32), z(C * 32)
-        for k in ("obs_cam", "obs_pt", "pt_ptr", "cam_obs", "obs_campos", "cam_chunks",
-                  "cam_chunk_ptr", "pair_o", "pair_chunks", "blocks", "block_chunk_ptr",
-                  "grp_ptr"):
+        for k in _INDEX_TABLES:
             arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
             t[k] = T(arr.astype(np.int32))
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
-        O, C9 = self.O, 9 * C
-        t["recc"] = z(O * 32)
-        t["wy"] = z(O * 54)
+        C9 = 9 * C
+        n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])
         t["ptdata"] = z(P * 16)
-        t["cam_part"] = z(len(pl["cam_chunks"]) * 256)
-        t["pair_part"] = z(len(pl["pair_chunks"]) * 81)
+        t["cpart"] = z(n_cs * 112)
+        t["bpart"] = z(n_bs * 81)
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C))
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
@@ -173,19 +192,14 @@ class BAProblem:
         t["small"] = z(4)
         t["state"] = z(N_STATE)
         s = _Prob()
-        s.n_cams, s.n_pts, s.n_obs = C, P, O
-        s.n_cam_chunks = len(pl["cam_chunks"])
+        s.n_cams, s.n_pts, s.n_obs, s.n_grps = C, P, self.O, G
         s.n_blocks = len(pl["blocks"])
-        s.n_pair_chunks = len(pl["pair_chunks"])
-        s.n_pairs = len(pl["pair_o"])
-        s.n_grps = G
+        s.n_cslots, s.n_bslots = n_cs, n_bs
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
-        for k in ("obs_cam", "obs_pt", "obs_q", "pt_ptr", "cam_obs", "cam_chunks", "cam_chunk_ptr",
-                  "pair_o", "pair_chunks", "blocks", "block_chunk_ptr", "obs_campos", "grp_ptr",
-                  "recc", "wy", "ptdata", "cam_part", "pair_part", "sys", "chol", "delta_c",
-                  "red_part", "small", "state", "ticket"):
+        for k in _INDEX_TABLES + ("obs_q", "ptdata", "cpart", "bpart", "sys", "chol", "delta_c",
+                                  "red_part", "small", "state", "ticket"):
             setattr(s, k, t[k].data_ptr())
         self._s = s
         self.reset(lam0)

@@ -77,47 +77,64 @@ def test_oracle_lm_reaches_reference_optimum(g):
     assert hist[-1]["cost"] <= ref_default
 
 
-def test_planner_pairs_cover_schur_structure():
+def test_planner_slots_cover_schur_structure():
     from slam355 import ba
 
     cams, pts, ci, pi, qs = make_problem(1, 7, 200, 4)
-    # add a duplicate observation (camera sees a point twice) and an isolated obs
+    # add a duplicate observation (camera sees a point twice)
     ci = np.append(ci, ci[0])
     pi = np.append(pi, pi[0])
-    pl = ba.plan(7, 200, ci, pi, cam_chunk=16, pair_chunk=8)
-    # every point with n obs contributes sum over ordered pairs with cam_i <= cam_j
-    o1, o2 = pl["pair_o"][:, 0], pl["pair_o"][:, 1]
-    assert (pl["obs_pt"][o1] == pl["obs_pt"][o2]).all()
-    assert (pl["obs_cam"][o1] <= pl["obs_cam"][o2]).all()
-    exp = 0
-    for p in range(200):
-        cs = pl["obs_cam"][pl["pt_ptr"][p]:pl["pt_ptr"][p + 1]]
-        exp += int((cs[:, None] <= cs[None, :]).sum())
-    assert len(o1) == exp
-    # chunks tile each camera's observation list and each block's pair list
-    cc = pl["cam_chunks"]
-    assert cc[0, 1] == 0 and cc[-1, 2] == len(ci) and (cc[1:, 1] == cc[:-1, 2]).all()
-    assert ((cc[:, 2] - cc[:, 1]) <= 16).all()
-    pc = pl["pair_chunks"]
-    assert pc[0, 1] == 0 and pc[-1, 2] == len(o1) and (pc[1:, 1] == pc[:-1, 2]).all()
-    # camera-ordered record positions invert cam_obs; all 28 upper blocks listed
-    assert np.array_equal(pl["cam_obs"][pl["obs_campos"]], np.arange(len(ci)))
-    assert len(pl["blocks"]) == 7 * 8 // 2 and (pl["blocks"][:, 0] <= pl["blocks"][:, 1]).all()
-    bcp = pl["block_chunk_ptr"]
-    for k, (a, b) in enumerate(pl["blocks"]):
-        for ch in range(bcp[k], bcp[k + 1]):
-            lo, hi = pc[ch, 1], pc[ch, 2]
-            assert (pl["obs_cam"][o1[lo:hi]] == a).all() and (pl["obs_cam"][o2[lo:hi]] == b).all()
+    pl = ba.plan(7, 200, ci, pi)
+    gp, ptr = pl["grp_ptr"], pl["pt_ptr"]
+    G = len(gp) - 1
+    o0 = ptr[gp[:-1]]
     # point groups: whole points, <= 128 obs each, covering every point once
-    gp = pl["grp_ptr"]
     assert gp[0] == 0 and gp[-1] == 200 and (np.diff(gp) > 0).all()
-    assert (pl["pt_ptr"][gp[1:]] - pl["pt_ptr"][gp[:-1]] <= ba.GROUP_OBS).all()
+    assert (ptr[gp[1:]] - o0 <= ba.GROUP_OBS).all()
+    # camera slots: each observation exactly once, in its group and camera
+    seen = np.zeros(len(ci), int)
+    for g in range(G):
+        for s in range(pl["grp_cslot"][g], pl["grp_cslot"][g + 1]):
+            obs = o0[g] + pl["cslot_obs"][pl["cslot_obs_ptr"][s]:pl["cslot_obs_ptr"][s + 1]]
+            assert (obs < ptr[gp[g + 1]]).all() and (pl["obs_cam"][obs] == pl["cslot_cam"][s]).all()
+            seen[obs] += 1
+    assert (seen == 1).all()
+    # block slots: every within-point pair o1 < o2 once, in the block of its cameras
+    exp = sum(n * (n - 1) // 2 for n in np.diff(ptr))
+    tri = {tuple(b): k for k, b in enumerate(pl["blocks"])}
+    got = 0
+    for g in range(G):
+        for s in range(pl["grp_bslot"][g], pl["grp_bslot"][g + 1]):
+            pr = pl["bslot_pairs"][pl["bslot_pair_ptr"][s]:pl["bslot_pair_ptr"][s + 1]]
+            a, b = o0[g] + (pr & 0xFFFF), o0[g] + (pr >> 16)
+            assert (a < b).all() and (pl["obs_pt"][a] == pl["obs_pt"][b]).all()
+            c1, c2 = pl["obs_cam"][a], pl["obs_cam"][b]
+            assert (c1 <= c2).all()
+            assert all(tri[(x, y)] == pl["bslot_blk"][s] for x, y in zip(c1, c2))
+            got += len(pr)
+    assert got == exp
+    # partial rows: camera- / block-major, group order inside a camera / block
+    for key, row, ptr_, grp in (("cslot_cam", "cslot_row", "cam_cslot_ptr", "grp_cslot"),
+                                ("bslot_blk", "bslot_row", "blk_bslot_ptr", "grp_bslot")):
+        owner = pl[key]
+        rows = pl[row]
+        assert np.array_equal(np.sort(rows), np.arange(len(rows)))
+        sg = np.repeat(np.arange(G), np.diff(pl[grp]))
+        for b in range(len(pl[ptr_]) - 1):
+            sl = np.nonzero(owner == b)[0]
+            assert np.array_equal(np.sort(rows[sl]), np.arange(pl[ptr_][b], pl[ptr_][b + 1]))
+            assert (np.diff(sg[sl][np.argsort(rows[sl])]) >= 0).all()
+    # the duplicate observation makes a (c, c) pair
+    assert any(pl["blocks"][k][0] == pl["blocks"][k][1] for k in pl["bslot_blk"])
+    assert len(pl["blocks"]) == 7 * 8 // 2 and (pl["blocks"][:, 0] <= pl["blocks"][:, 1]).all()
+    assert np.array_equal(ba.block_index(pl["blocks"][:, 0], pl["blocks"][:, 1], 7),
+                          np.arange(28))
     assert np.array_equal(ba.point_groups(np.array([0])), [0, 0])
     with pytest.raises(ValueError):
         ba.point_groups(np.array([0, 200]))
     # a camera with no observations still plans (sharded problems)
     pl2 = ba.plan(9, 200, ci, pi)
-    assert len(pl2["blocks"]) == 45 and pl2["cam_chunk_ptr"][-1] == pl2["cam_chunk_ptr"][-2]
+    assert len(pl2["blocks"]) == 45 and pl2["cam_cslot_ptr"][-1] == pl2["cam_cslot_ptr"][-2]
 
 
 def test_bal_file_roundtrip(tmp_path):
@@ -155,11 +172,18 @@ def test_gpu_jacobian_matches_oracle(g):
 
 
 @pytest.mark.gpu
-def test_gpu_lm_iterates_match_oracle():
+@pytest.mark.parametrize("dup", [0, 5])
+def test_gpu_lm_iterates_match_oracle(dup):
+    """dup > 0: some points are observed twice by the same camera (a (c, c)
+    pair inside the point's Schur block)."""
     from slam355 import ba
 
     cams, pts, ci, pi, qs = make_problem(3, 6, 150, 4)
     rng = np.random.default_rng(4)
+    if dup:
+        k = rng.choice(len(ci), dup, replace=False)
+        ci, pi = np.append(ci, ci[k]), np.append(pi, pi[k])
+        qs = np.vstack([qs, qs[k] + rng.normal(0, 0.5, (dup, 2))])
     cams0 = cams.copy()
     cams0[:, :3] += rng.normal(0, 1e-3, (6, 3))
     cams0[:, 3:6] += rng.normal(0, 1e-2, (6, 3))
