@@ -51,6 +51,12 @@ constexpr double kDiagMin = 1e-6, kDiagMax = 1e32;
 constexpr double kLamMin = 1e-16, kLamMax = 1e32;
 constexpr int kBS = 256;   // block size of the element-wise kernels
 
+// The LM kernels are short and latency-bound and usually share their CUs with
+// the (throughput-bound) ORB workgroups of the concurrent tracking stream: they
+// raise their waves' issue priority so their dependent chains are issued first
+// and the ORB waves fill the gaps.
+__device__ __forceinline__ void lm_wave_priority() { __builtin_amdgcn_s_setprio(3); }
+
 // ---------------------------------------------------------------- projection
 // Residual (proj - q) of BundleAdjustment.py:317-337 with the operation order
 // of the numpy code, and optionally its analytic 2x12 Jacobian.
@@ -373,6 +379,7 @@ __device__ __forceinline__ void lin_slots(const slam_ba_problem& p, LinLds& L, i
 #define LIN_T(i) (void)0
 #endif
 __global__ __launch_bounds__(kLinWG) void k_linearize(slam_ba_problem p) {
+  lm_wave_priority();
   __shared__ LinLds L;
   LIN_T(0);
   const int g = blockIdx.x;
@@ -526,6 +533,7 @@ __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, in
 // Blocks without observations / common points are written as zeros, so sys
 // needs no separate clearing.
 __global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
+  lm_wave_priority();
   __shared__ double red[kAsmWG / 81][kCPart];
   __shared__ double sh[kCPart];
   __shared__ double sb[81];
@@ -666,6 +674,7 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
 
 // Large systems (9C > kLdsMaxN): packed factor in global memory (p.chol).
 __global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
+  lm_wave_priority();
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* red = lds;
   int* fail_p = reinterpret_cast<int*>(lds + 16);
@@ -779,6 +788,7 @@ struct BlkLds {
 };
 
 __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
+  lm_wave_priority();
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* red = lds;
   int* fail_p = reinterpret_cast<int*>(lds + 16);
@@ -1054,6 +1064,7 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
 // decision.
 template <bool DECIDE>
 __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* __restrict__ part) {
+  lm_wave_priority();
   __shared__ double sdy[kGrp][3];
   __shared__ double snp[kGrp][3];
   __shared__ double red[kGrp / 64];
