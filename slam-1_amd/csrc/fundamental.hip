@@ -34,6 +34,24 @@ __device__ inline uint64_t splitmix64(uint64_t& s) {
   return z ^ (z >> 31);
 }
 
+// 7 distinct indices in [0, M) from the hypothesis' splitmix64 stream
+// (rejection of repeats, as oracle/fundamental.c); unrolled so idx stays in
+// registers
+__device__ __forceinline__ void draw_sample(uint64_t& s, int M, int idx[kS]) {
+#pragma unroll
+  for (int k = 0; k < kS; ++k) {
+    int v;
+    bool dup;
+    do {
+      v = (int)((splitmix64(s) >> 32) % (uint64_t)M);
+      dup = false;
+#pragma unroll
+      for (int j = 0; j < k; ++j) dup |= idx[j] == v;
+    } while (dup);
+    idx[k] = v;
+  }
+}
+
 __device__ inline double det3(const double* F) {
   return F[0] * (F[4] * F[8] - F[5] * F[7]) - F[1] * (F[3] * F[8] - F[5] * F[6]) +
          F[2] * (F[3] * F[7] - F[4] * F[6]);
@@ -45,7 +63,12 @@ __device__ inline double detmix(const double* F1, const double* F2, double a) {
   return det3(F);
 }
 
-__device__ int cubic_roots(double c3, double c2, double c1, double c0, double* r) {
+// Real roots of c3 x^3 + c2 x^2 + c1 x + c0, polished by two Newton steps and
+// sorted ascending (oracle/fundamental.c states the same arithmetic).  The
+// roots live in three fixed registers (every index is a compile-time
+// constant, so nothing spills to scratch); unused slots hold +inf.
+__device__ int cubic_roots(double c3, double c2, double c1, double c0, double r[3]) {
+  r[0] = r[1] = r[2] = INFINITY;
   const double mx = fmax(fmax(fabs(c3), fabs(c2)), fmax(fabs(c1), fabs(c0)));
   if (mx == 0.0) return 0;
   int n = 0;
@@ -59,8 +82,12 @@ __device__ int cubic_roots(double c3, double c2, double c1, double c0, double* r
     if (d < 0) return 0;
     const double sq = sqrt(d);
     const double q = -0.5 * (c1 + (c1 >= 0 ? sq : -sq));
-    r[n++] = q / c2;
-    if (q != 0.0) r[n++] = c0 / q;
+    r[0] = q / c2;
+    n = 1;
+    if (q != 0.0) {
+      r[1] = c0 / q;
+      n = 2;
+    }
   } else {
     const double a = c2 / c3, b = c1 / c3, c = c0 / c3;
     const double p = b - a * a / 3.0;
@@ -69,95 +96,147 @@ __device__ int cubic_roots(double c3, double c2, double c1, double c0, double* r
     if (disc > 0) {
       const double sd = sqrt(disc);
       const double u = cbrt(-q / 2.0 + sd), v = cbrt(-q / 2.0 - sd);
-      r[n++] = u + v - a / 3.0;
+      r[0] = u + v - a / 3.0;
+      n = 1;
     } else {
       const double rr = sqrt(fmax(-p / 3.0, 0.0));
       double ca = rr > 0 ? -q / (2.0 * rr * rr * rr) : 0.0;
       ca = fmin(fmax(ca, -1.0), 1.0);
       const double phi = acos(ca);
+#pragma unroll
       for (int k = 0; k < 3; ++k)
-        r[n++] = 2.0 * rr * cos((phi + 2.0 * 3.14159265358979323846 * k) / 3.0) - a / 3.0;
+        r[k] = 2.0 * rr * cos((phi + 2.0 * 3.14159265358979323846 * k) / 3.0) - a / 3.0;
+      n = 3;
     }
   }
-  for (int i = 0; i < n; ++i)
-    for (int it = 0; it < 2; ++it) {
-      const double x = r[i];
-      const double f = ((c3 * x + c2) * x + c1) * x + c0;
-      const double df = (3.0 * c3 * x + 2.0 * c2) * x + c1;
-      if (df != 0.0) r[i] = x - f / df;
-    }
-  for (int i = 1; i < n; ++i)
-    for (int j = i; j > 0 && r[j] < r[j - 1]; --j) {
-      const double t = r[j];
-      r[j] = r[j - 1];
-      r[j - 1] = t;
-    }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < n)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const double x = r[i];
+        const double f = ((c3 * x + c2) * x + c1) * x + c0;
+        const double df = (3.0 * c3 * x + 2.0 * c2) * x + c1;
+        if (df != 0.0) r[i] = x - f / df;
+      }
+  // insertion sort of the first n (the +inf slots stay behind)
+  if (n > 1 && r[1] < r[0]) { const double t = r[0]; r[0] = r[1]; r[1] = t; }
+  if (n > 2 && r[2] < r[1]) {
+    const double t = r[1]; r[1] = r[2]; r[2] = t;
+    if (r[1] < r[0]) { const double u = r[0]; r[0] = r[1]; r[1] = u; }
+  }
   return n;
 }
 
-__device__ int seven_point(const double* m1, const double* m2, const int* idx, double* Fout) {
-  double c1x = 0, c1y = 0, c2x = 0, c2y = 0;
+// The 7-point algorithm on Hartley-normalised points: Gauss-Jordan with full
+// pivoting on the 7x9 system, the two-dimensional null space (F1, F2), the
+// cubic det(a F1 + (1 - a) F2) = 0, de-normalisation and unit Frobenius norm.
+// Writes up to 3 candidates to out (LDS) and returns their number.  Pivot rows,
+// pivot columns and the free columns are data-dependent, so they are applied
+// as selects over fully unrolled loops: the 7x9 matrix stays in registers.
+__device__ int seven_point(const double* m1, const double* m2, const int* idx, double (*out)[9]) {
+  double P1[kS][2], P2[kS][2];
+#pragma unroll
   for (int i = 0; i < kS; ++i) {
-    c1x += m1[2 * idx[i]]; c1y += m1[2 * idx[i] + 1];
-    c2x += m2[2 * idx[i]]; c2y += m2[2 * idx[i] + 1];
+    P1[i][0] = m1[2 * idx[i]]; P1[i][1] = m1[2 * idx[i] + 1];
+    P2[i][0] = m2[2 * idx[i]]; P2[i][1] = m2[2 * idx[i] + 1];
+  }
+  double c1x = 0, c1y = 0, c2x = 0, c2y = 0;
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    c1x += P1[i][0]; c1y += P1[i][1];
+    c2x += P2[i][0]; c2y += P2[i][1];
   }
   c1x /= kS; c1y /= kS; c2x /= kS; c2y /= kS;
   double d1 = 0, d2 = 0;
+#pragma unroll
   for (int i = 0; i < kS; ++i) {
-    d1 += sqrt((m1[2 * idx[i]] - c1x) * (m1[2 * idx[i]] - c1x) +
-               (m1[2 * idx[i] + 1] - c1y) * (m1[2 * idx[i] + 1] - c1y));
-    d2 += sqrt((m2[2 * idx[i]] - c2x) * (m2[2 * idx[i]] - c2x) +
-               (m2[2 * idx[i] + 1] - c2y) * (m2[2 * idx[i] + 1] - c2y));
+    d1 += sqrt((P1[i][0] - c1x) * (P1[i][0] - c1x) + (P1[i][1] - c1y) * (P1[i][1] - c1y));
+    d2 += sqrt((P2[i][0] - c2x) * (P2[i][0] - c2x) + (P2[i][1] - c2y) * (P2[i][1] - c2y));
   }
   d1 /= kS; d2 /= kS;
   if (!(d1 > 1e-12) || !(d2 > 1e-12)) return 0;
   const double s1 = sqrt(2.0) / d1, s2 = sqrt(2.0) / d2;
   double A[7][9];
+#pragma unroll
   for (int i = 0; i < kS; ++i) {
-    const double x1 = (m1[2 * idx[i]] - c1x) * s1, y1 = (m1[2 * idx[i] + 1] - c1y) * s1;
-    const double x2 = (m2[2 * idx[i]] - c2x) * s2, y2 = (m2[2 * idx[i] + 1] - c2y) * s2;
+    const double x1 = (P1[i][0] - c1x) * s1, y1 = (P1[i][1] - c1y) * s1;
+    const double x2 = (P2[i][0] - c2x) * s2, y2 = (P2[i][1] - c2y) * s2;
     A[i][0] = x2 * x1; A[i][1] = x2 * y1; A[i][2] = x2;
     A[i][3] = y2 * x1; A[i][4] = y2 * y1; A[i][5] = y2;
     A[i][6] = x1; A[i][7] = y1; A[i][8] = 1.0;
   }
-  int pc[7], used[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int pc[7];
+  unsigned used = 0;
+#pragma unroll
   for (int r = 0; r < 7; ++r) {
     int bi = -1, bj = -1;
     double bv = 0.0;
+#pragma unroll
     for (int i = r; i < 7; ++i)
+#pragma unroll
       for (int j = 0; j < 9; ++j)
-        if (!used[j] && fabs(A[i][j]) > bv) {
+        if (!((used >> j) & 1u) && fabs(A[i][j]) > bv) {
           bv = fabs(A[i][j]);
           bi = i;
           bj = j;
         }
     if (bv < 1e-10) return 0;
-    if (bi != r)
+#pragma unroll
+    for (int i = r + 1; i < 7; ++i) {
+      const bool sw = i == bi;
+#pragma unroll
       for (int j = 0; j < 9; ++j) {
         const double t = A[r][j];
-        A[r][j] = A[bi][j];
-        A[bi][j] = t;
+        A[r][j] = sw ? A[i][j] : t;
+        A[i][j] = sw ? t : A[i][j];
       }
-    used[bj] = 1;
+    }
+    used |= 1u << bj;
     pc[r] = bj;
-    const double inv = 1.0 / A[r][bj];
+    double piv = 0.0;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) piv = j == bj ? A[r][j] : piv;
+    const double inv = 1.0 / piv;
+#pragma unroll
     for (int j = 0; j < 9; ++j) A[r][j] *= inv;
+#pragma unroll
     for (int i = 0; i < 7; ++i) {
       if (i == r) continue;
-      const double f = A[i][bj];
-      if (f != 0.0)
-        for (int j = 0; j < 9; ++j) A[i][j] -= f * A[r][j];
+      double f = 0.0;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) f = j == bj ? A[i][j] : f;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) A[i][j] = f != 0.0 ? A[i][j] - f * A[r][j] : A[i][j];
     }
   }
-  int fr[2], nf = 0;
+  // the first two unused columns span the null space
+  int fr0 = -1, fr1 = -1;
+#pragma unroll
   for (int j = 0; j < 9; ++j)
-    if (!used[j] && nf < 2) fr[nf++] = j;
+    if (!((used >> j) & 1u)) {
+      if (fr0 < 0) fr0 = j;
+      else if (fr1 < 0) fr1 = j;
+    }
   double F1[9], F2[9];
-  for (int k = 0; k < 2; ++k) {
-    double* f = k ? F2 : F1;
-    for (int j = 0; j < 9; ++j) f[j] = 0.0;
-    f[fr[k]] = 1.0;
-    for (int r = 0; r < 7; ++r) f[pc[r]] = -A[r][fr[k]];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    F1[j] = j == fr0 ? 1.0 : 0.0;
+    F2[j] = j == fr1 ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    double a1 = 0.0, a2 = 0.0;  // A[r][fr0], A[r][fr1]
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      a1 = j == fr0 ? A[r][j] : a1;
+      a2 = j == fr1 ? A[r][j] : a2;
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      F1[j] = j == pc[r] ? -a1 : F1[j];
+      F2[j] = j == pc[r] ? -a2 : F2[j];
+    }
   }
   const double v0 = detmix(F1, F2, 0.0), v1 = detmix(F1, F2, 1.0);
   const double vm = detmix(F1, F2, -1.0), v2 = detmix(F1, F2, 2.0);
@@ -172,20 +251,29 @@ __device__ int seven_point(const double* m1, const double* m2, const int* idx, d
   const double T1[9] = {s1, 0, -s1 * c1x, 0, s1, -s1 * c1y, 0, 0, 1};
   const double T2[9] = {s2, 0, -s2 * c2x, 0, s2, -s2 * c2y, 0, 0, 1};
   int n = 0;
-  for (int k = 0; k < nr; ++k) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nr) break;
     double Fn[9], tmp[9], F[9];
+#pragma unroll
     for (int i = 0; i < 9; ++i) Fn[i] = roots[k] * F1[i] + (1.0 - roots[k]) * F2[i];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j)
         tmp[3 * i + j] = Fn[3 * i] * T1[j] + Fn[3 * i + 1] * T1[3 + j] + Fn[3 * i + 2] * T1[6 + j];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j)
         F[3 * i + j] = T2[i] * tmp[j] + T2[3 + i] * tmp[3 + j] + T2[6 + i] * tmp[6 + j];
     double nrm = 0.0;
+#pragma unroll
     for (int i = 0; i < 9; ++i) nrm += F[i] * F[i];
     nrm = sqrt(nrm);
     if (!(nrm > 0.0) || !isfinite(nrm)) continue;
-    for (int i = 0; i < 9; ++i) Fout[9 * n + i] = F[i] / nrm;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) out[n][i] = F[i] / nrm;
     ++n;
   }
   return n;
@@ -219,6 +307,7 @@ __global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1a
   __shared__ float wbest[kWaves];
   __shared__ int wbidx[kWaves];
   __shared__ double Fb[9];
+  __shared__ double Fw[3][9];  // the winner's candidates, recomputed
   __shared__ float best_s;
   __shared__ int found_s, cnt_s;
   const int b = blockIdx.x, t = threadIdx.x;
@@ -243,21 +332,8 @@ __global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1a
       uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
                    ((uint64_t)h * 0x9FB21C651E98DF25ull);
       int idx[kS];
-      for (int k = 0; k < kS; ++k) {
-        int v;
-        bool dup;
-        do {
-          v = (int)((splitmix64(s) >> 32) % (uint64_t)M);
-          dup = false;
-          for (int j = 0; j < k; ++j) dup |= idx[j] == v;
-        } while (dup);
-        idx[k] = v;
-      }
-      double F[27];
-      const int nc = seven_point(m1, m2, idx, F);
-      for (int k = 0; k < nc; ++k)
-        for (int i = 0; i < 9; ++i) cand[t][k][i] = F[9 * k + i];
-      ncand[t] = nc;
+      draw_sample(s, M, idx);
+      ncand[t] = seven_point(m1, m2, idx, cand[t]);
     }
     __syncthreads();
     for (int hl = w; hl < nh; hl += kWaves) {
@@ -336,19 +412,9 @@ __global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1a
       uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
                    ((uint64_t)h * 0x9FB21C651E98DF25ull);
       int idx[kS];
-      for (int kk = 0; kk < kS; ++kk) {
-        int v;
-        bool dup;
-        do {
-          v = (int)((splitmix64(s) >> 32) % (uint64_t)M);
-          dup = false;
-          for (int j = 0; j < kk; ++j) dup |= idx[j] == v;
-        } while (dup);
-        idx[kk] = v;
-      }
-      double F[27];
-      seven_point(m1, m2, idx, F);
-      for (int i = 0; i < 9; ++i) Fb[i] = F[9 * k + i];
+      draw_sample(s, M, idx);
+      seven_point(m1, m2, idx, Fw);
+      for (int i = 0; i < 9; ++i) Fb[i] = Fw[k][i];
     }
   }
   __syncthreads();
