@@ -127,6 +127,29 @@ def pmc_bytes(pmc, kernels):
     return float(sum(pmc["kernels"][k]["hbm_bytes"] for k in kernels))
 
 
+def masked_stream(n_cus):
+    """A HIP stream whose kernels may use only CUs [0, n_cus) (hipExtStreamCreateWithCUMask),
+    wrapped as a torch stream: `--track-cus` keeps the rest of the CUs free of
+    tracking work for the local-BA stream."""
+    import ctypes
+
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"),
+                      mode=ctypes.RTLD_GLOBAL)
+    n_total = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    words = (n_total + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for i in range(min(n_cus, n_total)):
+        mask[i // 32] |= 1 << (i % 32)
+    h = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), words, mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    st = torch.cuda.ExternalStream(h.value)
+    # torch does not own the stream: destroy it before the runtime tears down
+    st.destroy = lambda: (torch.cuda.synchronize(), hip.hipStreamDestroy(h))
+    return st
+
+
 def run_tracking(args, world, rank):
     from slam355.ba import BAProblem
     from slam355.pipeline import Tracker, chain_poses
@@ -134,7 +157,9 @@ def run_tracking(args, world, rank):
 
     B = args.batch
     L, R, poses, rig = stereo_sequence(B + 1, W_IMG, H_IMG, seed=1000 + rank)
-    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=56, seed=rank)
+    trk_stream = masked_stream(args.track_cus) if args.track_cus else None
+    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=56, seed=rank,
+                  stream=trk_stream)
     trk.imgs.copy_(torch.from_numpy(np.concatenate([L, R[:B]])))
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
@@ -156,6 +181,10 @@ def run_tracking(args, world, rank):
         return ev
 
     def step(marks):
+        with torch.cuda.stream(trk_stream if trk_stream is not None else stream):
+            tracked_step(marks)
+
+    def tracked_step(marks):
         tmarks = [] if marks is not None else None
         trk.track(0, marks=tmarks)
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
@@ -226,7 +255,8 @@ def run_tracking(args, world, rank):
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
                                f"x {args.ba_iters} LM iters",
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
-                   "local_ba_stream": "serial" if args.ba_serial else "concurrent"},
+                   "local_ba_stream": "serial" if args.ba_serial else "concurrent",
+                   "tracking_cus": args.track_cus or "all"},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
         "stage_ms_per_step": per_step,
@@ -239,6 +269,9 @@ def run_tracking(args, world, rank):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_tracking(L, R, rig, args, C3, (c0, p0, ci, pi, qs))
+    del trk, ba  # their kernels' buffers, then the masked stream itself
+    if trk_stream is not None:
+        trk_stream.destroy()
     return rec
 
 
@@ -374,6 +407,10 @@ def main():
     ap.add_argument("--ba-serial", action="store_true",
                     help="run local BA on the tracking stream (no overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--track-cus", type=int, default=224,
+                    help="restrict the tracking stream to this many CUs (0: all); the rest run "
+                         "only local-BA work, whose latency-bound kernels then do not share "
+                         "SIMDs and LDS with ORB workgroups")
     args = ap.parse_args()
     world, rank = dist_init()
     run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher}[args.workload]
