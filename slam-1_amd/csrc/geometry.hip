@@ -11,6 +11,8 @@
 // sequence is not reproducible here).
 #include "common.hpp"
 
+#include <climits>
+
 #include <cmath>
 
 namespace {
@@ -315,6 +317,23 @@ __device__ void lm_small(const double* Q, const double* q, const int* idx, int n
   }
 }
 
+// Sum over the 64 lanes of a wave, every lane ends with the total (xor butterfly).
+__device__ __forceinline__ double wave_allsum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// One workgroup per frame pair:
+//   hypotheses   one per lane: 5 distinct random points, LM from r = t = 0; the
+//                pose and its rotation matrix go to LDS;
+//   counting     (hypothesis, point) pairs spread over the whole workgroup,
+//                inliers tallied with LDS atomics (integer: order-free);
+//   selection    max inliers, lowest h; the inlier mask of the winner;
+//   refinement   LM over the mask by wave 0 alone: lanes take points, the 28
+//                normal-equation sums are wave butterflies (every lane holds
+//                them), every lane solves the same 6x6 system — no workgroup
+//                barriers inside the iteration loop.
 __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
                                                 const double* __restrict__ qall,
                                                 const int32_t* __restrict__ count, int cap,
@@ -325,161 +344,153 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
                                                 int32_t* __restrict__ ninl,
                                                 uint8_t* __restrict__ mask) {
   __shared__ double hp[kMaxHyp][6];
+  __shared__ double hR[kMaxHyp][9];
   __shared__ int hcnt[kMaxHyp];
-  __shared__ double red[kPnPWG / 64][28];
-  __shared__ double pose[6], stepd[6];
-  __shared__ int best_s, ok_s;
+  __shared__ int best_s;
   const int b = blockIdx.x, t = threadIdx.x;
   const int lane = t & 63, wid = t >> 6;
   const int L = min(max(count[b], 0), cap);
   const double* Q = Qall + (size_t)b * cap * 3;
   const double* q = qall + (size_t)b * cap * 2;
+  uint8_t* mk = mask + (size_t)b * cap;
   const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
   if (L < kMinSample) {
     if (t == 0) {
       ninl[b] = -1;
       for (int i = 0; i < 3; ++i) rvec[3 * b + i] = tvec[3 * b + i] = 0.0;
     }
-    for (int i = t; i < L; i += kPnPWG) mask[(size_t)b * cap + i] = 0;
+    for (int i = t; i < L; i += kPnPWG) mk[i] = 0;
     return;
   }
   const double thr2 = thresh * thresh;
-  // ---- hypotheses: one per thread, 5 distinct random points, LM from r = t = 0
+#ifdef SLAM_PNP_PROFILE
+  const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- hypotheses
   for (int h = t; h < n_hyp; h += kPnPWG) {
     uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
                  ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
     int idx[kMinSample];
+#pragma unroll
     for (int k = 0; k < kMinSample; ++k) {
       int v;
       bool dup;
       do {
         v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
         dup = false;
+#pragma unroll
         for (int j = 0; j < k; ++j) dup |= idx[j] == v;
       } while (dup);
       idx[k] = v;
     }
-    double p[6] = {0, 0, 0, 0, 0, 0};
+    double p[6] = {0, 0, 0, 0, 0, 0}, R[9];
     lm_small(Q, q, idx, kMinSample, K, hyp_iters, p);
-    for (int i = 0; i < 6; ++i) hp[h][i] = p[i];
-    hcnt[h] = 0;
-  }
-  __syncthreads();
-  // ---- inlier counts: hypothesis-major, points across the workgroup
-  for (int h = 0; h < n_hyp; ++h) {
-    double R[9], p[6];
-    for (int i = 0; i < 6; ++i) p[i] = hp[h][i];
     const bool finite = isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]) && isfinite(p[3]) &&
                         isfinite(p[4]) && isfinite(p[5]);
     rodrigues(p, R);
-    int c = 0;
-    if (finite)
-      for (int i = t; i < L; i += kPnPWG) {
-        double r[2], J[2][6];
-        pnp_residual<false>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
-        c += (r[0] * r[0] + r[1] * r[1] <= thr2) ? 1 : 0;
-      }
-    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-    if (lane == 0) atomicAdd(&hcnt[h], finite ? c : 0);
+    for (int i = 0; i < 6; ++i) hp[h][i] = p[i];
+    for (int i = 0; i < 9; ++i) hR[h][i] = R[i];
+    hcnt[h] = finite ? 0 : INT_MIN;  // a non-finite pose scores 0 (see below)
+  }
+  __syncthreads();
+#ifdef SLAM_PNP_PROFILE
+  const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
+  // ---- inlier counts over (hypothesis, point) pairs
+  for (int pr = t; pr < n_hyp * L; pr += kPnPWG) {
+    const int h = pr / L, i = pr - h * L;
+    if (hcnt[h] < 0) continue;
+    double r[2], J[2][6];
+    pnp_residual<false>(hp[h], hR[h], Q + 3 * i, q + 2 * i, K, r, J);
+    if (r[0] * r[0] + r[1] * r[1] <= thr2) atomicAdd(&hcnt[h], 1);
   }
   __syncthreads();
   if (t == 0) {
-    int bh = 0;
+    int bh = 0, bc = max(hcnt[0], 0);
     for (int h = 1; h < n_hyp; ++h)
-      if (hcnt[h] > hcnt[bh]) bh = h;
+      if (max(hcnt[h], 0) > bc) {
+        bc = max(hcnt[h], 0);
+        bh = h;
+      }
     best_s = bh;
-    for (int i = 0; i < 6; ++i) pose[i] = hp[bh][i];
   }
   __syncthreads();
-  // ---- LM refinement over the best hypothesis' inlier set (fixed set)
   const int bh = best_s;
-  {
-    double R[9], p[6];
-    for (int i = 0; i < 6; ++i) p[i] = hp[bh][i];
-    rodrigues(p, R);
-    for (int i = t; i < L; i += kPnPWG) {
-      double r[2], J[2][6];
-      pnp_residual<false>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
-      mask[(size_t)b * cap + i] = (r[0] * r[0] + r[1] * r[1] <= thr2) ? 1 : 0;
-    }
+  for (int i = t; i < L; i += kPnPWG) {
+    double r[2], J[2][6];
+    pnp_residual<false>(hp[bh], hR[bh], Q + 3 * i, q + 2 * i, K, r, J);
+    mk[i] = (r[0] * r[0] + r[1] * r[1] <= thr2) ? 1 : 0;
   }
   __syncthreads();
-  double lam = 1e-3;  // uniform across the workgroup
+#ifdef SLAM_PNP_PROFILE
+  const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+#endif
+  if (wid != 0) return;
+  // ---- LM refinement over the winner's inliers (fixed set), wave 0
+  double p[6];
+  for (int i = 0; i < 6; ++i) p[i] = hp[bh][i];
+  double lam = 1e-3;
   for (int it = 0; it < refine_iters; ++it) {
-    double p[6], R[9];
-    for (int i = 0; i < 6; ++i) p[i] = pose[i];
+    double R[9];
     rodrigues(p, R);
     double acc[28];
+#pragma unroll
     for (int i = 0; i < 28; ++i) acc[i] = 0.0;
-    for (int i = t; i < L; i += kPnPWG) {
-      if (!mask[(size_t)b * cap + i]) continue;
+    for (int i = lane; i < L; i += 64) {
+      if (!mk[i]) continue;
       double r[2], J[2][6];
       pnp_residual<true>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
+#pragma unroll
       for (int a = 0; a < 2; ++a) {
         int k = 0;
+#pragma unroll
         for (int u = 0; u < 6; ++u) {
+#pragma unroll
           for (int v = 0; v <= u; ++v) acc[k++] += J[a][u] * J[a][v];
           acc[21 + u] += J[a][u] * r[a];
         }
         acc[27] += r[a] * r[a];
       }
     }
-    for (int i = 0; i < 28; ++i) {
-      double v = acc[i];
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-      if (lane == 0) red[wid][i] = v;
-    }
-    __syncthreads();
-    if (t == 0) {
-      double H[21], g[6], cost = 0.0;
-      for (int i = 0; i < 28; ++i) {
-        double v = 0.0;
-        for (int w = 0; w < kPnPWG / 64; ++w) v += red[w][i];
-        if (i < 21) H[i] = v;
-        else if (i < 27) g[i - 21] = v;
-        else cost = v;
-      }
-      double d[6];
-      ok_s = solve6(H, g, lam, d) ? 1 : 0;
-      for (int i = 0; i < 6; ++i) stepd[i] = ok_s ? p[i] + d[i] : p[i];
-      red[0][27] = cost;
-    }
-    __syncthreads();
-    const double cost = red[0][27];
-    // trial cost
-    double pn[6], Rn[9];
-    for (int i = 0; i < 6; ++i) pn[i] = stepd[i];
+    double H[21], g[6];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) H[i] = wave_allsum(acc[i]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) g[i] = wave_allsum(acc[21 + i]);
+    const double cost = wave_allsum(acc[27]);
+    double d[6], pn[6], Rn[9];
+    const bool ok = solve6(H, g, lam, d);
+    for (int i = 0; i < 6; ++i) pn[i] = ok ? p[i] + d[i] : p[i];
     rodrigues(pn, Rn);
     double cn = 0.0;
-    for (int i = t; i < L; i += kPnPWG) {
-      if (!mask[(size_t)b * cap + i]) continue;
+    for (int i = lane; i < L; i += 64) {
+      if (!mk[i]) continue;
       double r[2], J[2][6];
       pnp_residual<false>(pn, Rn, Q + 3 * i, q + 2 * i, K, r, J);
       cn += r[0] * r[0] + r[1] * r[1];
     }
-    for (int off = 32; off > 0; off >>= 1) cn += __shfl_down(cn, off, 64);
-    __syncthreads();
-    if (lane == 0) red[wid][0] = cn;
-    __syncthreads();
-    double cns = 0.0;
-    for (int w = 0; w < kPnPWG / 64; ++w) cns += red[w][0];
-    const bool accept = ok_s && cns < cost;
-    __syncthreads();
-    if (accept) {
-      if (t < 6) pose[t] = stepd[t];
+    cn = wave_allsum(cn);
+    if (ok && cn < cost) {
+      for (int i = 0; i < 6; ++i) p[i] = pn[i];
       lam = fmax(lam * 0.1, 1e-12);
     } else {
       lam = fmin(lam * 10.0, 1e12);
     }
-    __syncthreads();
   }
-  if (t < 3) {
-    rvec[3 * b + t] = pose[t];
-    tvec[3 * b + t] = pose[3 + t];
+  if (lane < 3) {
+    rvec[3 * b + lane] = p[lane];
+    tvec[3 * b + lane] = p[3 + lane];
   }
-  if (t == 0) ninl[b] = hcnt[bh];
+  if (lane == 0) ninl[b] = max(hcnt[bh], 0);
+#ifdef SLAM_PNP_PROFILE
+  const uint64_t pt3 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {  // cycles of hypotheses / counting / refinement in rvec (debug build)
+    rvec[3 * b] = (double)(pt1 - pt0);
+    rvec[3 * b + 1] = (double)(pt2 - pt1);
+    rvec[3 * b + 2] = (double)(pt3 - pt2);
+  }
+#endif
 }
-
 
 // --------------------------------------------------------------- stereo VO pose
 // The reference's second pose estimator (visual_odometry.py:65-81, 135-157):
