@@ -312,28 +312,40 @@ def cpu_baseline_tracking(L, R, rig, args, C3, ba_in, pairs=2):
 
 # ---------------------------------------------------------------------------- local BA
 def run_ba(args, world, rank):
-    from slam355.ba import BAProblem
-    from slam355.synthetic import ba_problem, perturb
+    from slam355.ba import BAProblem, packed, tiled_solve_flops, upper_blocks
+    from slam355.synthetic import ba_problem, ba_problem_loop, perturb
 
-    C, P, k = (10, 5000, 6) if world == 1 and not args.c4 else (64, 50000, 6)
+    if args.c5:
+        C, P, k, name = 500, 200000, 6, "C5"
+    elif world == 1 and not args.c4:
+        C, P, k, name = 10, 5000, 6, "C3"
+    else:
+        C, P, k, name = 64, 50000, 6, "C4"
     rng = np.random.default_rng(7)  # same global problem on every rank
-    cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+    gen = ba_problem_loop if name == "C5" else ba_problem
+    cams, pts, ci, pi, qs = gen(rng, C, P, k)
     c0, p0 = perturb(rng, cams, pts)
     if world > 1:
         from slam355.dist import shard_by_anchor
 
         mine, keep, local_pi = shard_by_anchor(C, P, ci, pi, rank, world)
-        prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep])
+        prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep],
+                         block_list=upper_blocks(C, ci, pi))
         step_fn = prob.step_distributed
     else:
         prob = BAProblem(c0, p0, ci, pi, qs)
-        step_fn = lambda: prob.iterate(1)  # noqa: E731
+        if args.no_graph:
+            step_fn = lambda: prob.iterate(1)  # noqa: E731
+        else:  # one LM iteration = one HIP-graph replay (3T + 5 launches for the tiled solver)
+            step_fn = lambda: prob.iterate_graphed(1)  # noqa: E731
 
     def step(marks):
         step_fn()
 
     dt, _ = timed_loop(step, args.steps, args.warmup, world, marks_every=False)
     flops = ba_flops_per_iter(C, P, P * k, k)
+    if packed(C):  # tiled solver: count the tile envelope it factors, not a dense (9C)^3/3
+        flops += tiled_solve_flops(C, prob.plan["blocks"]) - (9 * C) ** 3 / 3
     it_s = args.steps / dt
     achieved = flops * it_s / 1e12
     return {
@@ -342,7 +354,9 @@ def run_ba(args, world, rank):
         "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic BA problem (seeded, 6 obs/point, sigma 0.5 px)",
-        "config": {"workload": f"{'C4' if C == 64 else 'C3'} local BA {C} KF x {P} pts x {P * k} obs",
+        "config": {"workload": f"{name} {'loop-closure global' if name == 'C5' else 'local'} BA "
+                               f"{C} KF x {P} pts x {P * k} obs",
+                   "packed_blocks": int(prob.plan["blocks"].shape[0]),
                    "parallelism": f"landmark shards x{world} + RCCL all-reduce" if world > 1 else "1 GPU"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / F64_PEAK_TFLOPS, "traffic": None,
@@ -402,6 +416,8 @@ def main():
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")
+    ap.add_argument("--c5", action="store_true",
+                    help="--workload ba: C5 loop-closure global BA (500 KF x 200k pts)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the LM iterations eagerly instead of replaying a HIP graph")
     ap.add_argument("--ba-serial", action="store_true",

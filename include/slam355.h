@@ -266,7 +266,9 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
 typedef struct slam_ba_problem {
   int32_t n_cams, n_pts, n_obs;
   int32_t n_grps;        /* point groups (>= 1): <= 128 obs / points each     */
-  int32_t n_blocks;      /* upper camera-pair blocks of S: C(C+1)/2            */
+  int32_t n_blocks;      /* upper camera-pair blocks of S: all C(C+1)/2 when
+                            9C <= 120, else the diagonal + every pair with a
+                            common point (across all ranks), sorted          */
   int32_t n_cslots;      /* (group, camera) slots                             */
   int32_t n_bslots;      /* (group, camera-pair block) slots                  */
   int32_t reserved;
@@ -294,7 +296,7 @@ typedef struct slam_ba_problem {
   double* ptdata;               /* [P][16] e(3) g(3) diagV(3) V*^-1(6) -       */
   double* cpart;                /* [n_cslots][112] U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2 */
   double* bpart;                /* [n_bslots][81] sum Y W^T                    */
-  double* sys;                  /* S[(9C)^2] b[9C] g[9C] diagU[9C] cost[C]     */
+  double* sys;                  /* S (dense or packed blocks) b[9C] g[9C] diagU[9C] cost[C] */
   double* chol;                 /* [slam_ba_chol_len] (9C > 120 only)           */
   double* delta_c;              /* [9C]                                        */
   double* red_part;             /* [slam_ba_red_slots(n_grps)]                 */
@@ -305,10 +307,12 @@ typedef struct slam_ba_problem {
 
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);
-/* Doubles of the factorisation workspace `chol` (needed only when 9C > 120). */
+/* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120). */
 long long slam_ba_chol_len(int n_cams);
-/* Doubles in the all-reduced system buffer: (9C)^2 + 27C + C. */
-long long slam_ba_sys_len(int n_cams);
+/* Doubles in the all-reduced system buffer `sys`: dense (9C <= 120) (9C)^2,
+ * packed (9C > 120) 81 * n_blocks (the listed upper camera blocks), then
+ * b, g, diag U (9C each) and the per-camera cost (C). */
+long long slam_ba_sys_len(int n_cams, int n_blocks);
 
 /* Phase 1 (per rank): linearise at the live parameters and build this
  * rank's share of the reduced camera system into prob->sys. */
@@ -323,6 +327,30 @@ int slam_ba_decide(const slam_ba_problem* prob, void* stream);
 int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream);
 /* Reset the LM state: lambda0, nu = 2, cur = 0, counters = 0. */
 int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream);
+
+/* ------------------------------------------------------------------ pose chain
+ * The live pose-chain optimisation of BundleAdjustment.py:79-183 (loop
+ * closure): m relative poses [r0 r1 r2 t0 t1 t2] (cv2.Rodrigues rotation
+ * vector, translation), residuals f_i (weighted |.| of the six parameters,
+ * :114-127) and, with loop != 0, the two loop-closure residuals of the chained
+ * absolute pose (:128-134).  All pointers are device pointers. */
+
+/* resid[v][m (+2)] = objective(params[v]) (or objective_without_loop_closure
+ * when loop == 0) for n_vec parameter vectors params[v][6m]; each vector's
+ * chain product runs in the reference's order.  Replaces objective /
+ * objective_without_loop_closure, BundleAdjustment.py:79-145. */
+int slam_pose_chain_objective(const double* params, int n_vec, int n_frames, int loop,
+                              double* resid, void* stream);
+/* Doubles of the LM workspace for m frames (the live parameters sit at its
+ * start: ws[0 .. 6m)). */
+long long slam_pose_chain_workspace_len(int n_frames);
+/* n_iter Levenberg iterations on ws[0 .. 6m) in place (one workgroup, no host
+ * round trip).  lam_rel0 > 0: start from lam_rel0 * max diag(J J^T); else from
+ * state[2].  state[8]: cost0, cost, lambda, nu, iterations, accepted, rho,
+ * stopped.  Replaces least_squares(objective, ..., method='trf') of
+ * bundle_adjustment_with_sparsity, BundleAdjustment.py:173-183. */
+int slam_pose_chain_lm(double* ws, int n_frames, int loop, int n_iter, double lam_rel0,
+                       double* state, void* stream);
 
 #ifdef __cplusplus
 }

@@ -15,7 +15,7 @@
 //                             b = -Jc^T r - Jc^T u, g, diag U, cost
 //   (all-reduce of sys over ranks happens here for multi-GPU)
 //   k_solve_blk     1 WG   -> damp, blocked LDL^T (MFMA trailing updates), camera
-//                             step, pred_cam, trial cameras (k_solve for 9C > 120)
+//                             step, pred_cam, trial cameras (tiled k_tl_* for 9C > 120)
 //   k_back_trial    point group -> point step, trial points, trial |r|^2 and
 //                                  pred partials; the last group sums them into
 //                                  small (and, single rank, decides)
@@ -256,6 +256,17 @@ __device__ __forceinline__ int cur_of(const double* state) {
 }
 
 __device__ __forceinline__ double clampd(double d) { return fmin(fmax(d, kDiagMin), kDiagMax); }
+
+// Layout of sys (the buffer all-reduced across ranks).  Dense (9C <= 120, the
+// one-workgroup solver): S [(9C)^2] row-major, all C(C+1)/2 blocks listed.
+// Packed (larger systems, tiled solver): only the listed upper blocks
+// (diagonal + camera pairs with common points), 81 doubles each, row-major
+// (rows of c1, columns of c2).  Then b, g, diag U [9C] each and cost [C].
+constexpr int kDenseMaxN = 120;
+__host__ __device__ __forceinline__ bool sys_packed(int n_cams) { return 9 * n_cams > kDenseMaxN; }
+__host__ __device__ __forceinline__ long long sys_vec_off(int n_cams, int n_blocks) {
+  return sys_packed(n_cams) ? 81ll * n_blocks : 81ll * n_cams * n_cams;
+}
 
 constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) V*^-1(6) pad
 constexpr int kCPart = 112;  // per camera slot: U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2, pad
@@ -530,8 +541,9 @@ __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, in
 //                      B + B^T for the block rows of (c, c) (a point observed
 //                      twice by c); b = -Jc^T r - Jc^T u, g = -Jc^T r, diag U, cost;
 //   block c1 < c2:     S = -sum Y W^T (and its transpose) over the block rows.
-// Blocks without observations / common points are written as zeros, so sys
-// needs no separate clearing.
+// Dense layout: blocks without common points are written as zeros, so sys
+// needs no separate clearing.  Packed layout: each listed block is written
+// once, full 9x9, at sys + 81 * blk.
 __global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
   lm_wave_priority();
   __shared__ double red[kAsmWG / 81][kCPart];
@@ -541,7 +553,7 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
   const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
   const int C9 = 9 * p.n_cams;
   double* S = p.sys;
-  double* bvec = S + (size_t)C9 * C9;
+  double* bvec = S + sys_vec_off(p.n_cams, p.n_blocks);
   double* gvec = bvec + C9;
   double* diagU = gvec + C9;
   double* costc = diagU + C9;
@@ -555,7 +567,9 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
     sb[t] = 0.0;
   }
   __syncthreads();
-  if (t < 81) {
+  if (sys_packed(p.n_cams)) {
+    if (t < 81) S[(size_t)blk * 81 + t] = diag ? sh[t] - (sb[t] + sb[9 * (t % 9) + t / 9]) : -sb[t];
+  } else if (t < 81) {
     const int i = t / 9, j = t - 9 * (t / 9);
     if (diag) {
       S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = sh[t] - (sb[t] + sb[9 * j + i]);
@@ -573,73 +587,15 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
 }
 
 // ---------------------------------------------------------------- solve
-// Reduced camera system S x = b, S SPD (damped).  LDL^T right-looking
-// elimination on packed lower-triangle storage ordered column by column from
-// the RIGHT: column j occupies [poff(j), poff(j) + n - j) with
-// poff(j) = (n-1-j)(n-j)/2, so at step k the trailing elements still to update
-// (columns > k) are exactly the prefix [0, poff(k)).  Forward substitution is
-// fused into the elimination (b is carried as an extra column), leaving one
-// workgroup barrier per column; back substitution is blocked by 16 rows (the
-// triangle by one wave, the rectangle by all waves).
-constexpr int kSolveWG = 512;
-constexpr int kLdsMaxN = 120;   // packed S + (i,j) table + rhs fit in LDS
-constexpr int kSolveHdr = 32;   // doubles of LDS header in k_solve
-constexpr int kBackNB = 16;
-
-__device__ __forceinline__ int poff(int n, int j) { return ((n - 1 - j) * (n - j)) >> 1; }
-
-template <int NT>
-__device__ bool ldl_solve(double* P, uint32_t* tab, int n, double* b, int* fail) {
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  for (int k = 0; k < n; ++k) {
-    const int ck = poff(n, k);
-    const double akk = P[ck];
-    if (!(akk > 0.0) || !isfinite(akk)) {
-      if (t == 0) *fail = 1;
-      return false;  // uniform: every thread read the same pivot
-    }
-    const double inv = 1.0 / akk;
-    const double bk = b[k];
-    for (int e = t; e < ck; e += NT) {
-      const uint32_t ij = tab[e];
-      const int i = (int)(ij >> 16), j = (int)(ij & 0xFFFFu);
-      P[e] -= P[ck + i - k] * P[ck + j - k] * inv;
-    }
-    for (int i = k + 1 + t; i < n; i += NT) b[i] -= P[ck + i - k] * inv * bk;
-    __syncthreads();
-  }
-  // z = D^-1 y
-  for (int i = t; i < n; i += NT) b[i] /= P[poff(n, i)];
-  __syncthreads();
-  // back substitution L^T x = z, L[i][r] = P(i, r) / D_r; blocks from the bottom
-  for (int hi = n; hi > 0; hi -= kBackNB) {
-    const int lo = max(0, hi - kBackNB);
-    if (wid == 0) {
-      for (int k = hi - 1; k >= lo; --k) {
-        const double xk = b[k];  // final
-        const int r = lo + lane;
-        if (r < k) {
-          const int cr = poff(n, r);
-          b[r] -= P[cr + k - r] / P[cr] * xk;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      }
-    }
-    __syncthreads();
-    for (int r = t; r < lo; r += NT) {
-      const int cr = poff(n, r);
-      const double dr = P[cr];
-      double acc = 0.0;
-      for (int k = lo; k < hi; ++k) acc += P[cr + k - r] * b[k];
-      b[r] -= acc / dr;
-    }
-    __syncthreads();
-  }
-  return true;
-}
+// Reduced camera system S x = b, S SPD (damped).  Two solvers: k_solve_blk
+// (one workgroup, whole system in LDS/registers) for the local-BA window
+// (9C <= kLdsMaxN), and the tiled multi-workgroup Cholesky k_tl_* below for
+// larger systems.
+constexpr int kLdsMaxN = kDenseMaxN;  // k_solve_blk keeps the system in LDS up to 9C = 120
+constexpr int kSolveHdr = 32;   // doubles of LDS header in k_solve_blk
 
 // Inputs of the epilogue: camera gradient, Gram diagonal, live cameras and the
-// per-camera cost partials (global memory in k_solve, LDS copies prefetched at
+// per-camera cost partials (global memory in k_tl_epilogue, LDS copies prefetched at
 // kernel start in k_solve_blk so their latency is off the critical path).
 struct EpiSrc {
   const double *g, *dU, *cam, *costc;
@@ -670,41 +626,6 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
     state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : 1.0;
   }
-}
-
-// Large systems (9C > kLdsMaxN): packed factor in global memory (p.chol).
-__global__ __launch_bounds__(kSolveWG) void k_solve(slam_ba_problem p) {
-  lm_wave_priority();
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  double* red = lds;
-  int* fail_p = reinterpret_cast<int*>(lds + 16);
-  const int C9 = 9 * p.n_cams;
-  const int ne = C9 * (C9 + 1) / 2;
-  const double* S = p.sys;
-  const double* bvec = S + (size_t)C9 * C9;
-  const double* diagU = bvec + 2 * C9;
-  const double lam = p.state[SLAM_BA_ST_LAMBDA];
-  const int t = threadIdx.x;
-  double* P = p.chol;
-  double* x = p.chol + ne;
-  uint32_t* tab = reinterpret_cast<uint32_t*>(x + C9);
-  if (t == 0) *fail_p = 0;
-  for (int j = 0; j < C9; ++j) {
-    const int cj = poff(C9, j);
-    for (int i = j + t; i < C9; i += kSolveWG) {
-      double a = S[(size_t)i * C9 + j];
-      if (i == j) a += lam * clampd(diagU[i]);
-      P[cj + i - j] = a;
-      tab[cj + i - j] = ((uint32_t)i << 16) | (uint32_t)j;
-    }
-  }
-  for (int i = t; i < C9; i += kSolveWG) x[i] = bvec[i];
-  __syncthreads();
-  const bool ok = ldl_solve<kSolveWG>(P, tab, C9, x, fail_p);
-  __syncthreads();
-  const double* gvec = bvec + C9;
-  solve_epilogue(p, x, ok, red,
-                 EpiSrc{gvec, diagU, p.cams[cur_of(p.state)], gvec + 2 * C9});
 }
 
 // -DSLAM_SOLVE_PROFILE: phase timestamps (wall_clock64, 100 MHz) of k_solve_blk
@@ -1052,6 +973,383 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
   SOLVE_PROF_END();
 }
 
+// ---------------------------------------------------------------- tiled solve
+// Large reduced camera systems (9C > kLdsMaxN: the sharded C4 window, global
+// BA): right-looking blocked Cholesky LL^T over 64x64 f64 tiles, spread over
+// many workgroups, one launch per phase:
+//   k_tl_load         lower tile (I, J): damped S -> A (padded to N = 64T,
+//                     identity on the padded diagonal), b, tile-nonzero flags
+//   k_tl_panel(k)     WG per row tile I >= k: every WG factors A_kk (wave 0,
+//                     row i in lane i's registers, columns broadcast by
+//                     v_readlane) and inverts it the same way; WG I = k stores
+//                     L_kk^-1 (dinv[k]) and y_k = L_kk^-1 b_k; WG I > k
+//                     forms L_Ik = A_Ik L_kk^-T on the f64 matrix cores and
+//                     updates b_I -= L_Ik y_k (forward substitution fused)
+//   k_tl_update(k)    WG per trailing lower tile (I >= J > k) with both L_Ik
+//                     and L_Jk nonzero: A_IJ -= L_Ik L_Jk^T (MFMA f64 16x16x4)
+//   k_tl_back(k)      k = T-1 .. 0: x_k = L_kk^-T y_k; WG J < k: y_J -= L_kJ^T x_k
+//   k_tl_epilogue     1 WG: camera step, trial cameras, predicted reduction
+// Tiles that stay structurally zero (cameras without common points: banded
+// windows, long trajectories) are skipped: nz[I][J] is set by the load and by
+// any update that writes the tile, so fill-in is tracked exactly.
+constexpr int kTB = 64;        // tile edge
+constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
+
+struct TlLayout {  // doubles inside p.chol
+  int T, N;
+  long long a, dinv, b, y, x, nz, fail, total;
+  __host__ __device__ explicit TlLayout(int n) {
+    T = (n + kTB - 1) / kTB;
+    N = T * kTB;
+    a = 0;
+    dinv = a + (long long)N * N;         // T tiles L_kk^-1 (row-major 64x64 each)
+    b = dinv + (long long)N * kTB;
+    y = b + N;
+    x = y + N;
+    nz = x + N;                          // T*T bytes
+    fail = nz + ((long long)T * T + 7) / 8;
+    total = fail + 8;                    // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
+  }
+};
+
+// fragment-ordered LDS image of a 64x64 tile: the MFMA operand of sub-tile s,
+// k-step kk is 64 consecutive doubles (lane l: row 16s + (l & 15), col 4kk + (l >> 4))
+__device__ __forceinline__ int frag_idx(int r, int c) {
+  return ((((r >> 4) << 4) + (c >> 2)) << 6) + (r & 15) + ((c & 3) << 4);
+}
+
+__device__ __forceinline__ void tile_to_frag(const double* __restrict__ g, int ld, double* f,
+                                             int w = threadIdx.x >> 6, int nw = kTlWG / 64) {
+  // wave w of nw writes fragments (s, kk) = w, w + nw, ...: 64 consecutive doubles
+  // per fragment (conflict-free LDS stores); the global reads are 16 rows x 32 B
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, c = lane >> 4;
+#pragma unroll 4
+  for (int fi = w; fi < 64; fi += nw) {
+    const int sub = fi >> 4, kk = fi & 15;
+    f[(fi << 6) + lane] = g[(size_t)(16 * sub + r) * ld + 4 * kk + c];
+  }
+}
+
+// acc[s] (wave w) = rows 16w.., cols 16s.. of X Y^T, X and Y in fragment order
+__device__ __forceinline__ void gemm_xyT(const double* Xf, const double* Yf, d4 acc[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int kk = 0; kk < 16; ++kk) {
+    const double a = Xf[((w * 16 + kk) << 6) + lane];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + lane], acc[s], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayout& L) {
+  return *reinterpret_cast<const volatile int*>(p.chol + L.fail) != 0;
+}
+
+// Lower tile (I, J): zeros (identity on the padded diagonal), tile flag
+// cleared (diagonal tiles always live); the diagonal tiles also load b.
+__global__ __launch_bounds__(kTlWG) void k_tl_load(slam_ba_problem p) {
+  lm_wave_priority();
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const int idx = blockIdx.x;
+  int I = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
+  while ((I + 1) * (I + 2) / 2 <= idx) ++I;
+  while (I * (I + 1) / 2 > idx) --I;
+  const int J = idx - I * (I + 1) / 2;
+  double* A = p.chol + L.a;
+  for (int e = threadIdx.x; e < kTB * kTB; e += kTlWG) {
+    const int i = I * kTB + (e >> 6), j = J * kTB + (e & 63);
+    A[(size_t)i * L.N + j] = (i == j && i >= n) ? 1.0 : 0.0;
+  }
+  if (threadIdx.x == 0) reinterpret_cast<uint8_t*>(p.chol + L.nz)[I * L.T + J] = I == J ? 1 : 0;
+  if (I == J && threadIdx.x < kTB) {
+    const int i = I * kTB + threadIdx.x;
+    p.chol[L.b + i] = i < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + i] : 0.0;
+  }
+  if (idx == 0 && threadIdx.x == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 0;
+}
+
+// One workgroup per packed block (c1 <= c2) of sys: its 81 values into the
+// lower tiles of A (transposed for c1 < c2), mirrored inside diagonal tiles,
+// camera damping lam * clamp(diag U) on the diagonal; flags the tiles it hits.
+__global__ __launch_bounds__(128) void k_tl_scatter(slam_ba_problem p) {
+  lm_wave_priority();
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const int blk = blockIdx.x, t = threadIdx.x;
+  if (t >= 81) return;
+  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
+  const double* vec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
+  const int i = t / 9, j = t - 9 * (t / 9);
+  const int r = 9 * c1 + i, c = 9 * c2 + j;  // element (r, c) of S
+  double v = p.sys[(size_t)blk * 81 + t];
+  if (r == c) v += p.state[SLAM_BA_ST_LAMBDA] * clampd(vec[2 * n + r]);
+  double* A = p.chol + L.a;
+  uint8_t* nz = reinterpret_cast<uint8_t*>(p.chol + L.nz);
+  const int tr = r / kTB, tc = c / kTB;
+  if (r >= c || tr == tc) A[(size_t)r * L.N + c] = v;  // lower, or inside a diagonal tile
+  if (r > c && tr != tc) nz[tr * L.T + tc] = 1;        // a diagonal block across a tile edge
+  if (c1 != c2) {
+    A[(size_t)c * L.N + r] = v;                       // the mirrored element (lower)
+    if (tr != tc) nz[tc * L.T + tr] = 1;
+  }
+}
+
+// Cholesky factor and inverse of the symmetric 64x64 diagonal tile at Akk
+// (row-major, ld), split over two waves so each holds 64 doubles per lane:
+// wave 0 keeps row i of A (then of L) in lane i's v[], wave 1 keeps column i
+// of L^-1 (v = L^-1 e_i, right-looking forward substitution).  Per column j,
+// wave 0 takes the pivot by readlane and publishes column j of L and 1/L_jj in
+// cb[j & 1] (double-buffered); after one workgroup barrier both waves apply
+// it (trailing update of A / update of v).  Every wave of the workgroup must
+// call this (64 barriers).  Returns false (uniform over the workgroup) on a
+// non-positive or non-finite pivot; on return wave 1's v[] is column i of L^-1.
+constexpr int kCb = kTB + 2;  // per buffer: column of L, 1/L_jj, pad
+__device__ __forceinline__ bool tile_chol_inv(const double* __restrict__ Akk, int ld, double* cb,
+                                              int* okp, double v[kTB]) {
+  const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w == 0) {
+#pragma unroll
+    for (int m = 0; m < kTB; ++m) v[m] = Akk[(size_t)m * ld + i];  // A symmetric: coalesced
+  } else if (w == 1) {
+#pragma unroll
+    for (int m = 0; m < kTB; ++m) v[m] = m == i ? 1.0 : 0.0;
+  }
+  // wave 0 publishes column j of L for step j, computed with one column of
+  // lookahead: at step j it first finishes v[j + 1], derives column j + 1
+  // (pivot, scale) and publishes it into the other buffer before the rest of
+  // step j's FMAs, so the pivot's latency chain overlaps the trailing update.
+  bool ok = true;
+  auto pivot = [&](int j) {  // wave 0: v[j] of every lane is final
+    const double djj = readlane_d(v[j], j);
+    ok = ok && djj > 0.0 && djj < INFINITY;
+    // 1/sqrt by v_rsq_f64 + two Newton steps (full double precision)
+    double r = __builtin_amdgcn_rsq(djj);
+    const double h = 0.5 * djj;
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
+    v[j] = lij;
+    double* c = cb + (j & 1) * kCb;
+    c[i] = lij;
+    if (i == 0) c[kTB] = r;
+  };
+  if (w == 0) pivot(0);
+#pragma unroll
+  for (int j = 0; j < kTB; ++j) {
+    const double* c = cb + (j & 1) * kCb;
+    __syncthreads();  // column j published; column j - 1's buffer free again
+    if (w < 2) {
+      // all broadcast reads of the step issued before the FMAs (LDS latency paid once)
+      double cc[kTB];
+#pragma unroll
+      for (int l = (j + 1) & ~1; l < kTB; l += 2) {
+        const double2 c2 = *reinterpret_cast<const double2*>(c + l);
+        cc[l] = c2.x;
+        cc[l + 1] = c2.y;
+      }
+      double sj = v[j];
+      if (w == 1) {
+        sj *= c[kTB];
+        v[j] = sj;
+      }
+      if (j + 1 < kTB) {
+        v[j + 1] = __builtin_fma(-sj, cc[j + 1], v[j + 1]);
+        if (w == 0) pivot(j + 1);
+      }
+#pragma unroll
+      for (int l = j + 2; l < kTB; ++l) v[l] = __builtin_fma(-sj, cc[l], v[l]);
+    }
+  }
+  if (w == 0 && i == 0) *okp = ok ? 1 : 0;
+  __syncthreads();
+  return *okp != 0;
+}
+
+__global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_tl_panel(slam_ba_problem p, int k) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int I = k + blockIdx.x;
+  const uint8_t* nz = reinterpret_cast<const uint8_t*>(p.chol + L.nz);
+  if (I > k && !nz[I * L.T + k]) return;  // L_Ik = 0, b_I unchanged
+  __shared__ double Vf[kTB * kTB];        // L_kk^-1, fragment order
+  __shared__ double Xf[kTB * kTB];        // A_Ik, fragment order; then L_Ik row-major (stride 64)
+  __shared__ double Xf2[kTB * kTB];       // terms of y_k = L_kk^-1 b_k
+  __shared__ double yk[kTB];
+  __shared__ __attribute__((aligned(16))) double cb[2 * kCb];
+  __shared__ int okf;
+  double* A = p.chol + L.a;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double* Akk = A + (size_t)k * kTB * L.N + k * kTB;
+#ifdef SLAM_TL_PROFILE
+  const uint64_t pt0 = wall_clock64();
+#endif
+  double* AIk = A + (size_t)I * kTB * L.N + k * kTB;
+  if (I > k && w >= 2) tile_to_frag(AIk, L.N, Xf, w - 2, 2);  // waves 2, 3 (published by the factor's barriers)
+  // wave 1, lane c ends with column c of L_kk^-1 (x[m] = Linv[m][c])
+  double x[kTB];
+  const bool ok = tile_chol_inv(Akk, L.N, cb, &okf, x);
+  if (w == 1) {
+    const double bc = p.chol[L.b + k * kTB + lane];
+    if (I == k) {
+      double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) Vkk[m * kTB + lane] = x[m];
+      // y_k[m] = sum_c Linv[m][c] b_k[c]: lane c's terms, summed across the wave in LDS
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) Vf[m * kTB + lane] = x[m] * bc;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double y = 0.0;
+      for (int c = 0; c < kTB; ++c) y += Vf[lane * kTB + ((c + lane) & 63)];
+      p.chol[L.y + k * kTB + lane] = y;
+      if (!ok && lane == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 1;
+    } else {
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) {
+        Vf[frag_idx(m, lane)] = x[m];
+        Xf2[m * kTB + lane] = x[m] * bc;  // y_k terms (Xf2: scratch rows of the yk sum)
+      }
+    }
+  }
+  if (I == k || !ok) return;
+  __syncthreads();
+  if (t < kTB) {
+    double y = 0.0;
+    for (int c = 0; c < kTB; ++c) y += Xf2[t * kTB + ((c + t) & 63)];
+    yk[t] = y;
+  }
+#ifdef SLAM_TL_PROFILE
+  const uint64_t pt1 = wall_clock64();
+#endif
+  d4 acc[4];
+  gemm_xyT(Xf, Vf, acc);  // L_Ik = A_Ik (L_kk^-1)^T
+  __syncthreads();        // Xf free
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = w * 16 + (lane >> 4) + 4 * r, col = s * 16 + (lane & 15);
+      AIk[(size_t)row * L.N + col] = acc[s][r];
+      Xf[row * kTB + col] = acc[s][r];
+    }
+  __syncthreads();
+  if (t < kTB) {
+    double s = 0.0;
+    for (int m = 0; m < kTB; ++m) s = __builtin_fma(Xf[t * kTB + ((m + t) & 63)], yk[(m + t) & 63], s);
+    p.chol[L.b + I * kTB + t] -= s;
+  }
+#ifdef SLAM_TL_PROFILE
+  // WG I = k + 1 of step 0, wall clock (100 MHz) -> ns: start -> factor done, -> end
+  if (k == 0 && I == 1 && t == 0) {
+    const uint64_t pt3 = wall_clock64();
+    p.chol[L.fail + 1] = 10.0 * (double)(pt1 - pt0);
+    p.chol[L.fail + 2] = 10.0 * (double)(pt3 - pt1);
+  }
+#endif
+}
+
+__global__ __launch_bounds__(kTlWG) void k_tl_update(slam_ba_problem p, int k) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int idx = blockIdx.x;
+  int Ii = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
+  while ((Ii + 1) * (Ii + 2) / 2 <= idx) ++Ii;
+  while (Ii * (Ii + 1) / 2 > idx) --Ii;
+  const int I = k + 1 + Ii, J = k + 1 + (idx - Ii * (Ii + 1) / 2);
+  uint8_t* nz = reinterpret_cast<uint8_t*>(p.chol + L.nz);
+  if (!nz[I * L.T + k] || !nz[J * L.T + k]) return;
+  __shared__ double Xf[kTB * kTB], Yf[kTB * kTB];
+  double* A = p.chol + L.a;
+  tile_to_frag(A + (size_t)I * kTB * L.N + k * kTB, L.N, Xf);
+  tile_to_frag(A + (size_t)J * kTB * L.N + k * kTB, L.N, Yf);
+  __syncthreads();
+  d4 acc[4];
+  gemm_xyT(Xf, Yf, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* AIJ = A + (size_t)I * kTB * L.N + J * kTB;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = w * 16 + (lane >> 4) + 4 * r, col = s * 16 + (lane & 15);
+      AIJ[(size_t)row * L.N + col] -= acc[s][r];
+    }
+  if (threadIdx.x == 0) nz[I * L.T + J] = 1;
+}
+
+// x_k = L_kk^-T y_k (every WG, from the stored inverse); WG 0 stores it, WG j > 0
+// updates y_J -= L_kJ^T x_k for J = j - 1 < k.
+__global__ __launch_bounds__(kTlWG) void k_tl_back(slam_ba_problem p, int k) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int J = (int)blockIdx.x - 1;
+  const uint8_t* nz = reinterpret_cast<const uint8_t*>(p.chol + L.nz);
+  if (J >= 0 && !nz[k * L.T + J]) return;
+  __shared__ double xk[kTB];
+  __shared__ double part[4][kTB];
+  const double* A = p.chol + L.a;
+  const double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;  // L_kk^-1
+  const int t = threadIdx.x, c = t & 63, q = t >> 6;
+  {
+    // x_k[c] = sum_m Linv[m][c] y_k[m]: thread (q, c) sums m in [16q, 16q + 16)
+    double s = 0.0;
+    for (int m = 16 * q; m < 16 * q + 16; ++m)
+      s = __builtin_fma(Vkk[m * kTB + c], p.chol[L.y + k * kTB + m], s);
+    part[q][c] = s;
+  }
+  __syncthreads();
+  if (t < kTB) xk[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+  __syncthreads();
+  if (J < 0) {
+    if (t < kTB) p.chol[L.x + k * kTB + t] = xk[t];
+    return;
+  }
+  // y_J[c] -= sum_m L_kJ[m][c] x_k[m]
+  const double* LkJ = A + (size_t)k * kTB * L.N + J * kTB;
+  double s = 0.0;
+  for (int m = 16 * q; m < 16 * q + 16; ++m) s = __builtin_fma(LkJ[(size_t)m * L.N + c], xk[m], s);
+  part[q][c] = s;
+  __syncthreads();
+  if (t < kTB) p.chol[L.y + J * kTB + t] -= ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+}
+
+__global__ __launch_bounds__(1024) void k_tl_epilogue(slam_ba_problem p) {
+  lm_wave_priority();
+  __shared__ double red[32];
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const bool ok = !tl_failed(p, L);
+  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
+  const double* gvec = bvec + n;
+  solve_epilogue(p, p.chol + L.x, ok, red,
+                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+}
+
+static void tl_solve(const slam_ba_problem& p, hipStream_t s) {
+  const TlLayout L(9 * p.n_cams);
+  const int T = L.T;
+  k_tl_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p);
+  k_tl_scatter<<<p.n_blocks, 128, 0, s>>>(p);
+  for (int k = 0; k < T; ++k) {
+    k_tl_panel<<<T - k, kTlWG, 0, s>>>(p, k);
+    const int m = T - 1 - k;
+    if (m > 0) k_tl_update<<<m * (m + 1) / 2, kTlWG, 0, s>>>(p, k);
+  }
+  // y of the last tile is final after its panel; the back pass walks up
+  for (int k = T - 1; k >= 0; --k) k_tl_back<<<k + 1, kTlWG, 0, s>>>(p, k);
+  k_tl_epilogue<<<1, 1024, 0, s>>>(p);
+}
+
 __device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
 
 // Back substitution + trial cost, one workgroup per point group:
@@ -1210,9 +1508,12 @@ int check_problem(const slam_ba_problem* p) {
                    p->small && p->red_part && p->delta_c,
                "slam_ba: null buffer");
   SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
-  SLAM_REQUIRE(p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
-               "slam_ba: n_blocks must list all C(C+1)/2 upper blocks");
-  SLAM_REQUIRE(9 * p->n_cams <= kLdsMaxN || p->chol != nullptr,
+  SLAM_REQUIRE(sys_packed(p->n_cams) ? (p->n_blocks >= p->n_cams &&
+                                        p->n_blocks <= p->n_cams * (p->n_cams + 1) / 2)
+                                     : p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
+               "slam_ba: n_blocks must list all C(C+1)/2 upper blocks (9C <= %d) or the "
+               "diagonal and every block with common points (packed)", kDenseMaxN);
+  SLAM_REQUIRE(!sys_packed(p->n_cams) || p->chol != nullptr,
                "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
                kLdsMaxN);
   return SLAM_OK;
@@ -1223,14 +1524,12 @@ int check_problem(const slam_ba_problem* p) {
 extern "C" int slam_ba_red_slots(int n_grps) { return 2 * n_grps; }
 
 extern "C" long long slam_ba_chol_len(int n_cams) {
-  const long long c9 = 9ll * n_cams;
-  const long long ne = c9 * (c9 + 1) / 2;
-  return ne + c9 + (ne + 1) / 2;  // packed factor + rhs + (i,j) table (u32)
+  return TlLayout(9 * n_cams).total;  // tiled factor workspace (9C > kLdsMaxN)
 }
 
-extern "C" long long slam_ba_sys_len(int n_cams) {
+extern "C" long long slam_ba_sys_len(int n_cams, int n_blocks) {
   const long long c9 = 9ll * n_cams;
-  return c9 * c9 + 3 * c9 + n_cams;
+  return sys_vec_off(n_cams, n_blocks) + 3 * c9 + n_cams;
 }
 
 extern "C" int slam_ba_residual(const double* d_cams, const double* d_pts,
@@ -1284,12 +1583,12 @@ static int solve_step(const slam_ba_problem* prob, bool fuse_decide, void* strea
   const slam_ba_problem& p = *prob;
   hipStream_t s = slam::as_stream(stream);
   const int C9 = 9 * p.n_cams;
-  if (C9 <= kLdsMaxN) {
+  if (!sys_packed(p.n_cams)) {
     k_solve_blk<<<1, kBlkWG, sizeof(double) * BlkLds(C9).total, s>>>(p);
     SLAM_LAUNCHED("k_solve_blk");
   } else {
-    k_solve<<<1, kSolveWG, sizeof(double) * kSolveHdr, s>>>(p);
-    SLAM_LAUNCHED("k_solve");
+    tl_solve(p, s);
+    SLAM_LAUNCHED("k_tl_*");
   }
   if (fuse_decide)
     k_back_trial<true><<<p.n_grps, kGrp, 0, s>>>(p, p.red_part);

@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libslam355.so")
+# SLAM355_LIB: an instrumented build of the same library (profiling scripts only)
+LIB_PATH = os.environ.get("SLAM355_LIB") or os.path.join(_HERE, "libslam355.so")
 
 c_int = ctypes.c_int
 c_double = ctypes.c_double
@@ -70,16 +71,19 @@ SIGNATURES = {
     "slam_ba_residual": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p],
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_ba_red_slots": [c_int],
-    "slam_ba_sys_len": [c_int],
+    "slam_ba_sys_len": [c_int, c_int],
     "slam_ba_chol_len": [c_int],
     "slam_ba_build_system": [_PROB, c_p],
     "slam_ba_solve_step": [_PROB, c_p],
     "slam_ba_decide": [_PROB, c_p],
     "slam_ba_iterate": [_PROB, c_int, c_p],
     "slam_ba_reset": [_PROB, c_double, c_p],
+    "slam_pose_chain_objective": [c_p, c_int, c_int, c_int, c_p, c_p],
+    "slam_pose_chain_workspace_len": [c_int],
+    "slam_pose_chain_lm": [c_p, c_int, c_int, c_int, c_double, c_p, c_p],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
-            "slam_ba_chol_len": ctypes.c_longlong}
+            "slam_ba_chol_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}
 
 
 class SlamError(RuntimeError):

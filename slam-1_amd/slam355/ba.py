@@ -24,7 +24,7 @@ from ._lib import BAProblemStruct as _Prob
 ST = dict(LAMBDA=0, NU=1, COST=2, COST_NEW=3, PRED=4, RHO=5, ACCEPTED=6, CUR=7, ITERS=8,
           NACCEPT=9, PRED_CAM=10, CHOL_FAIL=11)
 N_STATE = 16
-LDS_MAX_N = 120  # k_solve keeps S in LDS up to 9C <= 120
+LDS_MAX_N = 120  # k_solve_blk keeps S in LDS up to 9C <= 120 (dense sys); tiled solver above
 
 
 def _check_indices(n_cams, n_pts, cam_idx, pt_idx, qs):
@@ -72,12 +72,55 @@ def block_index(c1, c2, n_cams):
     return c1 * n_cams - c1 * (c1 - 1) // 2 + (np.asarray(c2, np.int64) - c1)
 
 
-def plan(n_cams, n_pts, cam_idx, pt_idx):
+def packed(n_cams):
+    """True when the reduced camera system goes to the tiled solver in the packed
+    block layout (9C > 120; csrc/ba.hip sys_packed)."""
+    return 9 * n_cams > LDS_MAX_N
+
+
+def upper_blocks(n_cams, cam_idx, pt_idx):
+    """Dense upper-block indices (np.triu_indices order) of the diagonal and of
+    every camera pair with a common point: the packed block list.  Ranks of a
+    sharded problem pass the list of the GLOBAL problem to BAProblem so their
+    packed systems line up for the all-reduce."""
+    cam_idx = np.asarray(cam_idx, np.int64).ravel()
+    pt_idx = np.asarray(pt_idx, np.int64).ravel()
+    o1, o2 = _pairs_by_point(cam_idx, pt_idx)
+    c1, c2 = np.minimum(cam_idx[o1], cam_idx[o2]), np.maximum(cam_idx[o1], cam_idx[o2])
+    diag = np.arange(n_cams)
+    return np.unique(np.concatenate([block_index(diag, diag, n_cams), block_index(c1, c2, n_cams)]))
+
+
+def _pairs_by_point(cam_idx, pt_idx):
+    """Observation pairs (o1 < o2 in (point, camera) order) of the same point."""
+    order = np.lexsort((cam_idx, pt_idx))
+    obs_pt = pt_idx[order]
+    n_pts = int(obs_pt.max()) + 1 if len(obs_pt) else 0
+    pt_ptr = np.zeros(n_pts + 1, np.int64)
+    np.cumsum(np.bincount(obs_pt, minlength=n_pts), out=pt_ptr[1:])
+    cnt = np.diff(pt_ptr)
+    o1s, o2s = [], []
+    for n in np.unique(cnt):
+        if n < 2:
+            continue
+        base = pt_ptr[np.nonzero(cnt == n)[0]][:, None]
+        ii, jj = np.triu_indices(n, 1)
+        o1s.append((base + ii[None]).ravel())
+        o2s.append((base + jj[None]).ravel())
+    o1 = np.concatenate(o1s) if o1s else np.zeros(0, np.int64)
+    o2 = np.concatenate(o2s) if o2s else np.zeros(0, np.int64)
+    return order[o1], order[o2]
+
+
+def plan(n_cams, n_pts, cam_idx, pt_idx, block_list=None):
     """Index tables for the LM kernels (host numpy, once per problem structure).
 
     Observations are sorted by (point, camera) and cut into point groups
     (whole points, <= GROUP_OBS observations).  Each group gets
       camera slots (g, c): its observations of camera c (group-local indices);
+    block_list (packed layout only, 9C > 120): dense upper-block indices of the
+      blocks to assemble (default: upper_blocks of this problem); every block
+      with a common point here must be listed.
       block slots (g, c1 <= c2): its points' observation pairs o1 < o2 (cameras
         c1 <= c2; c1 == c2 only for a point observed twice by one camera);
     and each slot's partial row sits in camera- / block-major order (rows of
@@ -123,6 +166,16 @@ def plan(n_cams, n_pts, cam_idx, pt_idx):
     o2 = np.concatenate(o2s) if o2s else np.zeros(0, np.int64)
     NB = C * (C + 1) // 2
     blk = block_index(obs_cam[o1], obs_cam[o2], C)
+    if packed(C):
+        diag = np.arange(C)
+        own = np.unique(np.concatenate([block_index(diag, diag, C), blk]))
+        blist = own if block_list is None else np.unique(np.asarray(block_list, np.int64))
+        if block_list is not None and not np.all(np.isin(own, blist)):
+            raise ValueError("block_list misses a camera block with common points")
+        blk = np.searchsorted(blist, blk)
+        NB = len(blist)
+    else:
+        blist = np.arange(NB)
     bk = obs_grp[o1] * NB + blk
     sp = np.lexsort((o2, o1, bk))
     bkey, bstart = np.unique(bk[sp], return_index=True)
@@ -137,6 +190,7 @@ def plan(n_cams, n_pts, cam_idx, pt_idx):
     np.cumsum(np.bincount(bslot_blk, minlength=NB), out=blk_bslot_ptr[1:])
 
     c1, c2 = np.triu_indices(C)
+    c1, c2 = c1[blist], c2[blist]
     i32 = lambda a: np.asarray(a, np.int32)  # noqa: E731
     return dict(
         order=order, obs_cam=i32(obs_cam), obs_pt=i32(obs_pt), pt_ptr=i32(pt_ptr),
@@ -148,6 +202,31 @@ def plan(n_cams, n_pts, cam_idx, pt_idx):
         n_obs=O)
 
 
+def tiled_solve_flops(n_cams, blocks, tb=64):
+    """Flops of the tiled Cholesky (csrc/ba.hip k_tl_*) for a packed block list
+    [n_blocks, 2]: the 64x64 tiles it factors, solves and updates, with the
+    structural fill-in tracked as the kernels track it (zero tiles skipped)."""
+    n = 9 * n_cams
+    T = (n + tb - 1) // tb
+    nz = np.eye(T, dtype=bool)
+    b = np.asarray(blocks, np.int64).reshape(-1, 2)
+    i, j = np.meshgrid(np.arange(9), np.arange(9), indexing="ij")
+    r = (9 * b[:, 0, None, None] + i[None]).ravel() // tb
+    c = (9 * b[:, 1, None, None] + j[None]).ravel() // tb
+    nz[np.maximum(r, c), np.minimum(r, c)] = True
+    flops = 0.0
+    g = 2.0 * tb ** 3
+    for k in range(T):
+        flops += tb ** 3 / 3.0 * 2  # factor + inverse of the diagonal tile
+        rows = k + 1 + np.flatnonzero(nz[k + 1:, k])
+        m = len(rows)
+        flops += m * g + m * (m + 1) / 2 * g  # panel GEMMs + trailing updates
+        if m:
+            ii, jj = np.tril_indices(m)
+            nz[rows[ii], rows[jj]] = True
+    return flops
+
+
 _INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
                  "cslot_obs_ptr", "cslot_obs", "grp_bslot", "bslot_blk", "bslot_pair_ptr",
                  "bslot_pairs", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
@@ -157,13 +236,14 @@ _INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_c
 class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
-    def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None):
+    def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
+                 block_list=None):
         dev = require_gpu()
         cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
         C, P = len(cams), len(pts)
         cam_idx, pt_idx, qs = _check_indices(C, P, cam_idx, pt_idx, qs)
-        pl = plan(C, P, cam_idx, pt_idx)
+        pl = plan(C, P, cam_idx, pt_idx, block_list)
         self.plan = pl
         self.C, self.P, self.O = C, P, pl["n_obs"]
         self.stream = stream
@@ -182,7 +262,7 @@ class BAProblem:
         t["ptdata"] = z(P * 16)
         t["cpart"] = z(n_cs * 112)
         t["bpart"] = z(n_bs * 81)
-        self.sys_len = int(_lib.lib.slam_ba_sys_len(C))
+        self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
         t["delta_c"] = z(C9)

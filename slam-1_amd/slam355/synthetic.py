@@ -39,7 +39,14 @@ def _rodrigues(r):
 
 def bal_project(X, cams):
     """BAL projection (camera looks down -z, radial k1/k2) for input synthesis."""
-    R = np.stack([_rodrigues(w) for w in cams[:, :3]])
+    w = cams[:, :3]
+    th = np.linalg.norm(w, axis=1)
+    k = np.divide(w, th[:, None], out=np.zeros_like(w), where=th[:, None] > 0)
+    K = np.zeros((len(w), 3, 3))
+    K[:, 0, 1], K[:, 0, 2], K[:, 1, 2] = -k[:, 2], k[:, 1], -k[:, 0]
+    K[:, 1, 0], K[:, 2, 0], K[:, 2, 1] = k[:, 2], -k[:, 1], k[:, 0]
+    R = (np.eye(3)[None] + np.sin(th)[:, None, None] * K
+         + (1 - np.cos(th))[:, None, None] * (K @ K))
     P = np.einsum("oij,oj->oi", R, X) + cams[:, 3:6]
     p = -P[:, :2] / P[:, 2:3]
     n = np.sum(p * p, axis=1)
@@ -66,6 +73,51 @@ def ba_problem(rng, n_cams, n_pts, obs_per_pt, f=716.8, noise=0.5):
     X = C[anchor] + np.stack([rng.uniform(-0.4, 0.4, n_pts) * depth,
                               rng.uniform(-0.25, 0.25, n_pts) * depth, -depth], 1)
     cam_idx = (anchor[:, None] + np.arange(obs_per_pt)[None, :]).ravel()
+    pt_idx = np.repeat(np.arange(n_pts), obs_per_pt)
+    perm = rng.permutation(len(cam_idx))
+    cam_idx, pt_idx = cam_idx[perm], pt_idx[perm]
+    qs = bal_project(X[pt_idx], cams[cam_idx]) + rng.normal(0, noise, (len(cam_idx), 2))
+    return cams, X, cam_idx.astype(np.int64), pt_idx.astype(np.int64), qs
+
+
+def _log_so3(R):
+    """Rotation vector of a rotation matrix (angle < pi)."""
+    c = np.clip((np.trace(R) - 1.0) * 0.5, -1.0, 1.0)
+    th = np.arccos(c)
+    w = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return w * 0.5 if th < 1e-12 else w * (th / (2.0 * np.sin(th)))
+
+
+def ba_problem_loop(rng, n_cams, n_pts, obs_per_pt, f=716.8, noise=0.5, step=1.0):
+    """Loop-closure global-BA problem (BASELINE config 5 shape): keyframes `step`
+    m apart on a closed circular trajectory (the reference closes loops between
+    the last and first frames, main.py:100-118), each landmark seen by
+    `obs_per_pt` consecutive keyframes from its anchor, modulo n_cams, so the
+    tracks of the last keyframes continue into the first ones (the loop-closure
+    camera blocks of S).  BAL convention (camera looks down -z).  Returns the
+    same tuple as ba_problem."""
+    R0 = n_cams * step / (2.0 * np.pi)
+    phi = 2.0 * np.pi * np.arange(n_cams) / n_cams
+    centers = np.stack([R0 * np.cos(phi), rng.normal(0, 0.05, n_cams), R0 * np.sin(phi)], 1)
+    fwd = np.stack([-np.sin(phi), np.zeros(n_cams), np.cos(phi)], 1)
+    cams = np.zeros((n_cams, 9))
+    Rs = np.empty((n_cams, 3, 3))
+    for c in range(n_cams):
+        z = -fwd[c]
+        y = np.array([0.0, 1.0, 0.0])
+        x = np.cross(y, z)
+        R = np.stack([x, y, z]) @ _rodrigues(rng.normal(0, 0.02, 3)).T
+        Rs[c] = R
+        cams[c, :3] = _log_so3(R)
+        cams[c, 3:6] = -R @ centers[c]
+        cams[c, 6] = f
+    anchor = rng.integers(0, n_cams, n_pts)
+    depth = rng.uniform(8.0, 60.0, n_pts)
+    side = np.cross(np.array([0.0, 1.0, 0.0]), -fwd[anchor])
+    X = (centers[anchor] + fwd[anchor] * depth[:, None]
+         + side * (rng.uniform(-0.4, 0.4, n_pts) * depth)[:, None]
+         + np.array([0.0, 1.0, 0.0]) * (rng.uniform(-0.25, 0.25, n_pts) * depth)[:, None])
+    cam_idx = ((anchor[:, None] + np.arange(obs_per_pt)[None, :]) % n_cams).ravel()
     pt_idx = np.repeat(np.arange(n_pts), obs_per_pt)
     perm = rng.permutation(len(cam_idx))
     cam_idx, pt_idx = cam_idx[perm], pt_idx[perm]

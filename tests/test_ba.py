@@ -254,7 +254,7 @@ def test_gpu_solver_reaches_reference_optimum(g):
 @pytest.mark.gpu
 @pytest.mark.parametrize("C,P,k", [(10, 5000, 6), (13, 2500, 5), (16, 3000, 5)])
 def test_gpu_local_ba_config3_converges(C, P, k):
-    """C3 shape (10 KF x 5k pts x 30k obs) and a 9C > 120 case (global-memory Cholesky)."""
+    """C3 shape (10 KF x 5k pts x 30k obs) and 9C > 120 cases (tiled multi-workgroup Cholesky)."""
     from slam355 import ba
 
     cams, pts, ci, pi, qs = make_problem(5 + C, C, P, k)
@@ -274,3 +274,55 @@ def test_gpu_local_ba_config3_converges(C, P, k):
     gc, gp = prob.params()
     r = oba.residual_and_jacobian(gc, gp, ci, pi, qs)[0]
     assert abs(0.5 * float(np.sum(r * r)) - st["COST"]) <= 1e-8 * st["COST"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,P,k", [(14, 400, 4), (40, 1500, 5), (130, 3000, 6)])
+def test_gpu_tiled_solver_iterates_match_oracle(C, P, k):
+    """9C > 120: the reduced camera system goes through the tiled Cholesky
+    (k_tl_*; 2, 6 and 19 tiles of 64).  The 130-camera trajectory window is
+    block-banded (points seen by 6 consecutive keyframes), so most tiles stay
+    structurally zero and are skipped.  LM iterates equal the oracle's Schur LM."""
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(11 + C, C, P, k)
+    rng = np.random.default_rng(C)
+    cams0 = cams.copy()
+    cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
+    pts0 = pts + rng.normal(0, 0.05, pts.shape)
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
+    st = oba.LMState(1e-4)
+    oc, op = cams0.copy(), pts0.copy()
+    pairs = oba._obs_pairs(ci, pi)
+    for it in range(5):
+        prob.iterate(1)
+        oc, op, info = oba.lm_iteration_schur(oc, op, ci, pi, qs, st, pairs)
+        s = prob.state()
+        assert s["CHOL_FAIL"] == 0.0, it
+        assert bool(s["ACCEPTED"]) == bool(info["accepted"]), it
+        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-8 * info["cost_new"] + 1e-12, it
+        assert abs(s["LAMBDA"] - st.lam) <= 1e-6 * st.lam, it
+        gc, gp = prob.params()
+        assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9), it
+        assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), it
+
+
+def test_planner_packed_block_list():
+    """9C > 120: the plan lists only the diagonal and the camera pairs with a
+    common point (the packed sys layout); an explicit global list is honoured
+    and a list that misses a local block is rejected."""
+    from slam355 import ba
+
+    C = 20
+    cams, pts, ci, pi, qs = make_problem(3, C, 300, 4)
+    pl = ba.plan(C, len(pts), ci, pi)
+    blocks = {tuple(b) for b in pl["blocks"]}
+    pairs = {(min(a, b), max(a, b)) for p in range(len(pts))
+             for a in ci[pi == p] for b in ci[pi == p]}
+    assert blocks == pairs | {(c, c) for c in range(C)}
+    full = ba.block_index(*np.triu_indices(C), C)
+    pl2 = ba.plan(C, len(pts), ci, pi, block_list=full)
+    assert len(pl2["blocks"]) == C * (C + 1) // 2
+    with pytest.raises(ValueError):
+        ba.plan(C, len(pts), ci, pi, block_list=ba.block_index(np.arange(C), np.arange(C), C))
