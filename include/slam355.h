@@ -344,13 +344,42 @@ int slam_pose_chain_objective(const double* params, int n_vec, int n_frames, int
 /* Doubles of the LM workspace for m frames (the live parameters sit at its
  * start: ws[0 .. 6m)). */
 long long slam_pose_chain_workspace_len(int n_frames);
-/* n_iter Levenberg iterations on ws[0 .. 6m) in place (one workgroup, no host
- * round trip).  lam_rel0 > 0: start from lam_rel0 * max diag(J J^T); else from
- * state[2].  state[8]: cost0, cost, lambda, nu, iterations, accepted, rho,
- * stopped.  Replaces least_squares(objective, ..., method='trf') of
- * bundle_adjustment_with_sparsity, BundleAdjustment.py:173-183. */
-int slam_pose_chain_lm(double* ws, int n_frames, int loop, int n_iter, double lam_rel0,
-                       double* state, void* stream);
+/* scipy's TRF (least_squares method='trf', x_scale='jac', 'exact' trust-region
+ * subproblem) on ws[0 .. 6m) in place, one workgroup, at most max_iter outer
+ * iterations per call (first != 0 starts the run: scale, Delta; else it
+ * resumes from state).  Analytic Jacobian; the subproblem's SVD solves are
+ * replaced by the O(m) arrow-structured dual system.  state[16]: cost0, cost,
+ * nfev, njev, status (0 running, 1 gtol, 2 ftol, 3 xtol, 4 ftol+xtol), Delta,
+ * alpha, iterations.  Replaces least_squares(objective, ..., method='trf') of
+ * bundle_adjustment_with_sparsity, BundleAdjustment.py:179-183. */
+int slam_pose_chain_trf(double* ws, int n_frames, int loop, int max_iter, int first, double ftol,
+                        double xtol, double gtol, int max_nfev, double* state, void* stream);
+
+/* ------------------------------------------------------------------ BoW
+ * Bag-of-words place recognition (bag_of_words.py).  Descriptors are ORB rows
+ * (32 bytes, used as float64 features as scikit-learn converts them); K <= 128
+ * clusters, centres [K][32] f64.  All pointers are device pointers. */
+
+/* Labels (nearest centre, argmin |c|^2 - 2 x.c, first index on ties) and label
+ * histograms hist[n_img][K] of desc[n_img][cap][32] with count[n_img] rows
+ * each (count null: n_each rows each); labels may be null.  Replaces
+ * BoW.hist (bag_of_words.py:24-27: kmeans.predict + np.histogram). */
+int slam_bow_histograms(const uint8_t* desc, const int32_t* count, int n_each, int n_img, int cap,
+                        const double* centers, int n_clusters, int32_t* labels, int32_t* hist,
+                        void* stream);
+/* For each query histogram q: argmin / min over database rows [0, n_db[q]) of
+ * sum 2 (x - y)^2 / max(1, x + y) (numpy's summation order; first index on
+ * ties; n_db <= 0 -> (-1, -1)).  Replaces the chi2 loop + np.argmin/np.min of
+ * BoW.predict_previous / predict (bag_of_words.py:30-56). */
+int slam_bow_query(const int32_t* qhist, int n_query, const int32_t* db, const int32_t* n_db,
+                   int n_clusters, int32_t* idx, double* val, void* stream);
+/* n_iter Lloyd iterations (E-step, then centres = means; an empty cluster keeps
+ * its centre) on X[n_points][32] in place on centers (centers_tmp: [K][32]
+ * scratch), then labels of the final centres; shift[K] (optional) = squared
+ * centre shift of the last iteration.  Replaces KMeans.fit's Lloyd loop
+ * (bag_of_words.py:20). */
+int slam_bow_lloyd(const uint8_t* X, int n_points, double* centers, double* centers_tmp,
+                   int n_clusters, int n_iter, int32_t* labels, double* shift, void* stream);
 
 #ifdef __cplusplus
 }

@@ -79,8 +79,12 @@ SIGNATURES = {
     "slam_ba_iterate": [_PROB, c_int, c_p],
     "slam_ba_reset": [_PROB, c_double, c_p],
     "slam_pose_chain_objective": [c_p, c_int, c_int, c_int, c_p, c_p],
+    "slam_bow_histograms": [c_p, c_p, c_int, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
+    "slam_bow_query": [c_p, c_int, c_p, c_p, c_int, c_p, c_p, c_p],
+    "slam_bow_lloyd": [c_p, c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_pose_chain_workspace_len": [c_int],
-    "slam_pose_chain_lm": [c_p, c_int, c_int, c_int, c_double, c_p, c_p],
+    "slam_pose_chain_trf": [c_p, c_int, c_int, c_int, c_int, c_double, c_double, c_double, c_int,
+                            c_p, c_p],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
             "slam_ba_chol_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}
