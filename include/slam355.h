@@ -381,6 +381,86 @@ int slam_bow_query(const int32_t* qhist, int n_query, const int32_t* db, const i
 int slam_bow_lloyd(const uint8_t* X, int n_points, double* centers, double* centers_tmp,
                    int n_clusters, int n_iter, int32_t* labels, double* shift, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Alternative stereo-VO front end: FAST on tiles,
+ * pyramidal Lucas-Kanade, semi-global block matching, disparity lookup and
+ * float32 triangulation (csrc/vofront.hip; semantics in oracle/vofront.c).
+ * ------------------------------------------------------------------------- */
+
+/* Workspace bytes of slam_fast_tiles. */
+int slam_fast_tiles_workspace_bytes(int batch, int H, int W, int tile_h, int tile_w, int per_tile,
+                                    size_t* bytes);
+/* FAST-9/16 (threshold, strict 3x3 NMS) on every tile_h x tile_w tile of
+ * img[batch][H][stride]; per tile the detection-order corners, or the first
+ * per_tile of a stable sort by response when there are more; tiles row-major.
+ * kp[batch][kp_cap][3] f32 (x, y, response), count[batch] (-n-1 if > kp_cap).
+ * Replaces VisualOdometry.get_tiled_keypoints (visual_odometry.py:84-96:
+ * cv2.FastFeatureDetector_create().detect per tile, sorted(...)[:10]). */
+int slam_fast_tiles(const uint8_t* d_img, int batch, int H, int W, int stride, int tile_h,
+                    int tile_w, int threshold, int per_tile, void* d_ws, size_t ws_bytes,
+                    float* d_kp, int32_t* d_count, int kp_cap, void* stream);
+
+/* Levels actually used and bytes of one image's LK pyramid (the derivative
+ * buffer of one image holds img_bytes int16x2 elements). */
+int slam_lk_pyramid_layout(int H, int W, int win, int max_level, int* nlev, size_t* img_bytes);
+/* Pyramids (pyrDown levels with a reflect-101 border of win+1) of n_img images
+ * into d_pyr[n_img][img_bytes]; if d_deriv is not null, also their Scharr
+ * derivatives (zero border) into d_deriv[n_img][img_bytes][2].  The pyramid
+ * half of cv2.calcOpticalFlowPyrLK (visual_odometry.py:100, keypoint.py:19). */
+int slam_lk_build_pyramids(const uint8_t* d_img, int n_img, int H, int W, int stride, int win,
+                           int max_level, uint8_t* d_pyr, int16_t* d_deriv, void* stream);
+/* Pyramidal LK for pair b = (prev image b * pair_stride_imgs of d_prev_pyr /
+ * d_prev_deriv, next image b * pair_stride_imgs of d_next_pyr): points
+ * pts[batch][cap][pts_stride] (x, y first), npts[batch] ->
+ * out[batch][cap][2], status[batch][cap], err[batch][cap] (mean |diff|).
+ * Replaces cv2.calcOpticalFlowPyrLK(img1, img2, pts, None, winSize=(win,win),
+ * maxLevel, criteria=(EPS|COUNT, max_count, eps)) (visual_odometry.py:26-29,100). */
+int slam_lk_track(const uint8_t* d_prev_pyr, const int16_t* d_prev_deriv, const uint8_t* d_next_pyr,
+                  long long pair_stride_imgs, int batch, int H, int W, int win, int max_level,
+                  int max_count, double eps, float min_eig, const float* d_pts, int pts_stride,
+                  const int32_t* d_npts, int cap, float* d_out, uint8_t* d_status, float* d_err,
+                  void* stream);
+/* The filters after the LK call, order-preserving: status, err < max_error,
+ * np.around(p2) inside (y < H, x < W; also > 0 when lower_bounds) ->
+ * tp1/tp2[batch][cap][2] f32, idx (source index, may be null), count[batch].
+ * Replaces visual_odometry.py:102-112 (lower_bounds 0) and keypoint.py:20-32
+ * (lower_bounds 1). */
+int slam_lk_filter(const float* d_p1, int p1_stride, const float* d_p2, const uint8_t* d_status,
+                   const float* d_err, const int32_t* d_npts, int cap, int batch, int H, int W,
+                   float max_error, int lower_bounds, float* d_tp1, float* d_tp2, int32_t* d_idx,
+                   int32_t* d_count, void* stream);
+
+/* Workspace bytes of slam_sgbm. */
+int slam_sgbm_workspace_bytes(int batch, int H, int W, int min_disp, int num_disp, int block,
+                              size_t* bytes);
+/* Semi-global block matching (MODE_SGBM, 5 directions, BT cost on the
+ * Sobel-prefiltered and raw images, uniqueness 0, left-right check 1, 3x3
+ * median) of left/right[batch][H][stride] -> disp[batch][H][W] int16 (x16) and,
+ * if not null, disp_f32 = disp / 16.  num_disp 32 or 64, min_disp in [0, 64].
+ * Replaces cv2.StereoSGBM_create(...).compute(l, r) (visual_odometry.py:22-24,191). */
+int slam_sgbm(const uint8_t* d_left, const uint8_t* d_right, int batch, int H, int W, int stride,
+              int min_disp, int num_disp, int block, int P1, int P2, void* d_ws, size_t ws_bytes,
+              int16_t* d_disp, float* d_disp_f32, void* stream);
+/* calculate_right_qs + calc_3d for pair b (visual_odometry.py:114-134): disp1 =
+ * d_disp + b * disp1_stride, disp2 = disp1 + disp2_offset (f32 maps [H][W]);
+ * (int) truncation and NumPy's negative-index wrap; min_disp < d < max_disp;
+ * q*_r = q*_l - (d, 0); Q1/Q2 = f32 homogeneous DLT points divided in f32.
+ * Optional f64 copies (q1l64/q2l64, Q1_64/Q2_64, in pairs) feed
+ * slam_vo_estimate_pose. */
+int slam_vo_right_qs_3d(const float* d_tp1, const float* d_tp2, const int32_t* d_cnt, int cap,
+                        int batch, const float* d_disp, long long disp1_stride,
+                        long long disp2_offset, int H, int W, float min_disp, float max_disp,
+                        const double* d_Pl, const double* d_Pr, float* d_q1l, float* d_q1r,
+                        float* d_q2l, float* d_q2r, float* d_Q1, float* d_Q2, double* d_q1l64,
+                        double* d_q2l64, double* d_Q1_64, double* d_Q2_64, int32_t* d_count,
+                        void* stream);
+/* cv2.triangulatePoints on float32 points (the homogeneous result in float32)
+ * followed by Q[:3] / Q[3] in float32 (calc_3d, visual_odometry.py:129-134):
+ * ptl/ptr[batch][cap][2] f32, count[batch] -> X[batch][cap][3] f32. */
+int slam_triangulate_f32(const float* d_ptl, const float* d_ptr, const int32_t* d_count, int cap,
+                         int batch, const double* d_Pl, const double* d_Pr, float* d_X,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,7 +10,7 @@ cd "$ROOT"
 TAG="${1:-r1}"
 shift || true
 BENCH_ARGS="$*"
-timeout -k 10 420 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu_$TAG.log" 2>&1 && \
+timeout -k 10 420 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1 && \
 timeout -k 10 300 python bench.py $BENCH_ARGS > "$OUT/bench_$TAG.log" 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run \

@@ -45,6 +45,9 @@ struct OrbGeom {
   int cand_cap;   // NMS candidates per level (global scratch, worst case 1/4 density)
   int list_cap;   // kept keypoints / retainBest(2n) survivors per level (LDS)
   int lds_a, lds_u, lds_l, lds_s, lds_m;  // byte offsets of the LDS regions
+  int glob;       // level images in global memory (whole images too large for LDS)
+  int lvl_bytes;  // global level buffer per image and ping-pong half (glob only)
+  int tab_x;      // resize-coefficient slots for x (>= W); y follows
   int lds_total;
   float ls[kNLev];  // (float)pow(1.2, l)
   int nl[kNLev];    // per-level budget
@@ -60,7 +63,7 @@ __device__ __forceinline__ int rne_f(float v) { return (int)rintf(v); }
 
 // Exact n / d for n >= 0, d >= 1 with n * d < 2^32, by a multiply-high with
 // m = ceil(2^32 / d): the error n (m - 2^32/d) / 2^32 < n / 2^32 < 1/d never
-// crosses an integer.  (Here n < W * H and d <= W <= 1023, so n d < 2^30.)
+// crosses an integer.  (Here n < W * H and d <= W; build_geom checks W * H * W < 2^32.)
 // d == 1 gives m == 0 (2^32 does not fit): fdiv then returns n.
 __device__ __forceinline__ uint32_t div_magic(uint32_t d) { return 0xFFFFFFFFu / d + 1u; }
 __device__ __forceinline__ int fdiv(int n, uint32_t m) {
@@ -212,18 +215,20 @@ struct KP {  // one kept keypoint of the current level (LDS)
   float resp, angle;
 };
 
+template <bool kGlob>
 __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
                                                      float* __restrict__ ws_kp,
                                                      int32_t* __restrict__ ws_oct,
                                                      uint8_t* __restrict__ ws_desc,
                                                      int32_t* __restrict__ ws_cnt,
-                                                     uint32_t* __restrict__ ws_cand) {
+                                                     uint32_t* __restrict__ ws_cand,
+                                                     uint8_t* __restrict__ ws_lvl) {
   // All LDS is one dynamic region with a 16-byte aligned base (Guideline 17).
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int* hist = reinterpret_cast<int*>(lds + g.lds_m);  // 256 bins of FAST score
   int* ctr = hist + 256;   // 0: candidates, 1: survivors, 2: threshold, 3: kept
-  int* tabx = ctr + 16;    // resize coefficients (<= 1024 each)
-  int* taby = tabx + 1024;
+  int* tabx = ctr + 16;    // resize coefficients (tab_x for x, the rest for y)
+  int* taby = tabx + g.tab_x;
 
   const int tile = blockIdx.x, b = blockIdx.y;
   const int t = threadIdx.x;
@@ -236,8 +241,10 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   // blurred level), L = kept keypoints, S = retainBest(2n) survivors.  Only
   // one level image is resident: level l is resized from A into U and copied
   // back, so an ORB workgroup leaves room on its CU for other kernels' groups.
-  uint8_t* A = lds + g.lds_a;
-  uint8_t* U = lds + g.lds_u;
+  // kGlob: level images in global memory (a separate instantiation, so the
+  // LDS variant keeps ds_* addressing)
+  uint8_t* A = kGlob ? ws_lvl + (size_t)b * 2 * g.lvl_bytes : lds + g.lds_a;
+  uint8_t* U = kGlob ? A + g.lvl_bytes : lds + g.lds_u;
   KP* L = reinterpret_cast<KP*>(lds + g.lds_l);
   uint32_t* svc = reinterpret_cast<uint32_t*>(lds + g.lds_s);
   float* svr = reinterpret_cast<float*>(svc + g.list_cap);
@@ -277,7 +284,6 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   const int nlev = g.nlev[shp];
   for (int l = 0; l < nlev; ++l) {
     const int W = g.lw[shp][l], H = g.lh[shp][l];
-    uint8_t* I = A;
     if (l > 0) {
       // ---- resize level l-1 (A) -> l (U, INTER_LINEAR_EXACT), then U -> A
       const int SW = g.lw[shp][l - 1], SH = g.lh[shp][l - 1];
@@ -302,11 +308,18 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
         U[i] = (uint8_t)min((v + 32768) >> 16, 255);
       }
       __syncthreads();
-      for (int i = t; i < (W * H + 15) >> 4; i += kOrbWG)
-        reinterpret_cast<uint4*>(A)[i] = reinterpret_cast<const uint4*>(U)[i];
-      __syncthreads();
+      if (kGlob) {  // global level buffers: swap roles instead of copying
+        uint8_t* tmp = A;
+        A = U;
+        U = tmp;
+      } else {
+        for (int i = t; i < (W * H + 15) >> 4; i += kOrbWG)
+          reinterpret_cast<uint4*>(A)[i] = reinterpret_cast<const uint4*>(U)[i];
+        __syncthreads();
+      }
       ORB_T(1);
     }
+    uint8_t* I = A;
     const int n_l = g.nl[l];
     if (W <= 2 * kEdge || H <= 2 * kEdge || n_l == 0) continue;  // uniform
 
@@ -335,7 +348,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
         if (s > sp[-1] && s > sp[1] && s > sp[-SWd - 1] && s > sp[-SWd] && s > sp[-SWd + 1] &&
             s > sp[SWd - 1] && s > sp[SWd] && s > sp[SWd + 1]) {
           const int k = atomicAdd(&ctr[0], 1);
-          if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 20) | ((uint32_t)y << 10) | (uint32_t)x;
+          if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 23) | ((uint32_t)y << 12) | (uint32_t)x;
           atomicAdd(&hist[s], 1);
         }
       }
@@ -399,7 +412,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
       const int T = ctr[2];
       for (int i = t; i < ncand; i += kOrbWG) {
         const uint32_t c = gcand[i];
-        if ((int)(c >> 20) >= T) {
+        if ((int)(c >> 23) >= T) {
           const int k = atomicAdd(&ctr[1], 1);
           cand[k] = c;
         }
@@ -410,7 +423,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     ORB_T(4);
     for (int i = t; i < nk; i += kOrbWG) {
       const uint32_t c = cand[i];
-      cresp[i] = harris(I, W, (int)(c & 1023u), (int)((c >> 10) & 1023u));
+      cresp[i] = harris(I, W, (int)(c & 4095u), (int)((c >> 12) & 2047u));
     }
     __syncthreads();
     ORB_T(5);
@@ -418,16 +431,16 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     for (int i = t; i < nk; i += kOrbWG) {
       const float ri = cresp[i];
       const uint32_t ci = cand[i];
-      const uint32_t yxi = ci & 0xFFFFFu;  // (y << 10) | x: y-major order
+      const uint32_t yxi = ci & 0x7FFFFFu;  // (y << 12) | x: y-major order
       int rank = 0;
       for (int j = 0; j < nk; ++j) {
         const float rj = cresp[j];
-        const uint32_t yxj = cand[j] & 0xFFFFFu;
+        const uint32_t yxj = cand[j] & 0x7FFFFFu;
         rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
       }
       if (rank < g.list_cap) {
-        L[rank].x = (int)(ci & 1023u);
-        L[rank].y = (int)((ci >> 10) & 1023u);
+        L[rank].x = (int)(ci & 4095u);
+        L[rank].y = (int)((ci >> 12) & 2047u);
         L[rank].resp = ri;
       }
     }
@@ -716,7 +729,8 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
         if (g->sw[s] == w && g->sh[s] == h) break;
       if (s == g->nshapes) {
         SLAM_REQUIRE(g->nshapes < kMaxShapes, "slam_orb: too many distinct patch shapes");
-        SLAM_REQUIRE(w <= 1023 && h <= 1023, "slam_orb: patch %dx%d too large", w, h);
+        SLAM_REQUIRE(w <= 4095 && h <= 2047 && (uint64_t)w * h * w < (1ull << 32),
+                     "slam_orb: patch %dx%d too large", w, h);
         g->sw[s] = w;
         g->sh[s] = h;
         int last = -1;
@@ -747,12 +761,32 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
   for (int l = 0; l < kNLev; ++l) nmax = max(nmax, g->nl[l]);
   g->cand_cap = max(max_cand, 1);
   g->list_cap = max(2 * nmax, nmax + 256);
-  g->lds_a = 0;
-  g->lds_u = al(max_a);
-  g->lds_l = g->lds_u + al(max_u);
+  int max_w = 0, max_h = 0;
+  for (int s = 0; s < g->nshapes; ++s) {
+    max_w = max(max_w, g->sw[s]);
+    max_h = max(max_h, g->sh[s]);
+  }
+  g->tab_x = (max_w + 3) & ~3;
+  const int lists = al(g->list_cap * (int)sizeof(KP)) + al(g->list_cap * 8) +
+                    (256 + 16 + g->tab_x + max_h) * 4;
+  g->glob = al(max_a) + al(max_u) + lists > 160 * 1024;
+  if (g->glob) {
+    // A patch (a whole image, orb_extraction_detect on a full frame) whose
+    // level images do not fit LDS keeps them in two global ping-pong buffers
+    // per image (L2-resident); the keypoint lists stay in LDS.
+    SLAM_REQUIRE(g->n_tiles == 1, "slam_orb: %d patches of %dx%d do not fit LDS", g->n_tiles, pw, ph);
+    g->lvl_bytes = (max(max_a, max_u) + 64 + 255) & ~255;
+    g->lds_a = g->lds_u = 0;
+    g->lds_l = 0;
+  } else {
+    g->lvl_bytes = 0;
+    g->lds_a = 0;
+    g->lds_u = al(max_a);
+    g->lds_l = g->lds_u + al(max_u);
+  }
   g->lds_s = g->lds_l + al(g->list_cap * (int)sizeof(KP));
   g->lds_m = g->lds_s + al(g->list_cap * 8);
-  g->lds_total = g->lds_m + (256 + 16 + 2 * 1024) * 4;
+  g->lds_total = g->lds_m + (256 + 16 + g->tab_x + max_h) * 4;
   g->tcap = max_kp + 64;
   SLAM_REQUIRE(g->lds_total <= 160 * 1024,
                "slam_orb: patch %dx%d needs %d B of LDS (> 160 KiB)", pw, ph, g->lds_total);
@@ -783,7 +817,8 @@ extern "C" int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int
   SLAM_REQUIRE(bytes != nullptr && batch >= 0, "slam_orb_workspace_bytes: bad args");
   const size_t slots = (size_t)batch * g.n_tiles * g.tcap;
   *bytes = slots * (5 * sizeof(float) + sizeof(int32_t) + 32) + (size_t)batch * g.n_tiles * 4 +
-           256 + (size_t)batch * g.n_tiles * 3 * g.cand_cap * sizeof(uint32_t);
+           256 + (size_t)batch * g.n_tiles * 3 * g.cand_cap * sizeof(uint32_t) + 256 +
+           (size_t)batch * 2 * g.lvl_bytes;
   return SLAM_OK;
 }
 
@@ -820,9 +855,14 @@ extern "C" int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int
   int32_t* ws_cnt = reinterpret_cast<int32_t*>(ws_desc + slots * 32);
   uint32_t* ws_cand = reinterpret_cast<uint32_t*>(
       (reinterpret_cast<uintptr_t>(ws_cnt + (size_t)batch * g.n_tiles) + 255) & ~(uintptr_t)255);
+  uint8_t* ws_lvl = reinterpret_cast<uint8_t*>(
+      (reinterpret_cast<uintptr_t>(ws_cand + (size_t)batch * g.n_tiles * 3 * g.cand_cap) + 255) &
+      ~(uintptr_t)255);
   SLAM_REQUIRE(((uintptr_t)ws_cnt & 3) == 0, "slam_orb_tiles: workspace misaligned");
-  k_orb_tile<<<dim3(g.n_tiles, batch), kOrbWG, g.lds_total, s>>>(d_img, g, ws_kp, ws_oct,
-                                                                  ws_desc, ws_cnt, ws_cand);
+  auto kern = g.glob ? k_orb_tile<true> : k_orb_tile<false>;
+  kern<<<dim3(g.n_tiles, batch), kOrbWG, g.lds_total, s>>>(d_img, g, ws_kp, ws_oct,
+                                                                  ws_desc, ws_cnt, ws_cand,
+                                                                  ws_lvl);
   SLAM_LAUNCHED("k_orb_tile");
   k_orb_compact<<<batch, 256, 0, s>>>(ws_kp, ws_oct, ws_desc, ws_cnt, g.n_tiles, g.tcap, d_kp,
                                       d_octave, d_desc, d_count, kp_cap);

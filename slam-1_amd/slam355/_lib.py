@@ -83,6 +83,25 @@ SIGNATURES = {
     "slam_bow_query": [c_p, c_int, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_bow_lloyd": [c_p, c_int, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_pose_chain_workspace_len": [c_int],
+    "slam_fast_tiles_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int,
+                                        ctypes.POINTER(c_size_t)],
+    "slam_fast_tiles": [c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
+                        c_size_t, c_p, c_p, c_int, c_p],
+    "slam_lk_pyramid_layout": [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int),
+                               ctypes.POINTER(c_size_t)],
+    "slam_lk_build_pyramids": [c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_p],
+    "slam_lk_track": [c_p, c_p, c_p, ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int,
+                      c_double, ctypes.c_float, c_p, c_int, c_p, c_int, c_p, c_p, c_p, c_p],
+    "slam_lk_filter": [c_p, c_int, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, ctypes.c_float,
+                       c_int, c_p, c_p, c_p, c_p, c_p],
+    "slam_sgbm_workspace_bytes": [c_int, c_int, c_int, c_int, c_int, c_int,
+                                  ctypes.POINTER(c_size_t)],
+    "slam_sgbm": [c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
+                  c_size_t, c_p, c_p, c_p],
+    "slam_vo_right_qs_3d": [c_p, c_p, c_p, c_int, c_int, c_p, ctypes.c_longlong,
+                            ctypes.c_longlong, c_int, c_int, ctypes.c_float, ctypes.c_float, c_p,
+                            c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    "slam_triangulate_f32": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p],
     "slam_pose_chain_trf": [c_p, c_int, c_int, c_int, c_int, c_double, c_double, c_double, c_int,
                             c_p, c_p],
 }

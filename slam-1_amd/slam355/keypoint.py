@@ -61,3 +61,30 @@ def track_keypoints_left_to_right_new(key_points_left, descriptors_left, key_poi
     mask, _, _ = geometry.fundamental_lmeds(m1, m2, cnt, seed=seed, item0=frame)
     keep = mask[0, :M].cpu().numpy().astype(bool)
     return pts_left[keep], pts_right[keep], des_left[keep], des_right[keep]
+
+
+def track_keypoints_left_to_right(image_left, image_right, key_points_left, descriptors_left,
+                                  max_error=500):
+    """(keypoint.py:13-32) pyramidal LK from the left to the right image (15x15,
+    3 levels, 50 iterations / 0.03), then status, err < max_error and
+    0 < np.around(p2) < (w, h) -> (trackpoints1 [M,2] f32, descriptors [M,32],
+    trackpoints2 [M,2] f32), all on the GPU (csrc/vofront.hip)."""
+    from . import vofront
+
+    dev = require_gpu()
+    p1 = _pts(key_points_left)
+    des = np.asarray(descriptors_left)
+    n = len(p1)
+    if n == 0:
+        return p1, des[:0], p1.copy()
+    H, W = np.asarray(image_right).shape
+    imgs = to_dev(np.stack([np.asarray(image_left, np.uint8), np.asarray(image_right, np.uint8)]))
+    pyr = vofront.LKPyramids(imgs)
+    t1 = to_dev(p1[None])
+    cnt = torch.tensor([n], dtype=torch.int32, device=dev)
+    p2, st, err = vofront.lk_track(pyr, pyr, t1, cnt, prev0=0, next0=1)
+    tp1, tp2, idx, m = vofront.lk_filter(t1, p2, st, err, cnt, H, W, max_error=max_error,
+                                         lower_bounds=True)
+    k = int(m[0])
+    sel = idx[0, :k].cpu().numpy()
+    return tp1[0, :k].cpu().numpy(), des[sel], tp2[0, :k].cpu().numpy()

@@ -213,6 +213,27 @@ def test_gpu_orb_extraction_detect_single_patch():
 
 
 @pytest.mark.gpu
+def test_gpu_orb_whole_frames_global_levels():
+    """cv2.ORB_create(n).detectAndCompute on a whole frame (bag_of_words.py:12,17):
+    level images too large for LDS live in global ping-pong buffers."""
+    from slam355 import orb
+
+    L, R = _frames(1, 640, 480, seed=6)
+    rng = np.random.default_rng(8)
+    noise = rng.integers(0, 256, (1, 480, 640), dtype=np.uint8)
+    for img, n in ((L[0], 100), (R[0], 500), (noise[0], 500)):
+        kps, des = orb.orb_extraction_detect(img, n)
+        ek, eo, ed = oracle.orb_tiles(img, n, 1, 0, 0)
+        assert len(kps) == len(ek) > 0
+        assert np.array_equal(np.array([k.pt for k in kps], np.float32), ek[:, :2])
+        assert np.array_equal(des, ed)
+    L2, _ = _frames(1, 1280, 720, seed=7)
+    kps, des = orb.orb_extraction_detect(L2[0], 1000)
+    ek, eo, ed = oracle.orb_tiles(L2[0], 1000, 1, 0, 0)
+    assert len(kps) == len(ek) > 0 and np.array_equal(des, ed)
+
+
+@pytest.mark.gpu
 def test_gpu_orb_reference_api_shapes():
     from slam355 import orb
 
