@@ -406,12 +406,109 @@ def run_matcher(args, world, rank):
     }
 
 
+# ---------------------------------------------------------------------------- LK/SGBM VO
+SGBM_OPS_PER_CELL = 58  # BT cost 12 + box sums 4 + 5 paths x 7 + S/saturation 6 + argmin 1
+
+
+def run_vo(args, world, rank):
+    """The alternative stereo-VO front end (visual_odometry.py get_pose :188-195):
+    one step = B frame pairs at 1280x720: FAST on 10x20 tiles, LK pyramids,
+    pyramidal LK, SGBM on B+1 stereo pairs, disparity lookup + float32 DLT and
+    the RANSAC-6 + LM pose, all on one stream."""
+    from slam355 import geometry, vofront
+    from slam355.synthetic import stereo_sequence
+
+    B = args.batch
+    L, R, poses, rig = stereo_sequence(B + 1, W_IMG, H_IMG, seed=rank)
+    dev = torch.device("cuda")
+    tl, tr = torch.from_numpy(L).to(dev), torch.from_numpy(R).to(dev)
+    stream = torch.cuda.current_stream()
+    out = {}
+
+    def mark(marks, name):
+        if marks is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            marks.append((name, e))
+
+    def step(marks):
+        mark(marks, "start")
+        kp, nkp = vofront.fast_tiles(tl[:B])
+        mark(marks, "fast")
+        pyr = vofront.LKPyramids(tl)
+        mark(marks, "lk_pyramids")
+        p2, st, err = vofront.lk_track(pyr, pyr, kp, nkp, prev0=0, next0=1)
+        mark(marks, "lk_track")
+        tp1, tp2, _, ntp = vofront.lk_filter(kp, p2, st, err, nkp, H_IMG, W_IMG)
+        mark(marks, "lk_filter")
+        _, dispf = vofront.sgbm(tl, tr, **vofront.SGBM)
+        mark(marks, "sgbm")
+        o = vofront.right_qs_3d(tp1, tp2, ntp, dispf, rig.P_l, rig.P_r)
+        mark(marks, "right_qs_3d")
+        pose, _, _, _ = geometry.vo_estimate_pose(o["q1_l64"], o["q2_l64"], o["Q1_64"],
+                                                  o["Q2_64"], o["count"], rig.P_l, seed=0)
+        mark(marks, "pose")
+        out.update(nkp=nkp, ntp=ntp, cnt=o["count"], pose=pose)
+
+    dt, stages = timed_loop(step, args.steps, args.warmup, world)
+    frames = B * args.steps
+    value = reduce_scalar(frames, world, "sum") / dt
+    W1 = W_IMG - 32
+    cells = (B + 1) * H_IMG * W1 * 32
+    sgbm_ms = stages["sgbm"]
+    achieved = cells * SGBM_OPS_PER_CELL / (sgbm_ms * 1e-3) / 1e12
+    dof = out["pose"].cpu().numpy()
+    gt_dz = [float((np.linalg.inv(poses[i]) @ poses[i + 1])[2, 3]) for i in range(B)]
+    rec = {
+        "metric": "frames/sec LK/SGBM stereo-VO front end @1280x720 (visual_odometry.py get_pose)",
+        "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8+i16+f32+f64",
+        "data": "synthetic (seeded 1280x720 stereo sequence, GT poses)",
+        "config": {"workload": "LK/SGBM VO: FAST 10x20 tiles x10, LK 15x15x4 levels, SGBM 32 disp "
+                               "block 11, RANSAC-6 LM pose", "frames_per_gpu_per_step": B,
+                   "parallelism": f"frame-pair shards x{world}"},
+        "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
+                     "unit": "Tops/s", "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
+                     "kernel": "SGBM (k_sgbm_hsum + vert + 2 diag + row + median)",
+                     "ms_per_launch": sgbm_ms, "cells_per_launch": cells,
+                     "ops_per_cell": SGBM_OPS_PER_CELL},
+        "stage_ms_per_step": stages,
+        "vo": {"fast_kp_mean": float(out["nkp"].float().mean()),
+               "tracked_mean": float(out["ntp"].float().mean()),
+               "with_disparity_mean": float(out["cnt"].float().mean()),
+               "t_err_max": float(np.abs(dof[:, 5] - np.array(gt_dz)).max())},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline_vo(L, R, rig)
+    return rec
+
+
+def cpu_baseline_vo(L, R, rig, pairs=1):
+    """oracle/vofront (C FAST/LK with OpenMP, C SGBM single-thread, numpy glue,
+    C pose) on `pairs` frame pairs: SGBM of both frames + get_pose."""
+    from oracle import vofront as vf
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    d0 = vf.disparity_f32(L[0], R[0])
+    for i in range(pairs):
+        d1 = vf.disparity_f32(L[i + 1], R[i + 1])
+        vf.get_pose(L[i], L[i + 1], d0, d1, rig.P_l, rig.P_r, seed=0, frame=i)
+        d0 = d1
+    dt = time.perf_counter() - t0
+    return {"value": pairs / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{pairs} frame pair(s) through oracle/vofront: SGBM of {pairs + 1} stereo "
+                      f"pairs (costs OpenMP x{threads}, paths single-thread C), FAST, LK "
+                      f"(OpenMP x{threads}), numpy glue, C pose = {dt * 1e3:.0f} ms"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="tracking", choices=["tracking", "ba", "matcher"])
+    ap.add_argument("--workload", default="tracking", choices=["tracking", "ba", "matcher", "vo"])
     ap.add_argument("--batch", type=int, default=32, help="frame pairs per GPU per step")
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
@@ -429,7 +526,8 @@ def main():
                          "SIMDs and LDS with ORB workgroups")
     args = ap.parse_args()
     world, rank = dist_init()
-    run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher}[args.workload]
+    run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher,
+           "vo": run_vo}[args.workload]
     rec = run(args, world, rank)
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -470,11 +470,17 @@ void oracle_sgbm(const uint8_t* L, const uint8_t* R, int H, int W, int minD, int
   if (W1 <= 0) goto median;
   {
     int16_t* pc = (int16_t*)malloc(sizeof(int16_t) * (size_t)H * W1 * D);
-    int* buf = (int*)malloc(sizeof(int) * 16 * W);
-    for (int y = 0; y < H; ++y) sgbm_pixel_cost(L, R, H, W, y, minD, D, pc + (size_t)y * W1 * D, buf);
-    free(buf);
+#pragma omp parallel
+    {
+      int* buf = (int*)malloc(sizeof(int) * 16 * W);
+#pragma omp for schedule(static)
+      for (int y = 0; y < H; ++y)
+        sgbm_pixel_cost(L, R, H, W, y, minD, D, pc + (size_t)y * W1 * D, buf);
+      free(buf);
+    }
     /* box sum, replicated borders */
     int16_t* C = (int16_t*)malloc(sizeof(int16_t) * (size_t)H * W1 * D);
+#pragma omp parallel for schedule(static)
     for (int y = 0; y < H; ++y)
       for (int x = 0; x < W1; ++x)
         for (int d = 0; d < D; ++d) {
