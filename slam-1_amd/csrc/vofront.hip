@@ -573,6 +573,31 @@ __device__ __forceinline__ void store_cell(int16_t* p, const int (&v)[DPL]) {
   }
 }
 
+// Raw cells for register prefetch rings (loads issued kPF steps ahead of use).
+constexpr int kPF = 8;
+template <int DPL>
+struct RawCell;
+template <>
+struct RawCell<2> {
+  uint32_t u;
+  __device__ __forceinline__ void load(const int16_t* p) { u = *reinterpret_cast<const uint32_t*>(p); }
+  __device__ __forceinline__ void get(int (&v)[2]) const {
+    v[0] = (int)(int16_t)(u & 0xFFFFu);
+    v[1] = (int)(int16_t)(u >> 16);
+  }
+};
+template <>
+struct RawCell<4> {
+  uint2 u;
+  __device__ __forceinline__ void load(const int16_t* p) { u = *reinterpret_cast<const uint2*>(p); }
+  __device__ __forceinline__ void get(int (&v)[4]) const {
+    v[0] = (int)(int16_t)(u.x & 0xFFFFu);
+    v[1] = (int)(int16_t)(u.x >> 16);
+    v[2] = (int)(int16_t)(u.y & 0xFFFFu);
+    v[3] = (int)(int16_t)(u.y >> 16);
+  }
+};
+
 // K1: per (image, row, 64-column band): prefilter + BT pixel costs + horizontal
 // 11-sum (replicated at x = 0, W1-1) -> hs[y][x][d]
 constexpr int kHsBand = 64;
@@ -641,15 +666,19 @@ __global__ __launch_bounds__(kBS) void k_sgbm_hsum(const uint8_t* __restrict__ l
     pc[(xc - pc_lo) * D + d] = (int16_t)cost;
   }
   __syncthreads();
+  // sliding horizontal sums: thread = (d, run of kHsBand / (kBS / D) columns)
   int16_t* out = hs + (size_t)n * g.vol + (size_t)y * g.W1 * D;
-  for (int i = t; i < (xe - x0) * D; i += kBS) {
-    const int x = x0 + i / D, d = i % D;
+  constexpr int kRun = kHsBand / (kBS / D);
+  const int d = t % D, xr0 = x0 + (t / D) * kRun;
+  if (xr0 < xe) {
+    auto at = [&](int x) { return (int)pc[(min(max(x, 0), g.W1 - 1) - pc_lo) * D + d]; };
     int s = 0;
-    for (int dx = -SW2; dx <= SW2; ++dx) {
-      const int xx = min(max(x + dx, 0), g.W1 - 1);
-      s += pc[(xx - pc_lo) * D + d];
+    for (int dx = -SW2; dx <= SW2; ++dx) s += at(xr0 + dx);
+    out[(size_t)xr0 * D + d] = (int16_t)s;
+    for (int x = xr0 + 1; x < min(xr0 + kRun, xe); ++x) {
+      s += at(x + SW2) - at(x - SW2 - 1);
+      out[(size_t)x * D + d] = (int16_t)s;
     }
-    out[(size_t)x * D + d] = (int16_t)s;
   }
 }
 
@@ -678,25 +707,36 @@ __global__ __launch_bounds__(kBS) void k_sgbm_vert(const int16_t* __restrict__ h
     for (int i = 0; i < DPL; ++i) C[i] += tmp[i];
   }
   int mp = 0;
-  // prefetch one row ahead
-  int na[DPL], ns[DPL];
-  if (H > 1) {
-    load_cell<DPL>(h + (size_t)min(1 + SH2, H - 1) * rowst, na);
-    load_cell<DPL>(h + (size_t)max(1 - SH2 - 1, 0) * rowst, ns);
-  }
-  for (int y = 0; y < H; ++y) {
-    if (y > 0) {
+  // rows y + SH2 (added) and y - SH2 - 1 (removed) of the running sum, kPF rows ahead
+  RawCell<DPL> ra[kPF], rs[kPF];
 #pragma unroll
-      for (int i = 0; i < DPL; ++i) C[i] += na[i] - ns[i];
-      if (y + 1 < H) {
-        load_cell<DPL>(h + (size_t)min(y + 1 + SH2, H - 1) * rowst, na);
-        load_cell<DPL>(h + (size_t)max(y - SH2, 0) * rowst, ns);
+  for (int k = 0; k < kPF; ++k) {
+    ra[k].load(h + (size_t)min(k + SH2, H - 1) * rowst);
+    rs[k].load(h + (size_t)max(k - SH2 - 1, 0) * rowst);
+  }
+  for (int y0 = 0; y0 < H; y0 += kPF) {
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int y = y0 + k;
+      if (y < H) {
+        int a[DPL], b[DPL];
+        ra[k].get(a);
+        rs[k].get(b);
+        const int yn = y + kPF;
+        if (yn < H) {
+          ra[k].load(h + (size_t)min(yn + SH2, H - 1) * rowst);
+          rs[k].load(h + (size_t)max(yn - SH2 - 1, 0) * rowst);
+        }
+        if (y > 0) {
+#pragma unroll
+          for (int i = 0; i < DPL; ++i) C[i] += a[i] - b[i];
+        }
+        mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
+        if (live) {
+          store_cell<DPL>(co + (size_t)y * rowst, C);
+          store_cell<DPL>(lo + (size_t)y * rowst, L);
+        }
       }
-    }
-    mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
-    if (live) {
-      store_cell<DPL>(co + (size_t)y * rowst, C);
-      store_cell<DPL>(lo + (size_t)y * rowst, L);
     }
   }
 }
@@ -729,17 +769,26 @@ __global__ __launch_bounds__(kBS) void k_sgbm_diag(const int16_t* __restrict__ C
   const int16_t* c = Cv + (size_t)n * g.vol + (size_t)y * rowst + (size_t)x * D + j * DPL;
   int16_t* lo = Lv + (size_t)n * g.vol + (size_t)y * rowst + (size_t)x * D + j * DPL;
   const long long step = (long long)rowst + (long long)DX * D;
-  int L[DPL], C[DPL], Cn[DPL];
+  int L[DPL];
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) L[i] = C[i] = Cn[i] = 0;
+  for (int i = 0; i < DPL; ++i) L[i] = 0;
   int mp = 0;
-  if (len > 0) load_cell<DPL>(c, Cn);
-  for (int k = 0; k < lmax; ++k) {
+  RawCell<DPL> rc[kPF];
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) C[i] = Cn[i];
-    if (k + 1 < len) load_cell<DPL>(c + (k + 1) * step, Cn);
-    mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
-    if (k < len) store_cell<DPL>(lo + k * step, L);
+  for (int k = 0; k < kPF; ++k)
+    if (k < len) rc[k].load(c + k * step);
+  for (int k0 = 0; k0 < lmax; k0 += kPF) {
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int i = k0 + k;
+      if (i < lmax) {
+        int C[DPL];
+        rc[k].get(C);
+        if (i + kPF < len) rc[k].load(c + (i + kPF) * step);
+        mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
+        if (i < len) store_cell<DPL>(lo + i * step, L);
+      }
+    }
   }
 }
 
@@ -754,6 +803,7 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
                                                  int16_t* __restrict__ S1v, SgbmGeom g,
                                                  int16_t* __restrict__ raw) {
   constexpr int DPL = D / 16;
+  constexpr int kPFR = 16;  // cells in flight per lane and volume
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int t = threadIdx.x, r = t >> 4, j = t & 15, n = blockIdx.y;
   const int y = blockIdx.x * 4 + r;
@@ -761,11 +811,12 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
   const int ys = live ? y : g.H - 1;
   const int W = g.W, W1 = g.W1, minX1 = g.minX1;
   uint32_t* cost2 = reinterpret_cast<uint32_t*>(lds) + r * W;
-  int16_t* d1 = reinterpret_cast<int16_t*>(reinterpret_cast<uint32_t*>(lds) + 4 * W) + r * W;
+  // the row's left-view disparities go straight to `raw` (only live rows write)
+  int16_t* out = raw + (size_t)n * g.H * W + (size_t)ys * W;
   const int INVALID = (g.minD - 1) * 16;
   for (int x = j; x < W; x += 16) {
     cost2[x] = 0xFFFFFFFFu;
-    d1[x] = (int16_t)INVALID;
+    if (live) out[x] = (int16_t)INVALID;
   }
   __syncthreads();
   const size_t base = (size_t)n * g.vol + (size_t)ys * W1 * D + j * DPL;
@@ -774,70 +825,115 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
   const int16_t* l2 = L2v + base;
   const int16_t* l3 = L3v + base;
   int16_t* s1 = S1v + base;
-  int L[DPL], C[DPL], a1[DPL], a2[DPL], a3[DPL];
+  int L[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) L[i] = 0;
   int mp = 0;
-  for (int x = 0; x < W1; ++x) {
-    const size_t q = (size_t)x * D;
-    load_cell<DPL>(c + q, C);
-    load_cell<DPL>(l1 + q, a1);
-    load_cell<DPL>(l2 + q, a2);
-    load_cell<DPL>(l3 + q, a3);
-    mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
-    int s[DPL];
+  {
+    RawCell<DPL> rc[kPFR], r1[kPFR], r2[kPFR], r3[kPFR];
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) s[i] = sat16(L[i] + a1[i] + a2[i] + a3[i]);
-    store_cell<DPL>(s1 + q, s);
+    for (int k = 0; k < kPFR; ++k)
+      if (k < W1) {
+        rc[k].load(c + (size_t)k * D);
+        r1[k].load(l1 + (size_t)k * D);
+        r2[k].load(l2 + (size_t)k * D);
+        r3[k].load(l3 + (size_t)k * D);
+      }
+    for (int x0 = 0; x0 < W1; x0 += kPFR) {
+#pragma unroll
+      for (int k = 0; k < kPFR; ++k) {
+        const int x = x0 + k;
+        if (x < W1) {
+          int C[DPL], a1[DPL], a2[DPL], a3[DPL];
+          rc[k].get(C);
+          r1[k].get(a1);
+          r2[k].get(a2);
+          r3[k].get(a3);
+          const int xn = x + kPFR;
+          if (xn < W1) {
+            rc[k].load(c + (size_t)xn * D);
+            r1[k].load(l1 + (size_t)xn * D);
+            r2[k].load(l2 + (size_t)xn * D);
+            r3[k].load(l3 + (size_t)xn * D);
+          }
+          mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
+          int sv[DPL];
+#pragma unroll
+          for (int i = 0; i < DPL; ++i) sv[i] = sat16(L[i] + a1[i] + a2[i] + a3[i]);
+          store_cell<DPL>(s1 + (size_t)x * D, sv);
+        }
+      }
+    }
   }
+  // the S1 stores of this row must land before the right->left pass reads them
+  __threadfence_block();
 #pragma unroll
   for (int i = 0; i < DPL; ++i) L[i] = 0;
   mp = 0;
   const int gbase = r * 16;
-  for (int x = W1 - 1; x >= 0; --x) {
-    const size_t q = (size_t)x * D;
-    int S[DPL];
-    load_cell<DPL>(c + q, C);
-    load_cell<DPL>(s1 + q, S);
-    mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
-    int key = 0x7FFFFFFF;
+  RawCell<DPL> rc[kPFR], rsv[kPFR];
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) {
-      S[i] = sat16(S[i] + L[i]);
-      key = min(key, S[i] * 64 + j * DPL + i);  // first minimum over d
+  for (int k = 0; k < kPFR; ++k)
+    if (k < W1) {
+      rc[k].load(c + (size_t)(W1 - 1 - k) * D);
+      rsv[k].load(s1 + (size_t)(W1 - 1 - k) * D);
     }
-    key = row_min16(key);
-    const int minS = key >> 6;  // arithmetic shift: floor division for negative S
-    int d = key - minS * 64;
-    const int xa = x + minX1;
-    if (minS >= kMaxCost) continue;  // bestDisp = -1 in the reference: stays invalid
-    // S[d-1], S[d+1] from their owner lanes
-    const int dm = max(d - 1, 0), dp = min(d + 1, D - 1);
-    int sm = 0, sp = 0;
+  for (int i0 = 0; i0 < W1; i0 += kPFR) {
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) {
-      const int vm = __shfl(S[i], gbase + dm / DPL, 64);
-      const int vp = __shfl(S[i], gbase + dp / DPL, 64);
-      if (i == dm % DPL) sm = vm;
-      if (i == dp % DPL) sp = vp;
-    }
-    if (j == 0) {
-      const int x2 = xa - d - g.minD;
-      atomicMin(&cost2[x2], ((uint32_t)(minS + 32768) << 16) | (uint32_t)(65535 - xa));
-      if (0 < d && d < D - 1) {
-        const int den = max(sm + sp - 2 * minS, 1);
-        d = d * 16 + ((sm - sp) * 16 + den) / (den * 2);
-      } else {
-        d *= 16;
+    for (int k = 0; k < kPFR; ++k) {
+      const int i = i0 + k;
+      if (i < W1) {
+        const int x = W1 - 1 - i;
+        int C[DPL], S[DPL];
+        rc[k].get(C);
+        rsv[k].get(S);
+        const int in = i + kPFR;
+        if (in < W1) {
+          rc[k].load(c + (size_t)(W1 - 1 - in) * D);
+          rsv[k].load(s1 + (size_t)(W1 - 1 - in) * D);
+        }
+        mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
+        int key = 0x7FFFFFFF;
+#pragma unroll
+        for (int q = 0; q < DPL; ++q) {
+          S[q] = sat16(S[q] + L[q]);
+          key = min(key, S[q] * 64 + j * DPL + q);  // first minimum over d
+        }
+        key = row_min16(key);
+        const int minS = key >> 6;  // arithmetic shift: floor division for negative S
+        int d = key - minS * 64;
+        const int xa = x + minX1;
+        if (minS < kMaxCost) {  // else bestDisp = -1 in the reference: stays invalid
+          // S[d-1], S[d+1] from their owner lanes
+          const int dm = max(d - 1, 0), dp = min(d + 1, D - 1);
+          int sm = 0, sp = 0;
+#pragma unroll
+          for (int q = 0; q < DPL; ++q) {
+            const int vm = __shfl(S[q], gbase + dm / DPL, 64);
+            const int vp = __shfl(S[q], gbase + dp / DPL, 64);
+            if (q == dm % DPL) sm = vm;
+            if (q == dp % DPL) sp = vp;
+          }
+          if (j == 0) {
+            const int x2 = xa - d - g.minD;
+            atomicMin(&cost2[x2], ((uint32_t)(minS + 32768) << 16) | (uint32_t)(65535 - xa));
+            if (0 < d && d < D - 1) {
+              const int den = max(sm + sp - 2 * minS, 1);
+              d = d * 16 + ((sm - sp) * 16 + den) / (den * 2);
+            } else {
+              d *= 16;
+            }
+            if (live) out[xa] = (int16_t)(d + g.minD * 16);
+          }
+        }
       }
-      d1[xa] = (int16_t)(d + g.minD * 16);
     }
   }
   __syncthreads();
+  if (!live) return;
   // left-right consistency (disp12MaxDiff 1)
-  int16_t* out = raw + (size_t)n * g.H * W + (size_t)ys * W;
   for (int x = j; x < W; x += 16) {
-    int v = d1[x];
+    int v = out[x];
     if (x >= minX1 && v != INVALID) {
       const int _d = v >> 4, d_ = (v + 15) >> 4;
       const int _x = x - _d, x_ = x - d_;
@@ -847,10 +943,10 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
       };
       if (0 <= _x && _x < W && 0 <= x_ && x_ < W) {
         const int a = disp2(_x), b = disp2(x_);
-        if (a >= g.minD && abs(a - _d) > 1 && b >= g.minD && abs(b - d_) > 1) v = INVALID;
+        if (a >= g.minD && abs(a - _d) > 1 && b >= g.minD && abs(b - d_) > 1)
+          out[x] = (int16_t)INVALID;
       }
     }
-    if (live) out[x] = (int16_t)v;
   }
 }
 
@@ -936,7 +1032,7 @@ int sgbm_launch(const uint8_t* l, const uint8_t* r, int batch, const SgbmGeom& g
     SLAM_LAUNCHED("k_sgbm_diag");
     k_sgbm_diag<D, -1><<<dim3((np + 15) / 16, batch), kBS, 0, s>>>(C, gg, L3);
     SLAM_LAUNCHED("k_sgbm_diag");
-    const size_t lds = (size_t)4 * g.W * 4 + (size_t)4 * g.W * 2;
+    const size_t lds = (size_t)4 * g.W * 4;
     k_sgbm_row<D><<<dim3((g.H + 3) / 4, batch), 64, lds, s>>>(C, L1, L2, L3, hs, gg, raw);
     SLAM_LAUNCHED("k_sgbm_row");
   }
