@@ -272,7 +272,46 @@ def run_tracking(args, world, rank):
     del trk, ba  # their kernels' buffers, then the masked stream itself
     if trk_stream is not None:
         trk_stream.destroy()
+    if not args.no_ba_scale:
+        # the metric's second half: local-BA LM iterations/s of ONE C4 window
+        # sharded over all ranks (landmarks by anchor keyframe, RCCL all-reduce
+        # of the reduced camera system per iteration) -- strong scaling in N
+        rec["local_ba_sharded"] = c4_sharded_iters(world, rank, steps=20, warmup=3)
     return rec
+
+
+def c4_sharded_iters(world, rank, steps=20, warmup=3):
+    """LM iterations/s of the C4 window (64 KF x 50k points x 300k obs) on `world`
+    ranks: every rank holds all cameras and the observations of its landmark
+    shard, builds its partial reduced camera system, RCCL all-reduces it
+    (packed upper blocks, f64 sum) and the 2-double trial cost, and solves the
+    camera system redundantly (BAProblem.step_distributed)."""
+    from slam355.ba import BAProblem, upper_blocks
+    from slam355.synthetic import ba_problem, perturb
+
+    C, P, k = 64, 50000, 6
+    rng = np.random.default_rng(7)  # the same global problem on every rank
+    cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+    c0, p0 = perturb(rng, cams, pts)
+    if world > 1:
+        from slam355.dist import shard_by_anchor
+
+        mine, keep, local_pi = shard_by_anchor(C, P, ci, pi, rank, world)
+        prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep],
+                         block_list=upper_blocks(C, ci, pi))
+        step_fn = prob.step_distributed
+        n_obs = int(keep.sum())
+    else:
+        prob = BAProblem(c0, p0, ci, pi, qs)
+        step_fn = lambda: prob.iterate_graphed(1)  # noqa: E731
+        n_obs = len(ci)
+    dt, _ = timed_loop(lambda marks: step_fn(), steps, warmup, world, marks_every=False)
+    return {"workload": f"C4 local BA {C} KF x {P} pts x {P * k} obs, one window over all ranks",
+            "iters_per_s": steps / dt, "ms_per_iter": dt / steps * 1e3, "ranks": world,
+            "obs_per_rank": n_obs, "scaling": "strong",
+            "collective": "RCCL all_reduce (sum, f64) of the packed reduced camera system + "
+                          "2 doubles per LM iteration" if world > 1 else "none (1 GPU)",
+            "final_cost": prob.state()["COST"]}
 
 
 def cpu_baseline_tracking(L, R, rig, args, C3, ba_in, pairs=2):
@@ -520,6 +559,8 @@ def main():
     ap.add_argument("--ba-serial", action="store_true",
                     help="run local BA on the tracking stream (no overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ba-scale", action="store_true",
+                    help="tracking: skip the sharded C4 local-BA iterations/s measurement")
     ap.add_argument("--track-cus", type=int, default=224,
                     help="restrict the tracking stream to this many CUs (0: all); the rest run "
                          "only local-BA work, whose latency-bound kernels then do not share "

@@ -26,3 +26,15 @@ for C, P, k in ((64, 50000, 6),):
         rows.append(prob.t["chol"][n - 7:n - 5].cpu().numpy())
     m = np.median(np.array(rows), 0)
     print(f"C={C}: panel WG: factor {m[0]:.0f} ns, gemm+store+b {m[1]:.0f} ns")
+
+# sub-phases of the diagonal-tile factor (WG 1 of step 0, wall clock 100 MHz)
+import ctypes  # noqa: E402
+
+fn = getattr(_lib.lib, "slam_tl_stamps", None)
+if fn is not None:
+    buf = (ctypes.c_ulonglong * 8)()
+    fn.argtypes = [ctypes.c_void_p]
+    fn(ctypes.cast(buf, ctypes.c_void_p))
+    st = [int(v) for v in buf[:4]]
+    print("factor sub-phases (ns): load %d, blocked chol %d, inverse assembly %d" %
+          tuple(10 * (b - a) for a, b in zip(st[:3], st[1:4])))

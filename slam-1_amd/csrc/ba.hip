@@ -979,9 +979,10 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
 // many workgroups, one launch per phase:
 //   k_tl_load         lower tile (I, J): damped S -> A (padded to N = 64T,
 //                     identity on the padded diagonal), b, tile-nonzero flags
-//   k_tl_panel(k)     WG per row tile I >= k: every WG factors A_kk (wave 0,
-//                     row i in lane i's registers, columns broadcast by
-//                     v_readlane) and inverts it the same way; WG I = k stores
+//   k_tl_panel(k)     WG per row tile I >= k: every WG factors A_kk and
+//                     inverts it (blocked over 16x16 blocks: diagonal blocks
+//                     in wave 0's registers, panel / trailing / inverse
+//                     blocks on the f64 matrix cores); WG I = k stores
 //                     L_kk^-1 (dinv[k]) and y_k = L_kk^-1 b_k; WG I > k
 //                     forms L_Ik = A_Ik L_kk^-T on the f64 matrix cores and
 //                     updates b_I -= L_Ik y_k (forward substitution fused)
@@ -1024,10 +1025,19 @@ __device__ __forceinline__ void tile_to_frag(const double* __restrict__ g, int l
   // per fragment (conflict-free LDS stores); the global reads are 16 rows x 32 B
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, c = lane >> 4;
-#pragma unroll 4
-  for (int fi = w; fi < 64; fi += nw) {
-    const int sub = fi >> 4, kk = fi & 15;
-    f[(fi << 6) + lane] = g[(size_t)(16 * sub + r) * ld + 4 * kk + c];
+  // 16 loads in flight per lane before their LDS stores
+  for (int f0 = w; f0 < 64; f0 += 16 * nw) {
+    double tmp[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int fi = f0 + q * nw;
+      tmp[q] = fi < 64 ? g[(size_t)(16 * (fi >> 4) + r) * ld + 4 * (fi & 15) + c] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int fi = f0 + q * nw;
+      if (fi < 64) f[(fi << 6) + lane] = tmp[q];
+    }
   }
 }
 
@@ -1099,74 +1109,182 @@ __global__ __launch_bounds__(128) void k_tl_scatter(slam_ba_problem p) {
   }
 }
 
-// Cholesky factor and inverse of the symmetric 64x64 diagonal tile at Akk
-// (row-major, ld), split over two waves so each holds 64 doubles per lane:
-// wave 0 keeps row i of A (then of L) in lane i's v[], wave 1 keeps column i
-// of L^-1 (v = L^-1 e_i, right-looking forward substitution).  Per column j,
-// wave 0 takes the pivot by readlane and publishes column j of L and 1/L_jj in
-// cb[j & 1] (double-buffered); after one workgroup barrier both waves apply
-// it (trailing update of A / update of v).  Every wave of the workgroup must
-// call this (64 barriers).  Returns false (uniform over the workgroup) on a
-// non-positive or non-finite pivot; on return wave 1's v[] is column i of L^-1.
-constexpr int kCb = kTB + 2;  // per buffer: column of L, 1/L_jj, pad
-__device__ __forceinline__ bool tile_chol_inv(const double* __restrict__ Akk, int ld, double* cb,
-                                              int* okp, double v[kTB]) {
-  const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (w == 0) {
+// Blocked factor + inverse of the 64x64 diagonal tile (4 x 4 blocks of 16):
+// per block column p, wave 0 factors the 16x16 diagonal block in registers
+// (lane i = row i, pivots and column entries broadcast by v_readlane) and
+// inverts it (lane c = column c of L_pp^-1); the panel L_ip = A_ip L_pp^-T and
+// the trailing update A_ij -= L_ip L_jp^T run on the f64 matrix cores
+// (16x16x4), one block per wave.  L^-1 is then assembled by block levels:
+// X_ip = -X_ii sum_{k=p}^{i-1} L_ik X_kp.  The serial chain is 4 x 16 pivots
+// (was 64 pivots with a workgroup barrier each).  M: LDS [64][65] (A, then L's
+// off-diagonal blocks), Xb: LDS [10][16][17] (lower blocks of L^-1), Tb:
+// LDS [3][16][17] scratch.  Every wave must call it; returns false (uniform)
+// on a non-positive or non-finite pivot.
+constexpr int kMS = 65;   // row stride of M (odd: MFMA operand reads spread over banks)
+constexpr int kBS17 = 17; // row stride of a 16x16 block
+__device__ __forceinline__ int blk_id(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// C (+)= X Y^T (16x16 blocks, strides sx / sy); a_neg negates the product
+__device__ __forceinline__ d4 mm16_xyT(const double* X, int sx, const double* Y, int sy, d4 acc,
+                                       bool a_neg) {
+  const int l = threadIdx.x & 63;
 #pragma unroll
-    for (int m = 0; m < kTB; ++m) v[m] = Akk[(size_t)m * ld + i];  // A symmetric: coalesced
-  } else if (w == 1) {
-#pragma unroll
-    for (int m = 0; m < kTB; ++m) v[m] = m == i ? 1.0 : 0.0;
+  for (int kk = 0; kk < 4; ++kk) {
+    const double a = X[(l & 15) * sx + 4 * kk + (l >> 4)];
+    const double b = Y[(l & 15) * sy + 4 * kk + (l >> 4)];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a_neg ? -a : a, b, acc, 0, 0, 0);
   }
-  // wave 0 publishes column j of L for step j, computed with one column of
-  // lookahead: at step j it first finishes v[j + 1], derives column j + 1
-  // (pivot, scale) and publishes it into the other buffer before the rest of
-  // step j's FMAs, so the pivot's latency chain overlaps the trailing update.
-  bool ok = true;
-  auto pivot = [&](int j) {  // wave 0: v[j] of every lane is final
-    const double djj = readlane_d(v[j], j);
-    ok = ok && djj > 0.0 && djj < INFINITY;
-    // 1/sqrt by v_rsq_f64 + two Newton steps (full double precision)
-    double r = __builtin_amdgcn_rsq(djj);
-    const double h = 0.5 * djj;
-    r = r * __builtin_fma(-h * r, r, 1.5);
-    r = r * __builtin_fma(-h * r, r, 1.5);
-    const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
-    v[j] = lij;
-    double* c = cb + (j & 1) * kCb;
-    c[i] = lij;
-    if (i == 0) c[kTB] = r;
-  };
-  if (w == 0) pivot(0);
+  return acc;
+}
+// C (+)= X Y (16x16 blocks)
+__device__ __forceinline__ d4 mm16_xy(const double* X, int sx, const double* Y, int sy, d4 acc,
+                                      bool a_neg) {
+  const int l = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < kTB; ++j) {
-    const double* c = cb + (j & 1) * kCb;
-    __syncthreads();  // column j published; column j - 1's buffer free again
-    if (w < 2) {
-      // all broadcast reads of the step issued before the FMAs (LDS latency paid once)
-      double cc[kTB];
+  for (int kk = 0; kk < 4; ++kk) {
+    const double a = X[(l & 15) * sx + 4 * kk + (l >> 4)];
+    const double b = Y[(4 * kk + (l >> 4)) * sy + (l & 15)];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a_neg ? -a : a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+__device__ __forceinline__ void st16(double* C, int sc, d4 acc) {
+  const int l = threadIdx.x & 63;
 #pragma unroll
-      for (int l = (j + 1) & ~1; l < kTB; l += 2) {
-        const double2 c2 = *reinterpret_cast<const double2*>(c + l);
-        cc[l] = c2.x;
-        cc[l + 1] = c2.y;
-      }
-      double sj = v[j];
-      if (w == 1) {
-        sj *= c[kTB];
-        v[j] = sj;
-      }
-      if (j + 1 < kTB) {
-        v[j + 1] = __builtin_fma(-sj, cc[j + 1], v[j + 1]);
-        if (w == 0) pivot(j + 1);
-      }
+  for (int r = 0; r < 4; ++r) C[((l >> 4) + 4 * r) * sc + (l & 15)] = acc[r];
+}
+__device__ __forceinline__ d4 ld16(const double* C, int sc) {
+  const int l = threadIdx.x & 63;
+  d4 acc;
 #pragma unroll
-      for (int l = j + 2; l < kTB; ++l) v[l] = __builtin_fma(-sj, cc[l], v[l]);
+  for (int r = 0; r < 4; ++r) acc[r] = C[((l >> 4) + 4 * r) * sc + (l & 15)];
+  return acc;
+}
+
+#ifdef SLAM_TL_PROFILE
+__device__ unsigned long long g_tl_stamp[8];
+#define TL_STAMP(i) \
+  if (blockIdx.x == 1 && threadIdx.x == 0 && tl_prof_on) g_tl_stamp[i] = wall_clock64()
+#else
+#define TL_STAMP(i) (void)0
+#endif
+__device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk, int ld,
+                                                  double* M, double* Xb, double* Tb, int* okp,
+                                                  bool tl_prof_on = false) {
+  const int t = threadIdx.x, l = t & 63, w = t >> 6;
+  TL_STAMP(0);
+  {
+    // all 16 loads of a lane in flight before the LDS stores
+    double tmp[kTB * kTB / kTlWG];
+#pragma unroll
+    for (int q = 0; q < kTB * kTB / kTlWG; ++q) {
+      const int e = t + kTlWG * q;
+      tmp[q] = Akk[(size_t)(e >> 6) * ld + (e & 63)];
+    }
+#pragma unroll
+    for (int q = 0; q < kTB * kTB / kTlWG; ++q) {
+      const int e = t + kTlWG * q;
+      M[(e >> 6) * kMS + (e & 63)] = tmp[q];
     }
   }
-  if (w == 0 && i == 0) *okp = ok ? 1 : 0;
+  bool ok = true;
   __syncthreads();
+  TL_STAMP(1);
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    if (w == 0) {
+      // rows of the 16x16 diagonal block in lanes 0..15 (lower part read)
+      const int i = l & 15;
+      double v[16], rj[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
+      // column j of L goes through LDS (Lt[j][i] = L[i][j], one store per lane,
+      // broadcast reads back) instead of 15 v_readlane pairs per step
+      double* Lt = Tb;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const double djj = readlane_d(v[j], j);
+        ok = ok && djj > 0.0 && djj < INFINITY;
+        double r = __builtin_amdgcn_rsq(djj);
+        const double h = 0.5 * djj;
+        r = r * __builtin_fma(-h * r, r, 1.5);
+        r = r * __builtin_fma(-h * r, r, 1.5);
+        rj[j] = r;
+        const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
+        v[j] = lij;
+        if (l < 16) Lt[j * kBS17 + i] = lij;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int m = j + 1; m < 16; ++m) v[m] = __builtin_fma(-lij, Lt[j * kBS17 + m], v[m]);
+      }
+      // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
+      const int c = l & 15;
+      double x[16];
+#pragma unroll
+      for (int ii = 0; ii < 16; ++ii) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int k = 0; k < ii; ++k) sacc = __builtin_fma(Lt[k * kBS17 + ii], x[k], sacc);
+        x[ii] = ii < c ? 0.0 : (ii == c ? rj[ii] : -sacc * rj[ii]);
+      }
+      if (l < 16) {
+        double* X = Xb + blk_id(p, p) * 16 * kBS17;
+#pragma unroll
+        for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = x[ii];
+      }
+    }
+    __syncthreads();
+    // panel: L_ip = A_ip X_pp^T (one block per wave)
+    const int ip = p + 1 + w;
+    if (ip < 4) {
+      double* Aip = M + (16 * ip) * kMS + 16 * p;
+      const d4 z = d4{0.0, 0.0, 0.0, 0.0};
+      const d4 acc = mm16_xyT(Aip, kMS, Xb + blk_id(p, p) * 16 * kBS17, kBS17, z, false);
+      st16(Aip, kMS, acc);
+    }
+    __syncthreads();
+    // trailing: A_ij -= L_ip L_jp^T for p < j <= i <= 3
+    const int nt = (3 - p) * (4 - p) / 2;
+    for (int q = w; q < nt; q += 4) {
+      int i = p + 1, rem = q;
+      while (rem >= i - p) {
+        rem -= i - p;
+        ++i;
+      }
+      const int j = p + 1 + rem;
+      double* Aij = M + (16 * i) * kMS + 16 * j;
+      d4 acc = ld16(Aij, kMS);
+      acc = mm16_xyT(M + (16 * i) * kMS + 16 * p, kMS, M + (16 * j) * kMS + 16 * p, kMS, acc, true);
+      st16(Aij, kMS, acc);
+    }
+    __syncthreads();
+  }
+  TL_STAMP(2);
+  // L^-1 by levels d = i - p: T = sum_k L_ik X_kp, then X_ip = -X_ii T
+#pragma unroll 1
+  for (int d = 1; d < 4; ++d) {
+    const int pp = w, i = pp + d;
+    if (i < 4) {
+      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
+      for (int k = pp; k < i; ++k)
+        acc = mm16_xy(M + (16 * i) * kMS + 16 * k, kMS, Xb + blk_id(k, pp) * 16 * kBS17, kBS17,
+                      acc, false);
+      double* T = Tb + w * 16 * kBS17;
+      st16(T, kBS17, acc);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const d4 z = d4{0.0, 0.0, 0.0, 0.0};
+      const d4 xi = mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, T, kBS17, z, true);
+      st16(Xb + blk_id(i, pp) * 16 * kBS17, kBS17, xi);
+    }
+    __syncthreads();
+  }
+  if (w == 0 && l == 0) *okp = ok ? 1 : 0;
+  __syncthreads();
+  TL_STAMP(3);
   return *okp != 0;
 }
 
@@ -1178,11 +1296,13 @@ void k_tl_panel(slam_ba_problem p, int k) {
   const int I = k + blockIdx.x;
   const uint8_t* nz = reinterpret_cast<const uint8_t*>(p.chol + L.nz);
   if (I > k && !nz[I * L.T + k]) return;  // L_Ik = 0, b_I unchanged
-  __shared__ double Vf[kTB * kTB];        // L_kk^-1, fragment order
+  // Vf and Xf2 are one buffer: the blocked factor's M / Xb / Tb live in it until
+  // L_kk^-1 has been read into registers
+  __shared__ double VX[2 * kTB * kTB];
+  double* Vf = VX;                        // L_kk^-1, fragment order
+  double* Xf2 = VX + kTB * kTB;           // terms of y_k = L_kk^-1 b_k
   __shared__ double Xf[kTB * kTB];        // A_Ik, fragment order; then L_Ik row-major (stride 64)
-  __shared__ double Xf2[kTB * kTB];       // terms of y_k = L_kk^-1 b_k
   __shared__ double yk[kTB];
-  __shared__ __attribute__((aligned(16))) double cb[2 * kCb];
   __shared__ int okf;
   double* A = p.chol + L.a;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1192,9 +1312,24 @@ void k_tl_panel(slam_ba_problem p, int k) {
 #endif
   double* AIk = A + (size_t)I * kTB * L.N + k * kTB;
   if (I > k && w >= 2) tile_to_frag(AIk, L.N, Xf, w - 2, 2);  // waves 2, 3 (published by the factor's barriers)
-  // wave 1, lane c ends with column c of L_kk^-1 (x[m] = Linv[m][c])
+  // wave 1, lane c: column c of L_kk^-1 (x[m] = Linv[m][c]) into registers
   double x[kTB];
-  const bool ok = tile_chol_inv(Akk, L.N, cb, &okf, x);
+  double* Mb = VX;
+  double* Xb = VX + kTB * kMS;
+  double* Tb = Xb + 10 * 16 * kBS17;
+#ifdef SLAM_TL_PROFILE
+  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf, k == 0);
+#else
+  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf);
+#endif
+  if (w == 1) {
+    const int cb16 = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < kTB; ++m)
+      x[m] = (m >> 4) >= cb16 ? Xb[blk_id(m >> 4, cb16) * 16 * kBS17 + (m & 15) * kBS17 + (lane & 15)]
+                              : 0.0;
+  }
+  __syncthreads();  // VX is reused below
   if (w == 1) {
     const double bc = p.chol[L.b + k * kTB + lane];
     if (I == k) {
@@ -1616,3 +1751,11 @@ extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* st
   }
   return SLAM_OK;
 }
+
+#ifdef SLAM_TL_PROFILE
+extern "C" int slam_tl_stamps(unsigned long long* out8) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_tl_stamp), 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif
