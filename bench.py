@@ -49,8 +49,15 @@ def dist_init():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # SLAM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+        # on one GPU (RCCL refuses two ranks per device); the driver uses nccl = RCCL
+        backend = os.environ.get("SLAM_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank
@@ -280,6 +287,13 @@ def run_tracking(args, world, rank):
     return rec
 
 
+def _backend_name():
+    import torch.distributed as dist
+
+    b = dist.get_backend()
+    return "RCCL (nccl)" if b == "nccl" else b
+
+
 def c4_sharded_iters(world, rank, steps=20, warmup=3):
     """LM iterations/s of the C4 window (64 KF x 50k points x 300k obs) on `world`
     ranks: every rank holds all cameras and the observations of its landmark
@@ -309,8 +323,8 @@ def c4_sharded_iters(world, rank, steps=20, warmup=3):
     return {"workload": f"C4 local BA {C} KF x {P} pts x {P * k} obs, one window over all ranks",
             "iters_per_s": steps / dt, "ms_per_iter": dt / steps * 1e3, "ranks": world,
             "obs_per_rank": n_obs, "scaling": "strong",
-            "collective": "RCCL all_reduce (sum, f64) of the packed reduced camera system + "
-                          "2 doubles per LM iteration" if world > 1 else "none (1 GPU)",
+            "collective": (f"{_backend_name()} all_reduce (sum, f64) of the packed reduced camera "
+                           "system + 2 doubles per LM iteration") if world > 1 else "none (1 GPU)",
             "final_cost": prob.state()["COST"]}
 
 
