@@ -870,7 +870,6 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
 #pragma unroll
   for (int i = 0; i < DPL; ++i) L[i] = 0;
   mp = 0;
-  const int gbase = r * 16;
   RawCell<DPL> rc[kPFR], rsv[kPFR];
 #pragma unroll
   for (int k = 0; k < kPFR; ++k)
@@ -903,18 +902,20 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
         const int minS = key >> 6;  // arithmetic shift: floor division for negative S
         int d = key - minS * 64;
         const int xa = x + minX1;
-        if (minS < kMaxCost) {  // else bestDisp = -1 in the reference: stays invalid
-          // S[d-1], S[d+1] from their owner lanes
-          const int dm = max(d - 1, 0), dp = min(d + 1, D - 1);
-          int sm = 0, sp = 0;
+        // S[d - 1], S[d + 1] of the lane owning the best d: the neighbours across
+        // lanes by DPP row shifts (as in path_step), inside the lane directly
+        const int sl = dpp_shr1(S[DPL - 1], kMaxCost), sr = dpp_shl1(S[0], kMaxCost);
+        int sm = 0, sp = 0;
+        bool owner = false;
 #pragma unroll
-          for (int q = 0; q < DPL; ++q) {
-            const int vm = __shfl(S[q], gbase + dm / DPL, 64);
-            const int vp = __shfl(S[q], gbase + dp / DPL, 64);
-            if (q == dm % DPL) sm = vm;
-            if (q == dp % DPL) sp = vp;
+        for (int q = 0; q < DPL; ++q)
+          if (j * DPL + q == d) {
+            owner = true;
+            sm = q > 0 ? S[q - 1] : sl;
+            sp = q < DPL - 1 ? S[q + 1] : sr;
           }
-          if (j == 0) {
+        if (minS < kMaxCost) {  // else bestDisp = -1 in the reference: stays invalid
+          if (owner) {
             const int x2 = xa - d - g.minD;
             atomicMin(&cost2[x2], ((uint32_t)(minS + 32768) << 16) | (uint32_t)(65535 - xa));
             if (0 < d && d < D - 1) {
