@@ -116,11 +116,11 @@ def ba_flops_per_iter(C, P, O, n_per_pt):
 
 
 # ---------------------------------------------------------------------------- tracking
-def pmc_traffic():
-    """Per-kernel HBM bytes per dispatch from the committed PMC summary
-    profiles/pmc_traffic.json (scripts/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE
-    in separate rocprofv3 --pmc passes of this bench), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(name="pmc_traffic.json"):
+    """Per-kernel HBM bytes per dispatch from a committed PMC summary
+    profiles/<name> (scripts/pmc_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE in
+    separate rocprofv3 --pmc passes of this bench), or None."""
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
@@ -522,7 +522,10 @@ def run_vo(args, world, rank):
                                "block 11, RANSAC-6 LM pose", "frames_per_gpu_per_step": B,
                    "parallelism": f"frame-pair shards x{world}"},
         "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS,
-                     "unit": "Tops/s", "frac": achieved / VALU_PEAK_TOPS, "traffic": None,
+                     "unit": "Tops/s", "frac": achieved / VALU_PEAK_TOPS,
+                     "traffic": sgbm_traffic(),
+                     "traffic_unit": "bytes per launch (33 stereo pairs), HBM, from PMC",
+                     "traffic_source": "profiles/pmc_traffic_vo.json",
                      "kernel": "SGBM (k_sgbm_hsum + vert + 2 diag + row + median)",
                      "ms_per_launch": sgbm_ms, "cells_per_launch": cells,
                      "ops_per_cell": SGBM_OPS_PER_CELL},
@@ -535,6 +538,12 @@ def run_vo(args, world, rank):
     if rank == 0 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_vo(L, R, rig)
     return rec
+
+
+def sgbm_traffic():
+    pmc = pmc_traffic("pmc_traffic_vo.json")
+    return pmc_bytes(pmc, ("k_sgbm_hsum<32>", "k_sgbm_vert<32>", "k_sgbm_diag<32, 1>",
+                           "k_sgbm_diag<32, -1>", "k_sgbm_row<32>", "k_sgbm_median"))
 
 
 def cpu_baseline_vo(L, R, rig, pairs=1):
