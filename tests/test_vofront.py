@@ -213,6 +213,8 @@ def test_gpu_sgbm_bit_exact():
                        ((tiny[:1], tiny[1:]), {}),
                        ((L[:1, :, :301], R[:1, :, :301]), dict(num_disp=64, block=5, P1=200,
                                                                P2=800)),
+                       ((L[:1, :120, :200], R[:1, :120, :200]), dict(block=3)),
+                       ((L[:1, :60, :150], R[:1, :60, :150]), dict(block=21)),
                        ((L[:1, :101], R[:1, :101]), dict(min_disp=3, block=7))):
         kw = dict(dict(min_disp=0, num_disp=32, block=11, P1=968, P2=3872), **kw)
         d, _ = vofront.sgbm(_dev(l), _dev(r), **kw, f32=False)
