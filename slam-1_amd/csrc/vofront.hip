@@ -309,10 +309,16 @@ __global__ __launch_bounds__(kBS) void k_lk_scharr(LkGeom g, int l, const uint8_
   der[(size_t)n * g.img_bytes + g.off[l] + (long long)y * g.pitch[l] + x] = o;
 }
 
-__device__ __forceinline__ long long wave_sum64(long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Exact wave sum of per-lane int32 partials whose 16-lane row sums fit int32
+// (|lane partial| <= 4 * 8160 * 4080 = 133M, so |row sum| < 2^31): DPP sums
+// inside each 16-lane row, then the four row sums added in 64 bits.
+__device__ __forceinline__ long long wave_sum_i32(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return (long long)__builtin_amdgcn_readlane(v, 0) + (long long)__builtin_amdgcn_readlane(v, 16) +
+         (long long)__builtin_amdgcn_readlane(v, 32) + (long long)__builtin_amdgcn_readlane(v, 48);
 }
 
 __device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
@@ -411,9 +417,9 @@ __global__ __launch_bounds__(kBS) void k_lk_track(LkGeom g, LkArgs a) {
         s22 += Iy[k] * Iy[k];
       }
     }
-    const float A11 = (float)wave_sum64(s11) * FLT_SCALE;
-    const float A12 = (float)wave_sum64(s12) * FLT_SCALE;
-    const float A22 = (float)wave_sum64(s22) * FLT_SCALE;
+    const float A11 = (float)wave_sum_i32(s11) * FLT_SCALE;
+    const float A12 = (float)wave_sum_i32(s12) * FLT_SCALE;
+    const float A22 = (float)wave_sum_i32(s22) * FLT_SCALE;
     float D = A11 * A22 - A12 * A12;
     const float dd = A11 - A22;
     const float minEig = (A22 + A11 - sqrtf(dd * dd + 4.f * A12 * A12)) / (float)(2 * area);
@@ -448,8 +454,8 @@ __global__ __launch_bounds__(kBS) void k_lk_track(LkGeom g, LkArgs a) {
           b2 += diff * Iy[k];
         }
       }
-      const float fb1 = (float)wave_sum64(b1) * FLT_SCALE;
-      const float fb2 = (float)wave_sum64(b2) * FLT_SCALE;
+      const float fb1 = (float)wave_sum_i32(b1) * FLT_SCALE;
+      const float fb2 = (float)wave_sum_i32(b2) * FLT_SCALE;
       const float dx = (A12 * fb2 - A22 * fb1) * D;
       const float dy = (A12 * fb1 - A11 * fb2) * D;
       nx += dx;
@@ -487,7 +493,7 @@ __global__ __launch_bounds__(kBS) void k_lk_track(LkGeom g, LkArgs a) {
           e += diff < 0 ? -diff : diff;
         }
       }
-      er = (float)wave_sum64(e) * 1.f / (float)(32 * area);
+      er = (float)wave_sum_i32(e) * 1.f / (float)(32 * area);
     }
   }
   if (lane == 0) {
