@@ -160,7 +160,11 @@ int slam_vo_estimate_pose(const double* d_q1, const double* d_q2, const double* 
                           const double* d_Q2, const int32_t* d_count, int cap, int batch,
                           const double* d_P, uint64_t seed, int item0, int max_iter,
                           int lm_iters, int early_stop, double* d_pose, int32_t* d_best,
-                          int32_t* d_ntried, double* d_err, void* stream);
+                          int32_t* d_ntried, double* d_err, void* d_ws, size_t ws_bytes,
+                          void* stream);
+/* Workspace of slam_vo_estimate_pose: every hypothesis' dof and error
+ * (the error is np.sum's order over the pair norms: 8192-chunks of pairwise sums). */
+int slam_vo_pose_workspace_bytes(int batch, int max_iter, size_t* bytes);
 
 /* reprojection_residuals(dof, q1, q2, Q1, Q2) (visual_odometry.py:65-81) for
  * one dof per item: d_dof [batch][6]; d_res [batch][4 * cap], the first

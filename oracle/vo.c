@@ -14,8 +14,12 @@
  *     from splitmix64 seeded with seed ^ (item * C1) ^ (h * C2);
  *   - LM with the analytic Jacobian from dof = 0 on the sample (lambda 1e-3,
  *     x0.1 / x10, Marquardt diagonal), lm_iters iterations;
- *   - error = sum_k sqrt(f[2k]^2 + f[2k+1]^2), k ascending: the reshape((2N, 2))
- *     of :144-145 pairs CONSECUTIVE entries of the flat f;
+ *   - error = np.sum(np.linalg.norm(f.reshape((2N, 2)), axis=1)) (:144-146): the
+ *     reshape pairs CONSECUTIVE entries of the flat f, each norm is
+ *     sqrt(a*a + b*b), and the sum follows numpy's order for a contiguous
+ *     float64 array: chunks of 8192 added in sequence, each chunk a pairwise sum
+ *     (blocks of <= 128 with 8 accumulators, halves split at multiples of 8);
+ *     checked bit for bit against np.sum in tests/test_vo.py;
  *   - the sequential selection of :147-154 (strict <, early stop after
  *     early_stop non-improving hypotheses); no improvement -> dof = 0.
  * The converged LM optimum is cross-checked against scipy least_squares(lm)
@@ -23,6 +27,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "pose_util.h"
@@ -185,6 +190,35 @@ void oracle_vo_hypothesis(const double* q1, const double* q2, const double* Q1, 
   }
 }
 
+/* numpy's pairwise sum (loops_utils.h: pairwise_sum, PW_BLOCKSIZE 128) */
+static double pw_sum(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  if (n <= 128) {
+    double r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_sum(a, n2) + pw_sum(a + n2, n - n2);
+}
+
+/* np.sum of a contiguous float64 array: buffered reduction in chunks of 8192 */
+double oracle_np_sum(const double* a, int n) {
+  double r = 0.0;
+  for (int c = 0; c < n; c += 8192) r += pw_sum(a + c, n - c < 8192 ? n - c : 8192);
+  return r;
+}
+
 /* estimate_pose (:135-157).  Returns the selected hypothesis index (-1 if none);
  * pose <- its dof; *ntried <- hypotheses the sequential loop evaluates;
  * errs[h] (optional, max_iter) <- every hypothesis' error. */
@@ -198,17 +232,18 @@ int oracle_vo_estimate_pose(const double* q1, const double* q2, const double* Q1
   if (N <= 0) return -1;
   double mn = INFINITY;
   int best = -1, early = 0;
+  double* nrm = (double*)malloc(sizeof(double) * 2 * (size_t)N);
   for (int h = 0; h < max_iter; ++h) {
     double pp[6], R[9];
     int idx[VO_SAMPLE];
     oracle_vo_hypothesis(q1, q2, Q1, Q2, N, P, seed, item, h, lm_iters, pp, idx);
     rodrigues(pp, R);
-    double e = 0.0;
     for (int k = 0; k < 2 * N; ++k) {
       const double f0 = elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k);
       const double f1 = elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k + 1);
-      e += sqrt(f0 * f0 + f1 * f1);
+      nrm[k] = sqrt(f0 * f0 + f1 * f1);
     }
+    const double e = oracle_np_sum(nrm, 2 * N);
     if (errs) errs[h] = e;
     if (*ntried) continue;  /* sequential loop already stopped: only record errs */
     if (e < mn) {
@@ -221,6 +256,7 @@ int oracle_vo_estimate_pose(const double* q1, const double* q2, const double* Q1
     }
     if (early == early_stop) *ntried = h + 1;
   }
+  free(nrm);
   if (!*ntried) *ntried = max_iter;
   *err = mn;
   return best;

@@ -575,107 +575,225 @@ __device__ inline double vo_elem(const double p[6], const double R[9], const dou
   return uv[row - 2] - q2[2 * col + row - 2];
 }
 
-__global__ __launch_bounds__(kVoWG) void k_vo_pose(
+// Hypothesis h of pair b: LM on its 6-point sample from dof = 0 -> ws_pp[b][h]
+__global__ __launch_bounds__(kVoWG) void k_vo_hyp(
     const double* __restrict__ q1a, const double* __restrict__ q2a, const double* __restrict__ Q1a,
     const double* __restrict__ Q2a, const int32_t* __restrict__ count, int cap,
     const double* __restrict__ Pg, uint64_t seed, int item0, int max_iter, int lm_iters,
-    int early_stop, double* __restrict__ pose, int32_t* __restrict__ best_out,
-    int32_t* __restrict__ ntried, double* __restrict__ err_out) {
-  __shared__ double hp[kVoWG][6];
-  __shared__ double herr[kVoWG];
+    double* __restrict__ ws_pp) {
   const int b = blockIdx.x, h = threadIdx.x;
   const int N = min(max(count[b], 0), cap);
+  if (N <= 0 || h >= max_iter) return;
   const double* q1 = q1a + (size_t)b * cap * 2;
   const double* q2 = q2a + (size_t)b * cap * 2;
   const double* Q1 = Q1a + (size_t)b * cap * 3;
   const double* Q2 = Q2a + (size_t)b * cap * 3;
   double P[12];
   for (int i = 0; i < 12; ++i) P[i] = Pg[i];
-  if (N > 0 && h < max_iter) {
-    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
-    double sQ1[kVoSample][3], sQ2[kVoSample][3], sq1[kVoSample][2], sq2[kVoSample][2];
-    for (int k = 0; k < kVoSample; ++k) {
-      const int v = (int)((splitmix64(s) >> 32) % (uint64_t)N);  // with replacement
-      for (int c = 0; c < 3; ++c) {
-        sQ1[k][c] = Q1[3 * v + c];
-        sQ2[k][c] = Q2[3 * v + c];
-      }
-      for (int c = 0; c < 2; ++c) {
-        sq1[k][c] = q1[2 * v + c];
-        sq2[k][c] = q2[2 * v + c];
-      }
+  uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+               ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+  double sQ1[kVoSample][3], sQ2[kVoSample][3], sq1[kVoSample][2], sq2[kVoSample][2];
+  for (int k = 0; k < kVoSample; ++k) {
+    const int v = (int)((splitmix64(s) >> 32) % (uint64_t)N);  // with replacement
+    for (int c = 0; c < 3; ++c) {
+      sQ1[k][c] = Q1[3 * v + c];
+      sQ2[k][c] = Q2[3 * v + c];
     }
-    // LM on the sample from dof = 0 (Marquardt diagonal, lambda x0.1 / x10)
-    double pp[6] = {0, 0, 0, 0, 0, 0}, lam = 1e-3, R[9];
-    for (int it = 0; it < lm_iters; ++it) {
-      rodrigues(pp, R);
-      double H[21] = {0}, g[6] = {0}, cost = 0.0;
-      for (int k = 0; k < kVoSample; ++k) {
-        double r[4], J[4][6];
-        vo_residual<true>(pp, R, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
-        for (int a = 0; a < 4; ++a) {
-          int m = 0;
-          for (int i = 0; i < 6; ++i) {
-            for (int j = 0; j <= i; ++j) H[m++] += J[a][i] * J[a][j];
-            g[i] += J[a][i] * r[a];
-          }
-          cost += r[a] * r[a];
-        }
-      }
-      double d[6], pn[6], Rn[9];
-      if (!solve6(H, g, lam, d)) {
-        lam = fmin(lam * 10.0, 1e12);
-        continue;
-      }
-      for (int i = 0; i < 6; ++i) pn[i] = pp[i] + d[i];
-      rodrigues(pn, Rn);
-      double cn = 0.0;
-      for (int k = 0; k < kVoSample; ++k) {
-        double r[4], J[4][6];
-        vo_residual<false>(pn, Rn, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
-        cn += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
-      }
-      if (cn < cost) {
-        for (int i = 0; i < 6; ++i) pp[i] = pn[i];
-        lam = fmax(lam * 0.1, 1e-12);
-      } else {
-        lam = fmin(lam * 10.0, 1e12);
-      }
+    for (int c = 0; c < 2; ++c) {
+      sq1[k][c] = q1[2 * v + c];
+      sq2[k][c] = q2[2 * v + c];
     }
-    // error over all points: sum_k |(f[2k], f[2k+1])| in order
+  }
+  // LM on the sample from dof = 0 (Marquardt diagonal, lambda x0.1 / x10)
+  double pp[6] = {0, 0, 0, 0, 0, 0}, lam = 1e-3, R[9];
+  for (int it = 0; it < lm_iters; ++it) {
     rodrigues(pp, R);
-    double e = 0.0;
-    for (int k = 0; k < 2 * N; ++k) {
-      const double f0 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k);
-      const double f1 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * k + 1);
-      e += sqrt(f0 * f0 + f1 * f1);
-    }
-    for (int i = 0; i < 6; ++i) hp[h][i] = pp[i];
-    herr[h] = e;
-  }
-  __syncthreads();
-  if (h == 0) {
-    // the sequential loop of :138-154 over the hypotheses in order
-    double mn = INFINITY;
-    int best = -1, tried = 0, early = 0;
-    if (N > 0)
-      for (int k = 0; k < max_iter; ++k) {
-        tried = k + 1;
-        if (herr[k] < mn) {
-          mn = herr[k];
-          best = k;
-          early = 0;
-        } else {
-          ++early;
+    double H[21] = {0}, g[6] = {0}, cost = 0.0;
+    for (int k = 0; k < kVoSample; ++k) {
+      double r[4], J[4][6];
+      vo_residual<true>(pp, R, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+      for (int a = 0; a < 4; ++a) {
+        int m = 0;
+        for (int i = 0; i < 6; ++i) {
+          for (int j = 0; j <= i; ++j) H[m++] += J[a][i] * J[a][j];
+          g[i] += J[a][i] * r[a];
         }
-        if (early == early_stop) break;
+        cost += r[a] * r[a];
       }
-    for (int i = 0; i < 6; ++i) pose[6 * b + i] = best >= 0 ? hp[best][i] : 0.0;
-    best_out[b] = best;
-    ntried[b] = tried;
-    err_out[b] = mn;
+    }
+    double d[6], pn[6], Rn[9];
+    if (!solve6(H, g, lam, d)) {
+      lam = fmin(lam * 10.0, 1e12);
+      continue;
+    }
+    for (int i = 0; i < 6; ++i) pn[i] = pp[i] + d[i];
+    rodrigues(pn, Rn);
+    double cn = 0.0;
+    for (int k = 0; k < kVoSample; ++k) {
+      double r[4], J[4][6];
+      vo_residual<false>(pn, Rn, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+      cn += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    }
+    if (cn < cost) {
+      for (int i = 0; i < 6; ++i) pp[i] = pn[i];
+      lam = fmax(lam * 0.1, 1e-12);
+    } else {
+      lam = fmin(lam * 10.0, 1e12);
+    }
   }
+  for (int i = 0; i < 6; ++i) ws_pp[((size_t)b * max_iter + h) * 6 + i] = pp[i];
+}
+
+// Error of hypothesis h of pair b over all points (:144-146):
+// np.sum(np.linalg.norm(f.reshape((2N, 2)), axis=1)) in numpy's order: chunks
+// of 8192 norms summed in sequence, each chunk a pairwise sum (leaves of <= 128
+// with 8 accumulators; halves split at multiples of 8).  One workgroup: the
+// norms of a chunk in LDS (one pass of all lanes), the leaves summed in
+// parallel, the tree combined by one lane in the recursion's order.
+constexpr int kErrWG = 256;
+constexpr int kNpChunk = 8192;
+constexpr int kMaxLeaves = 160;
+
+__device__ __forceinline__ double leaf_sum(const double* a, int n) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+    r0 += a[i]; r1 += a[i + 1]; r2 += a[i + 2]; r3 += a[i + 3];
+    r4 += a[i + 4]; r5 += a[i + 5]; r6 += a[i + 6]; r7 += a[i + 7];
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+__global__ __launch_bounds__(kErrWG) void k_vo_err(
+    const double* __restrict__ q1a, const double* __restrict__ q2a, const double* __restrict__ Q1a,
+    const double* __restrict__ Q2a, const int32_t* __restrict__ count, int cap,
+    const double* __restrict__ Pg, int max_iter, const double* __restrict__ ws_pp,
+    double* __restrict__ ws_err) {
+  extern __shared__ double nrm[];  // min(2N, kNpChunk) norms of the current chunk
+  __shared__ double lsum[kMaxLeaves];
+  __shared__ int llo[kMaxLeaves], lnn[kMaxLeaves];
+  __shared__ int nleaves;
+  // thread 0's recursion stacks live in LDS (dynamically indexed registers
+  // would go to scratch)
+  __shared__ int st_lo[32], st_n[32], fs[32];
+  __shared__ double vals[32];
+  const int h = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int N = min(max(count[b], 0), cap);
+  if (N <= 0) return;
+  const double* q1 = q1a + (size_t)b * cap * 2;
+  const double* q2 = q2a + (size_t)b * cap * 2;
+  const double* Q1 = Q1a + (size_t)b * cap * 3;
+  const double* Q2 = Q2a + (size_t)b * cap * 3;
+  double P[12], pp[6], R[9];
+  for (int i = 0; i < 12; ++i) P[i] = Pg[i];
+  for (int i = 0; i < 6; ++i) pp[i] = ws_pp[((size_t)b * max_iter + h) * 6 + i];
+  rodrigues(pp, R);
+  const int M = 2 * N;
+  double total = 0.0;
+  for (int c0 = 0; c0 < M; c0 += kNpChunk) {
+    const int n = min(kNpChunk, M - c0);
+    for (int k = t; k < n; k += kErrWG) {
+      const int kk = c0 + k;
+      const double f0 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * kk);
+      const double f1 = vo_elem(pp, R, P, Q1, Q2, q1, q2, N, 2 * kk + 1);
+      nrm[k] = sqrt(f0 * f0 + f1 * f1);
+    }
+    if (t == 0) {  // leaves of pairwise_sum(nrm, n), left to right
+      int sp = 0, nl = 0;
+      st_lo[sp] = 0;
+      st_n[sp++] = n;
+      while (sp > 0) {
+        --sp;
+        const int lo = st_lo[sp], m = st_n[sp];
+        if (m <= 128) {
+          llo[nl] = lo;
+          lnn[nl++] = m;
+        } else {
+          int m2 = m / 2;
+          m2 -= m2 % 8;
+          st_lo[sp] = lo + m2;  // right half below the left one
+          st_n[sp++] = m - m2;
+          st_lo[sp] = lo;
+          st_n[sp++] = m2;
+        }
+      }
+      nleaves = nl;
+    }
+    __syncthreads();
+    for (int i = t; i < nleaves; i += kErrWG) lsum[i] = leaf_sum(nrm + llo[i], lnn[i]);
+    __syncthreads();
+    if (t == 0) {  // combine in the recursion's order (post-order, explicit stacks)
+      int* fn = st_n;  // the leaf stacks are free again
+      int fp = 0, next = 0, vp = 0;
+      fn[fp] = n;
+      fs[fp++] = 0;
+      while (fp > 0) {
+        const int m = fn[fp - 1];
+        if (m <= 128) {
+          --fp;
+          vals[vp++] = lsum[next++];
+          continue;
+        }
+        int m2 = m / 2;
+        m2 -= m2 % 8;
+        if (fs[fp - 1] == 0) {
+          fs[fp - 1] = 1;
+          fn[fp] = m2;
+          fs[fp++] = 0;
+        } else if (fs[fp - 1] == 1) {
+          fs[fp - 1] = 2;
+          fn[fp] = m - m2;
+          fs[fp++] = 0;
+        } else {
+          --fp;
+          const double r = vals[--vp];
+          const double l = vals[--vp];
+          vals[vp++] = l + r;
+        }
+      }
+      total += vals[0];
+    }
+    __syncthreads();
+  }
+  if (t == 0) ws_err[(size_t)b * max_iter + h] = total;
+}
+
+// the sequential loop of :138-154 over the hypotheses' errors in order
+__global__ void k_vo_select(const int32_t* __restrict__ count, int cap, int batch, int max_iter,
+                            int early_stop, const double* __restrict__ ws_pp,
+                            const double* __restrict__ ws_err, double* __restrict__ pose,
+                            int32_t* __restrict__ best_out, int32_t* __restrict__ ntried,
+                            double* __restrict__ err_out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const int N = min(max(count[b], 0), cap);
+  double mn = INFINITY;
+  int best = -1, tried = 0, early = 0;
+  if (N > 0)
+    for (int k = 0; k < max_iter; ++k) {
+      tried = k + 1;
+      const double e = ws_err[(size_t)b * max_iter + k];
+      if (e < mn) {
+        mn = e;
+        best = k;
+        early = 0;
+      } else {
+        ++early;
+      }
+      if (early == early_stop) break;
+    }
+  for (int i = 0; i < 6; ++i)
+    pose[6 * b + i] = best >= 0 ? ws_pp[((size_t)b * max_iter + best) * 6 + i] : 0.0;
+  best_out[b] = best;
+  ntried[b] = tried;
+  err_out[b] = mn;
 }
 
 // reprojection_residuals(dof, q1, q2, Q1, Q2) (:65-81): f [batch][4 cap], the
@@ -769,12 +887,18 @@ extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32
   return SLAM_OK;
 }
 
+extern "C" int slam_vo_pose_workspace_bytes(int batch, int max_iter, size_t* bytes) {
+  SLAM_REQUIRE(batch >= 0 && max_iter >= 1 && bytes, "slam_vo_pose_workspace_bytes: bad args");
+  *bytes = (size_t)batch * max_iter * 7 * sizeof(double) + 256;
+  return SLAM_OK;
+}
+
 extern "C" int slam_vo_estimate_pose(const double* d_q1, const double* d_q2, const double* d_Q1,
                                      const double* d_Q2, const int32_t* d_count, int cap,
                                      int batch, const double* d_P, uint64_t seed, int item0,
                                      int max_iter, int lm_iters, int early_stop, double* d_pose,
                                      int32_t* d_best, int32_t* d_ntried, double* d_err,
-                                     void* stream) {
+                                     void* d_ws, size_t ws_bytes, void* stream) {
   SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_vo_estimate_pose: bad shape");
   SLAM_REQUIRE(max_iter >= 1 && max_iter <= kVoWG, "slam_vo_estimate_pose: max_iter in [1, %d]",
                kVoWG);
@@ -783,11 +907,26 @@ extern "C" int slam_vo_estimate_pose(const double* d_q1, const double* d_q2, con
   SLAM_REQUIRE(d_q1 && d_q2 && d_Q1 && d_Q2 && d_count && d_P && d_pose && d_best && d_ntried &&
                    d_err,
                "slam_vo_estimate_pose: null pointer");
-  k_vo_pose<<<batch, kVoWG, 0, slam::as_stream(stream)>>>(d_q1, d_q2, d_Q1, d_Q2, d_count, cap,
-                                                         d_P, seed, item0, max_iter, lm_iters,
-                                                         early_stop, d_pose, d_best, d_ntried,
-                                                         d_err);
-  SLAM_LAUNCHED("k_vo_pose");
+  SLAM_REQUIRE(d_ws != nullptr, "slam_vo_estimate_pose: null workspace");
+  size_t need = 0;
+  if (int rc = slam_vo_pose_workspace_bytes(batch, max_iter, &need)) return rc;
+  if (ws_bytes < need) {
+    slam::set_error("slam_vo_estimate_pose: workspace %zu < %zu bytes", ws_bytes, need);
+    return SLAM_ERR_WORKSPACE;
+  }
+  double* ws_pp = static_cast<double*>(d_ws);
+  double* ws_err = ws_pp + (size_t)batch * max_iter * 6;
+  hipStream_t s = slam::as_stream(stream);
+  k_vo_hyp<<<batch, kVoWG, 0, s>>>(d_q1, d_q2, d_Q1, d_Q2, d_count, cap, d_P, seed, item0,
+                                   max_iter, lm_iters, ws_pp);
+  SLAM_LAUNCHED("k_vo_hyp");
+  const size_t lds = sizeof(double) * (size_t)min(2 * cap, kNpChunk);
+  k_vo_err<<<dim3(max_iter, batch), kErrWG, lds, s>>>(d_q1, d_q2, d_Q1, d_Q2, d_count, cap, d_P,
+                                                      max_iter, ws_pp, ws_err);
+  SLAM_LAUNCHED("k_vo_err");
+  k_vo_select<<<(batch + 63) / 64, 64, 0, s>>>(d_count, cap, batch, max_iter, early_stop, ws_pp,
+                                               ws_err, d_pose, d_best, d_ntried, d_err);
+  SLAM_LAUNCHED("k_vo_select");
   return SLAM_OK;
 }
 

@@ -1,6 +1,8 @@
 """Device wrappers for gather / triangulation / PnP (csrc/geometry.hip)."""
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
 
@@ -125,10 +127,13 @@ def vo_estimate_pose(q1, q2, Q1, Q2, count, P, seed=0, item0=0, out=None, stream
         err = torch.zeros((B,), dtype=torch.float64, device=dev)
     else:
         pose, best, ntried, err = out
+    nb = ctypes.c_size_t(0)
+    _lib.call("slam_vo_pose_workspace_bytes", B, prm["max_iter"], ctypes.byref(nb))
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=dev)
     _lib.call("slam_vo_estimate_pose", ptr(q1), ptr(q2), ptr(Q1), ptr(Q2), ptr(count), cap, B,
               ptr(Pt.contiguous()), int(seed) & ((1 << 64) - 1), int(item0), prm["max_iter"],
               prm["lm_iters"], prm["early_stop"], ptr(pose), ptr(best), ptr(ntried), ptr(err),
-              stream_ptr(stream))
+              ptr(ws), nb.value, stream_ptr(stream))
     return pose, best, ntried, err
 
 

@@ -116,6 +116,21 @@ def test_oracle_selection_is_the_sequential_loop(seed):
     assert np.allclose(dof, dof_true, atol=0.05)
 
 
+def test_oracle_error_sum_is_numpy_sum():
+    """The hypothesis error is np.sum over the pair norms (:146): the oracle's
+    sum (and k_vo_err's) follows numpy's order bit for bit."""
+    import ctypes
+
+    import oracle
+
+    f = oracle.lib().oracle_np_sum
+    f.argtypes, f.restype = [ctypes.c_void_p, ctypes.c_int], ctypes.c_double
+    rng = np.random.default_rng(4)
+    for n in list(range(0, 300)) + [1339, 2048, 8192, 8193, 9001, 20000]:
+        a = np.ascontiguousarray(rng.random(n) * rng.choice([1.0, 1e4]))
+        assert f(a.ctypes.data, n) == np.sum(a), n
+
+
 def test_oracle_no_points():
     z2, z3 = np.zeros((0, 2)), np.zeros((0, 3))
     dof, best, ntried, err, _ = og.vo_estimate_pose(z2, z2, z3, z3, P_L)
