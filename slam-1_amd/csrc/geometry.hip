@@ -583,27 +583,32 @@ __global__ __launch_bounds__(kVoWG) void k_vo_hyp(
     double* __restrict__ ws_pp) {
   const int b = blockIdx.x, h = threadIdx.x;
   const int N = min(max(count[b], 0), cap);
-  if (N <= 0 || h >= max_iter) return;
+  if (N <= 0) return;  // uniform: before the barrier
   const double* q1 = q1a + (size_t)b * cap * 2;
   const double* q2 = q2a + (size_t)b * cap * 2;
   const double* Q1 = Q1a + (size_t)b * cap * 3;
   const double* Q2 = Q2a + (size_t)b * cap * 3;
-  double P[12];
-  for (int i = 0; i < 12; ++i) P[i] = Pg[i];
+  // the lane's 6-point sample in LDS ([point][Q1 3, Q2 3, q1 2, q2 2]) and P in
+  // LDS: indexed loads there instead of spilled register arrays
+  __shared__ double smp[kVoWG][kVoSample][10];
+  __shared__ double Ps[12];
+  if (h < 12) Ps[h] = Pg[h];
+  const double* P = Ps;
   uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
                ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
-  double sQ1[kVoSample][3], sQ2[kVoSample][3], sq1[kVoSample][2], sq2[kVoSample][2];
   for (int k = 0; k < kVoSample; ++k) {
     const int v = (int)((splitmix64(s) >> 32) % (uint64_t)N);  // with replacement
+    double* d = smp[h][k];
     for (int c = 0; c < 3; ++c) {
-      sQ1[k][c] = Q1[3 * v + c];
-      sQ2[k][c] = Q2[3 * v + c];
+      d[c] = Q1[3 * v + c];
+      d[3 + c] = Q2[3 * v + c];
     }
     for (int c = 0; c < 2; ++c) {
-      sq1[k][c] = q1[2 * v + c];
-      sq2[k][c] = q2[2 * v + c];
+      d[6 + c] = q1[2 * v + c];
+      d[8 + c] = q2[2 * v + c];
     }
   }
+  __syncthreads();
   // LM on the sample from dof = 0 (Marquardt diagonal, lambda x0.1 / x10)
   double pp[6] = {0, 0, 0, 0, 0, 0}, lam = 1e-3, R[9];
   for (int it = 0; it < lm_iters; ++it) {
@@ -611,7 +616,8 @@ __global__ __launch_bounds__(kVoWG) void k_vo_hyp(
     double H[21] = {0}, g[6] = {0}, cost = 0.0;
     for (int k = 0; k < kVoSample; ++k) {
       double r[4], J[4][6];
-      vo_residual<true>(pp, R, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+      const double* d = smp[h][k];
+      vo_residual<true>(pp, R, P, d, d + 3, d + 6, d + 8, r, J);
       for (int a = 0; a < 4; ++a) {
         int m = 0;
         for (int i = 0; i < 6; ++i) {
@@ -631,7 +637,8 @@ __global__ __launch_bounds__(kVoWG) void k_vo_hyp(
     double cn = 0.0;
     for (int k = 0; k < kVoSample; ++k) {
       double r[4], J[4][6];
-      vo_residual<false>(pn, Rn, P, sQ1[k], sQ2[k], sq1[k], sq2[k], r, J);
+      const double* d = smp[h][k];
+      vo_residual<false>(pn, Rn, P, d, d + 3, d + 6, d + 8, r, J);
       cn += r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
     }
     if (cn < cost) {
@@ -641,7 +648,8 @@ __global__ __launch_bounds__(kVoWG) void k_vo_hyp(
       lam = fmin(lam * 10.0, 1e12);
     }
   }
-  for (int i = 0; i < 6; ++i) ws_pp[((size_t)b * max_iter + h) * 6 + i] = pp[i];
+  if (h < max_iter)
+    for (int i = 0; i < 6; ++i) ws_pp[((size_t)b * max_iter + h) * 6 + i] = pp[i];
 }
 
 // Error of hypothesis h of pair b over all points (:144-146):

@@ -1182,18 +1182,6 @@ __global__ __launch_bounds__(1024) void k_vo_right_qs_3d(
       q2l[2 * q + 1] = by;
       q2r[2 * q] = br;
       q2r[2 * q + 1] = by;
-      float X1[3], X2[3];
-      triangulate_f32(ax, ay, ar, ay, Pl, Pr, X1);
-      triangulate_f32(bx, by, br, by, Pl, Pr, X2);
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        Q1[3 * q + k] = X1[k];
-        Q2[3 * q + k] = X2[k];
-        if (Q1_64) {
-          Q1_64[3 * q + k] = (double)X1[k];
-          Q2_64[3 * q + k] = (double)X2[k];
-        }
-      }
       if (q1l64) {
         q1l64[2 * q] = ax;
         q1l64[2 * q + 1] = ay;
@@ -1210,7 +1198,8 @@ __global__ __launch_bounds__(kBS) void k_triangulate_f32(const float* __restrict
                                                          const int32_t* __restrict__ count,
                                                          int cap, const double* __restrict__ Pl,
                                                          const double* __restrict__ Pr,
-                                                         float* __restrict__ X) {
+                                                         float* __restrict__ X,
+                                                         double* __restrict__ X64) {
   const int b = blockIdx.y;
   const int n = min(max(count[b], 0), cap);
   const int k = blockIdx.x * kBS + threadIdx.x;
@@ -1221,6 +1210,11 @@ __global__ __launch_bounds__(kBS) void k_triangulate_f32(const float* __restrict
   X[3 * o] = x[0];
   X[3 * o + 1] = x[1];
   X[3 * o + 2] = x[2];
+  if (X64) {
+    X64[3 * o] = (double)x[0];
+    X64[3 * o + 1] = (double)x[1];
+    X64[3 * o + 2] = (double)x[2];
+  }
 }
 
 FastGeom fast_geom(int H, int W, int stride, int th, int tw, int thr, int per_tile) {
@@ -1432,10 +1426,17 @@ extern "C" int slam_vo_right_qs_3d(const float* d_tp1, const float* d_tp2, const
                "slam_vo_right_qs_3d: null pointer");
   SLAM_REQUIRE(!!d_q1l64 == !!d_q2l64 && !!d_Q1_64 == !!d_Q2_64,
                "slam_vo_right_qs_3d: f64 outputs come in pairs");
-  k_vo_right_qs_3d<<<batch, 1024, 0, slam::as_stream(stream)>>>(
+  hipStream_t s = slam::as_stream(stream);
+  k_vo_right_qs_3d<<<batch, 1024, 0, s>>>(
       d_tp1, d_tp2, d_cnt, cap, d_disp, disp1_stride, disp2_offset, H, W, min_disp, max_disp, d_Pl,
       d_Pr, d_q1l, d_q1r, d_q2l, d_q2r, d_Q1, d_Q2, d_q1l64, d_q2l64, d_Q1_64, d_Q2_64, d_count);
   SLAM_LAUNCHED("k_vo_right_qs_3d");
+  // calc_3d over the kept points: one thread per point (count read on the device)
+  const dim3 grid((cap + kBS - 1) / kBS, batch);
+  k_triangulate_f32<<<grid, kBS, 0, s>>>(d_q1l, d_q1r, d_count, cap, d_Pl, d_Pr, d_Q1, d_Q1_64);
+  SLAM_LAUNCHED("k_triangulate_f32");
+  k_triangulate_f32<<<grid, kBS, 0, s>>>(d_q2l, d_q2r, d_count, cap, d_Pl, d_Pr, d_Q2, d_Q2_64);
+  SLAM_LAUNCHED("k_triangulate_f32");
   return SLAM_OK;
 }
 
@@ -1447,7 +1448,7 @@ extern "C" int slam_triangulate_f32(const float* d_ptl, const float* d_ptr, cons
   SLAM_REQUIRE(d_ptl && d_ptr && d_count && d_Pl && d_Pr && d_X,
                "slam_triangulate_f32: null pointer");
   k_triangulate_f32<<<dim3((cap + kBS - 1) / kBS, batch), kBS, 0, slam::as_stream(stream)>>>(
-      d_ptl, d_ptr, d_count, cap, d_Pl, d_Pr, d_X);
+      d_ptl, d_ptr, d_count, cap, d_Pl, d_Pr, d_X, nullptr);
   SLAM_LAUNCHED("k_triangulate_f32");
   return SLAM_OK;
 }
