@@ -607,6 +607,7 @@ struct RawCell<4> {
 // K1: per (image, row, 64-column band): prefilter + BT pixel costs + horizontal
 // 11-sum (replicated at x = 0, W1-1) -> hs[y][x][d]
 constexpr int kHsBand = 64;
+constexpr int kHsRows = 4;
 
 template <int D>
 __global__ __launch_bounds__(kBS) void k_sgbm_hsum(const uint8_t* __restrict__ left,
@@ -615,7 +616,7 @@ __global__ __launch_bounds__(kBS) void k_sgbm_hsum(const uint8_t* __restrict__ l
   constexpr int kMaxWin = kHsBand + 20 + 64 + D + 4;  // min_disp <= 64, block <= 21
   __shared__ uint8_t ch[4][4][kMaxWin];  // [L0,L1,R0,R1][v, lo, hi, -][col]
   __shared__ int16_t pc[(kHsBand + 20) * D];
-  const int band = blockIdx.x, y = blockIdx.y, n = blockIdx.z, t = threadIdx.x;
+  const int band = blockIdx.x, n = blockIdx.z, t = threadIdx.x;
   const int x0 = band * kHsBand, xe = min(x0 + kHsBand, g.W1);
   const int SW2 = g.SW2;
   // pixel-cost columns (relative to minX1), clamped: [max(x0 - SW2, 0), min(xe + SW2, W1))
@@ -625,66 +626,72 @@ __global__ __launch_bounds__(kBS) void k_sgbm_hsum(const uint8_t* __restrict__ l
   const int whi = min(pc_hi + g.minX1 + 1, g.W);
   const int nw = whi - wlo;
   const uint8_t* img[2] = {left + (size_t)n * g.H * g.stride, right + (size_t)n * g.H * g.stride};
-  const int yn = y > 0 ? y - 1 : y, ys = y < g.H - 1 ? y + 1 : y;
-  // channel values over [wlo - 1, whi + 1) are needed for the BT min/max; compute v on
-  // [wlo - 1, whi + 1) into a staging pass (index c = x - wlo + 1)
   __shared__ uint8_t raw[4][kMaxWin + 2];
-  for (int i = t; i < 2 * (nw + 2); i += kBS) {
-    const int im = i / (nw + 2), c = i % (nw + 2), x = wlo - 1 + c;
-    uint8_t v0 = 15, v1 = 15;
-    if (x >= 1 && x < g.W - 1) {
-      const uint8_t* r = img[im] + (size_t)y * g.stride;
-      const uint8_t* rn = img[im] + (size_t)yn * g.stride;
-      const uint8_t* rs = img[im] + (size_t)ys * g.stride;
-      int v = (r[x + 1] - r[x - 1]) * 2 + rn[x + 1] - rn[x - 1] + rs[x + 1] - rs[x - 1];
-      v = min(max(v, -15), 15);
-      v0 = (uint8_t)(v + 15);
-      v1 = r[x];
+  // kHsRows rows per workgroup (fewer, longer workgroups: the per-row work is small)
+  const int y_end = min((int)(blockIdx.y + 1) * kHsRows, g.H);
+  for (int y = blockIdx.y * kHsRows; y < y_end; ++y) {
+    const int yn = y > 0 ? y - 1 : y, ys = y < g.H - 1 ? y + 1 : y;
+    // channel values over [wlo - 1, whi + 1) are needed for the BT min/max; compute v on
+    // [wlo - 1, whi + 1) into a staging pass (index c = x - wlo + 1)
+    for (int i = t; i < 2 * (nw + 2); i += kBS) {
+      const int im = i / (nw + 2), c = i % (nw + 2), x = wlo - 1 + c;
+      uint8_t v0 = 15, v1 = 15;
+      if (x >= 1 && x < g.W - 1) {
+        const uint8_t* r = img[im] + (size_t)y * g.stride;
+        const uint8_t* rn = img[im] + (size_t)yn * g.stride;
+        const uint8_t* rs = img[im] + (size_t)ys * g.stride;
+        int v = (r[x + 1] - r[x - 1]) * 2 + rn[x + 1] - rn[x - 1] + rs[x + 1] - rs[x - 1];
+        v = min(max(v, -15), 15);
+        v0 = (uint8_t)(v + 15);
+        v1 = r[x];
+      }
+      raw[2 * im][c] = v0;
+      raw[2 * im + 1][c] = v1;
     }
-    raw[2 * im][c] = v0;
-    raw[2 * im + 1][c] = v1;
-  }
-  __syncthreads();
-  for (int i = t; i < 4 * nw; i += kBS) {
-    const int k = i / nw, c = i % nw, x = wlo + c;
-    const int v = raw[k][c + 1];
-    const int vl = x > 0 ? (v + raw[k][c]) / 2 : v;
-    const int vr = x < g.W - 1 ? (v + raw[k][c + 2]) / 2 : v;
-    ch[k][0][c] = (uint8_t)v;
-    ch[k][1][c] = (uint8_t)min(min(vl, vr), v);
-    ch[k][2][c] = (uint8_t)max(max(vl, vr), v);
-  }
-  __syncthreads();
-  const int npc = pc_hi - pc_lo;
-  for (int i = t; i < npc * D; i += kBS) {
-    const int xc = pc_lo + i / D, d = i % D;
-    const int xa = xc + g.minX1, xr = xa - (d + g.minD);
-    const int cl = xa - wlo, cr = xr - wlo;
-    int cost = 0;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int u = ch[c][0][cl], u0 = ch[c][1][cl], u1 = ch[c][2][cl];
-      const int v = ch[2 + c][0][cr], v0 = ch[2 + c][1][cr], v1 = ch[2 + c][2][cr];
-      const int c0 = max(max(0, u - v1), v0 - u);
-      const int c1 = max(max(0, v - u1), u0 - v);
-      cost += min(c0, c1) >> (c ? 2 : 0);
+    __syncthreads();
+    for (int i = t; i < 4 * nw; i += kBS) {
+      const int k = i / nw, c = i % nw, x = wlo + c;
+      const int v = raw[k][c + 1];
+      const int vl = x > 0 ? (v + raw[k][c]) / 2 : v;
+      const int vr = x < g.W - 1 ? (v + raw[k][c + 2]) / 2 : v;
+      ch[k][0][c] = (uint8_t)v;
+      ch[k][1][c] = (uint8_t)min(min(vl, vr), v);
+      ch[k][2][c] = (uint8_t)max(max(vl, vr), v);
     }
-    pc[(xc - pc_lo) * D + d] = (int16_t)cost;
-  }
-  __syncthreads();
-  // sliding horizontal sums: thread = (d, run of kHsBand / (kBS / D) columns)
-  int16_t* out = hs + (size_t)n * g.vol + (size_t)y * g.W1 * D;
-  constexpr int kRun = kHsBand / (kBS / D);
-  const int d = t % D, xr0 = x0 + (t / D) * kRun;
-  if (xr0 < xe) {
-    auto at = [&](int x) { return (int)pc[(min(max(x, 0), g.W1 - 1) - pc_lo) * D + d]; };
-    int s = 0;
-    for (int dx = -SW2; dx <= SW2; ++dx) s += at(xr0 + dx);
-    out[(size_t)xr0 * D + d] = (int16_t)s;
-    for (int x = xr0 + 1; x < min(xr0 + kRun, xe); ++x) {
-      s += at(x + SW2) - at(x - SW2 - 1);
-      out[(size_t)x * D + d] = (int16_t)s;
+    __syncthreads();
+    const int npc = pc_hi - pc_lo;
+    for (int i = t; i < npc * D; i += kBS) {
+      const int xc = pc_lo + i / D, d = i % D;
+      const int xa = xc + g.minX1, xr = xa - (d + g.minD);
+      const int cl = xa - wlo, cr = xr - wlo;
+      int cost = 0;
+  #pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int u = ch[c][0][cl], u0 = ch[c][1][cl], u1 = ch[c][2][cl];
+        const int v = ch[2 + c][0][cr], v0 = ch[2 + c][1][cr], v1 = ch[2 + c][2][cr];
+        const int c0 = max(max(0, u - v1), v0 - u);
+        const int c1 = max(max(0, v - u1), u0 - v);
+        cost += min(c0, c1) >> (c ? 2 : 0);
+      }
+      pc[(xc - pc_lo) * D + d] = (int16_t)cost;
     }
+    __syncthreads();
+    // sliding horizontal sums: thread = (d, run of kHsBand / (kBS / D) columns)
+    int16_t* out = hs + (size_t)n * g.vol + (size_t)y * g.W1 * D;
+    constexpr int kRun = kHsBand / (kBS / D);
+    const int d = t % D, xr0 = x0 + (t / D) * kRun;
+    if (xr0 < xe) {
+      auto at = [&](int x) { return (int)pc[(min(max(x, 0), g.W1 - 1) - pc_lo) * D + d]; };
+      int s = 0;
+      for (int dx = -SW2; dx <= SW2; ++dx) s += at(xr0 + dx);
+      out[(size_t)xr0 * D + d] = (int16_t)s;
+      for (int x = xr0 + 1; x < min(xr0 + kRun, xe); ++x) {
+        s += at(x + SW2) - at(x - SW2 - 1);
+        out[(size_t)x * D + d] = (int16_t)s;
+      }
+    }
+
+    __syncthreads();  // raw / ch / pc are reused by the next row
   }
 }
 
@@ -1030,7 +1037,8 @@ int sgbm_launch(const uint8_t* l, const uint8_t* r, int batch, const SgbmGeom& g
   SgbmGeom gg = g;
   gg.vol = (long long)(vol / 2);  // image stride inside an array (elements)
   if (g.W1 > 0) {
-    k_sgbm_hsum<D><<<dim3((g.W1 + kHsBand - 1) / kHsBand, g.H, batch), kBS, 0, s>>>(l, r, gg, hs);
+    k_sgbm_hsum<D><<<dim3((g.W1 + kHsBand - 1) / kHsBand, (g.H + kHsRows - 1) / kHsRows, batch),
+                     kBS, 0, s>>>(l, r, gg, hs);
     SLAM_LAUNCHED("k_sgbm_hsum");
     k_sgbm_vert<D><<<dim3((g.W1 + 15) / 16, batch), kBS, 0, s>>>(hs, gg, C, L2);
     SLAM_LAUNCHED("k_sgbm_vert");
