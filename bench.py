@@ -542,8 +542,9 @@ def run_vo(args, world, rank):
 
 def sgbm_traffic():
     pmc = pmc_traffic("pmc_traffic_vo.json")
-    return pmc_bytes(pmc, ("k_sgbm_hsum<32>", "k_sgbm_vert<32>", "k_sgbm_diag<32, 1>",
-                           "k_sgbm_diag<32, -1>", "k_sgbm_row<32>", "k_sgbm_median"))
+    if pmc is None:
+        return None
+    return pmc_bytes(pmc, tuple(k for k in pmc["kernels"] if k.startswith("k_sgbm_")))
 
 
 def cpu_baseline_vo(L, R, rig, pairs=1):

@@ -757,8 +757,24 @@ __global__ __launch_bounds__(kBS) void k_sgbm_vert(const int16_t* __restrict__ h
 // K3: diagonal paths.  DX = +1: from (x-1, y-1) (walk x+1, y+1);
 // DX = -1: from (x+1, y-1) (walk x-1, y+1).  One 16-lane row per path.
 template <int D, int DX>
+__device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
+                                               int16_t* __restrict__ Lv);
+
+// both diagonal directions in one launch (blockIdx.z: 0 -> DX = +1 into L1,
+// 1 -> DX = -1 into L3): twice the independent paths in flight
+template <int D>
 __global__ __launch_bounds__(kBS) void k_sgbm_diag(const int16_t* __restrict__ Cv, SgbmGeom g,
-                                                   int16_t* __restrict__ Lv) {
+                                                   int16_t* __restrict__ L1v,
+                                                   int16_t* __restrict__ L3v) {
+  if (blockIdx.z == 0)
+    sgbm_diag_path<D, 1>(Cv, g, L1v);
+  else
+    sgbm_diag_path<D, -1>(Cv, g, L3v);
+}
+
+template <int D, int DX>
+__device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
+                                               int16_t* __restrict__ Lv) {
   constexpr int DPL = D / 16;
   const int n = blockIdx.y, t = threadIdx.x, j = t & 15;
   const int p = blockIdx.x * 16 + (t >> 4);
@@ -1043,10 +1059,9 @@ int sgbm_launch(const uint8_t* l, const uint8_t* r, int batch, const SgbmGeom& g
     k_sgbm_vert<D><<<dim3((g.W1 + 15) / 16, batch), kBS, 0, s>>>(hs, gg, C, L2);
     SLAM_LAUNCHED("k_sgbm_vert");
     const int np = g.W1 + g.H - 1;
-    k_sgbm_diag<D, 1><<<dim3((np + 15) / 16, batch), kBS, 0, s>>>(C, gg, L1);
+    k_sgbm_diag<D><<<dim3((np + 15) / 16, batch, 2), kBS, 0, s>>>(C, gg, L1, L3);
     SLAM_LAUNCHED("k_sgbm_diag");
-    k_sgbm_diag<D, -1><<<dim3((np + 15) / 16, batch), kBS, 0, s>>>(C, gg, L3);
-    SLAM_LAUNCHED("k_sgbm_diag");
+
     const size_t lds = (size_t)4 * g.W * 4;
     k_sgbm_row<D><<<dim3((g.H + 3) / 4, batch), 64, lds, s>>>(C, L1, L2, L3, hs, gg, raw);
     SLAM_LAUNCHED("k_sgbm_row");
