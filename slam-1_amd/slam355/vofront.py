@@ -174,16 +174,30 @@ class StereoVO:
         self.P_l = np.asarray(P_l, np.float64).reshape(3, 4)
         self.P_r = np.asarray(P_r, np.float64).reshape(3, 4)
         self.seed, self.max_iter = seed, max_iter
+        self._side = None
 
     def run(self, left: torch.Tensor, right: torch.Tensor, frame0=0, stream=None):
         require_gpu()
         B = left.shape[0] - 1
         H, W = left.shape[1:]
-        kp, nkp = fast_tiles(left[:B], stream=stream)
-        pyr = LKPyramids(left, stream=stream)
-        p2, st, err = lk_track(pyr, pyr, kp, nkp, prev0=0, next0=1, stream=stream)
-        tp1, tp2, _, ntp = lk_filter(kp, p2, st, err, nkp, H, W, max_error=4.0, stream=stream)
-        _, dispf = sgbm(left, right, **SGBM, stream=stream)
+        main = stream if stream is not None else torch.cuda.current_stream()
+        # SGBM does not depend on FAST / LK: it runs on a side stream meanwhile
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=left.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self._side.wait_event(ready)
+        with torch.cuda.stream(self._side):
+            _, dispf = sgbm(left, right, **SGBM, stream=self._side)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        dispf.record_stream(main)
+        kp, nkp = fast_tiles(left[:B], stream=main)
+        pyr = LKPyramids(left, stream=main)
+        p2, st, err = lk_track(pyr, pyr, kp, nkp, prev0=0, next0=1, stream=main)
+        tp1, tp2, _, ntp = lk_filter(kp, p2, st, err, nkp, H, W, max_error=4.0, stream=main)
+        main.wait_event(done)
+        stream = main
         o = right_qs_3d(tp1, tp2, ntp, dispf, self.P_l, self.P_r, stream=stream)
         pose, best, ntried, perr = geometry.vo_estimate_pose(
             o["q1_l64"], o["q2_l64"], o["Q1_64"], o["Q2_64"], o["count"], self.P_l,
