@@ -352,6 +352,15 @@ __global__ __launch_bounds__(kBS) void k_lk_track(LkGeom g, LkArgs a) {
   const size_t o = (size_t)b * a.cap + pt;
   const float px = a.pts[o * a.pts_stride], py = a.pts[o * a.pts_stride + 1];
   int st = 1;
+  if (!(fabsf(px) < 1e7f) || !(fabsf(py) < 1e7f)) {  // not finite / absurd: not trackable
+    if (lane == 0) {
+      a.out[2 * o] = px;
+      a.out[2 * o + 1] = py;
+      a.status[o] = 0;
+      a.err[o] = 0.f;
+    }
+    return;
+  }
   float er = 0.f, npx = 0.f, npy = 0.f;
   const uint8_t* prevb = a.prev + b * a.pyr_stride;
   const uint8_t* nextb = a.next + b * a.pyr_stride;
@@ -1183,15 +1192,26 @@ __global__ __launch_bounds__(1024) void k_vo_right_qs_3d(
       bx = tp2[2 * o];
       by = tp2[2 * o + 1];
       // q.astype(int): truncation toward zero; disp.T[x, y] with NumPy's negative wrap
+      // (an index NumPy would reject -- below -W or not finite -- raises IndexError in
+      // the reference; here the point is dropped instead of reading out of bounds)
+      bool inb = true;
       auto look = [&](const float* dm, float qx, float qy) {
+        if (!(fabsf(qx) < 1e9f) || !(fabsf(qy) < 1e9f)) {
+          inb = false;
+          return 0.f;
+        }
         int x = (int)qx, y = (int)qy;
         if (x < 0) x += W;
         if (y < 0) y += H;
+        if (x < 0 || x >= W || y < 0 || y >= H) {
+          inb = false;
+          return 0.f;
+        }
         return dm[(size_t)y * W + x];
       };
       e1 = look(d1, ax, ay);
       e2 = look(d2, bx, by);
-      keep = min_disp < e1 && e1 < max_disp && min_disp < e2 && e2 < max_disp;
+      keep = inb && min_disp < e1 && e1 < max_disp && min_disp < e2 && e2 < max_disp;
     }
     const int s = block_compact(keep, wsum, base);
     if (s >= 0) {

@@ -165,7 +165,8 @@ def test_gpu_lk_bit_exact():
     L, _, _, _ = _frames(3, 640, 480, seed=25)
     pts = [vf.fast_tiles(L[i])[:, :2] for i in range(2)]
     # add border / outside points (status paths)
-    extra = np.array([[0, 0], [639, 479], [-3.5, 10], [700, 200], [2.25, 477.75], [320.5, 0.1]],
+    extra = np.array([[0, 0], [639, 479], [-3.5, 10], [700, 200], [2.25, 477.75], [320.5, 0.1],
+                      [1e8, 5.0], [-40.0, -3e7]],
                      np.float32)
     pts = [np.concatenate([p, extra]) for p in pts]
     cap = max(len(p) for p in pts)
