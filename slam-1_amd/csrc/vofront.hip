@@ -765,32 +765,40 @@ __global__ __launch_bounds__(kBS) void k_sgbm_vert(const int16_t* __restrict__ h
 
 // K3: diagonal paths.  DX = +1: from (x-1, y-1) (walk x+1, y+1);
 // DX = -1: from (x+1, y-1) (walk x-1, y+1).  One 16-lane row per path.
-template <int D, int DX>
-__device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
-                                               int16_t* __restrict__ Lv);
+template <int D, int DX, int DY>
+__device__ __forceinline__ void sgbm_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
+                                          int16_t* __restrict__ Lv);
 
-// both diagonal directions in one launch (blockIdx.z: 0 -> DX = +1 into L1,
-// 1 -> DX = -1 into L3): twice the independent paths in flight
+// three path directions in one launch (blockIdx.z): 0 -> from (x-1, y-1) into
+// L1, 1 -> from (x+1, y-1) into L3, 2 -> from (x+1, y) (right to left along
+// the row) into L4: all independent paths in flight together
 template <int D>
-__global__ __launch_bounds__(kBS) void k_sgbm_diag(const int16_t* __restrict__ Cv, SgbmGeom g,
-                                                   int16_t* __restrict__ L1v,
-                                                   int16_t* __restrict__ L3v) {
+__global__ __launch_bounds__(kBS) void k_sgbm_paths(const int16_t* __restrict__ Cv, SgbmGeom g,
+                                                    int16_t* __restrict__ L1v,
+                                                    int16_t* __restrict__ L3v,
+                                                    int16_t* __restrict__ L4v) {
   if (blockIdx.z == 0)
-    sgbm_diag_path<D, 1>(Cv, g, L1v);
+    sgbm_path<D, 1, 1>(Cv, g, L1v);
+  else if (blockIdx.z == 1)
+    sgbm_path<D, -1, 1>(Cv, g, L3v);
   else
-    sgbm_diag_path<D, -1>(Cv, g, L3v);
+    sgbm_path<D, -1, 0>(Cv, g, L4v);
 }
 
-template <int D, int DX>
-__device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
-                                               int16_t* __restrict__ Lv) {
+template <int D, int DX, int DY>
+__device__ __forceinline__ void sgbm_path(const int16_t* __restrict__ Cv, const SgbmGeom& g,
+                                          int16_t* __restrict__ Lv) {
   constexpr int DPL = D / 16;
   const int n = blockIdx.y, t = threadIdx.x, j = t & 15;
   const int p = blockIdx.x * 16 + (t >> 4);
-  const int np = g.W1 + g.H - 1;
+  const int np = DY ? g.W1 + g.H - 1 : g.H;
+  if (blockIdx.x * 16 >= np) return;  // whole workgroup past the paths (uniform)
   const bool live = p < np;
   int x, y;
-  if (p < g.W1) {
+  if (!DY) {  // row p, walked from the right end
+    x = g.W1 - 1;
+    y = p;
+  } else if (p < g.W1) {
     x = DX > 0 ? p : g.W1 - 1 - p;
     y = 0;
   } else {
@@ -798,7 +806,7 @@ __device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, c
     y = p - g.W1 + 1;
   }
   int len = 0;
-  if (live) len = min(DX > 0 ? g.W1 - x : x + 1, g.H - y);
+  if (live) len = DY ? min(DX > 0 ? g.W1 - x : x + 1, g.H - y) : g.W1;
   // the 16 lanes of a row share len; rows of a wave differ, so loop to the wave max
   int lmax = len;
 #pragma unroll
@@ -806,7 +814,7 @@ __device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, c
   const size_t rowst = (size_t)g.W1 * D;
   const int16_t* c = Cv + (size_t)n * g.vol + (size_t)y * rowst + (size_t)x * D + j * DPL;
   int16_t* lo = Lv + (size_t)n * g.vol + (size_t)y * rowst + (size_t)x * D + j * DPL;
-  const long long step = (long long)rowst + (long long)DX * D;
+  const long long step = (long long)DY * rowst + (long long)DX * D;
   int L[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) L[i] = 0;
@@ -830,15 +838,18 @@ __device__ __forceinline__ void sgbm_diag_path(const int16_t* __restrict__ Cv, c
   }
 }
 
-// K4: per 4 rows (one 16-lane row each): left->right path summed with L1..L3
-// (saturated) -> S1, then right->left path, selection, subpixel, right-view
-// disparities and the left-right check -> raw disparity row.
+// K4: per 4 rows (one 16-lane row each), one left->right pass: the left->right
+// path L0 and S = sat16(sat16(L0 + L1 + L2 + L3) + L4), first-minimum argmin
+// by packed-key DPP min, subpixel (neighbours by DPP row shifts in the owner
+// lane), right-view disparities by LDS atomicMin on (cost, -x) keys (ties to
+// the larger x, as the reference's right-to-left visit), then the left-right
+// check -> raw disparity row.
 template <int D>
 __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
                                                  const int16_t* __restrict__ L1v,
                                                  const int16_t* __restrict__ L2v,
                                                  const int16_t* __restrict__ L3v,
-                                                 int16_t* __restrict__ S1v, SgbmGeom g,
+                                                 const int16_t* __restrict__ L4v, SgbmGeom g,
                                                  int16_t* __restrict__ raw) {
   constexpr int DPL = D / 16;
   constexpr int kPFR = 16;  // cells in flight per lane and volume
@@ -862,78 +873,46 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
   const int16_t* l1 = L1v + base;
   const int16_t* l2 = L2v + base;
   const int16_t* l3 = L3v + base;
-  int16_t* s1 = S1v + base;
+  const int16_t* l4 = L4v + base;
   int L[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) L[i] = 0;
   int mp = 0;
-  {
-    RawCell<DPL> rc[kPFR], r1[kPFR], r2[kPFR], r3[kPFR];
-#pragma unroll
-    for (int k = 0; k < kPFR; ++k)
-      if (k < W1) {
-        rc[k].load(c + (size_t)k * D);
-        r1[k].load(l1 + (size_t)k * D);
-        r2[k].load(l2 + (size_t)k * D);
-        r3[k].load(l3 + (size_t)k * D);
-      }
-    for (int x0 = 0; x0 < W1; x0 += kPFR) {
-#pragma unroll
-      for (int k = 0; k < kPFR; ++k) {
-        const int x = x0 + k;
-        if (x < W1) {
-          int C[DPL], a1[DPL], a2[DPL], a3[DPL];
-          rc[k].get(C);
-          r1[k].get(a1);
-          r2[k].get(a2);
-          r3[k].get(a3);
-          const int xn = x + kPFR;
-          if (xn < W1) {
-            rc[k].load(c + (size_t)xn * D);
-            r1[k].load(l1 + (size_t)xn * D);
-            r2[k].load(l2 + (size_t)xn * D);
-            r3[k].load(l3 + (size_t)xn * D);
-          }
-          mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
-          int sv[DPL];
-#pragma unroll
-          for (int i = 0; i < DPL; ++i) sv[i] = sat16(L[i] + a1[i] + a2[i] + a3[i]);
-          store_cell<DPL>(s1 + (size_t)x * D, sv);
-        }
-      }
-    }
-  }
-  // the S1 stores of this row must land before the right->left pass reads them
-  __threadfence_block();
-#pragma unroll
-  for (int i = 0; i < DPL; ++i) L[i] = 0;
-  mp = 0;
-  RawCell<DPL> rc[kPFR], rsv[kPFR];
+  RawCell<DPL> rc[kPFR], r1[kPFR], r2[kPFR], r3[kPFR], r4[kPFR];
 #pragma unroll
   for (int k = 0; k < kPFR; ++k)
     if (k < W1) {
-      rc[k].load(c + (size_t)(W1 - 1 - k) * D);
-      rsv[k].load(s1 + (size_t)(W1 - 1 - k) * D);
+      rc[k].load(c + (size_t)k * D);
+      r1[k].load(l1 + (size_t)k * D);
+      r2[k].load(l2 + (size_t)k * D);
+      r3[k].load(l3 + (size_t)k * D);
+      r4[k].load(l4 + (size_t)k * D);
     }
-  for (int i0 = 0; i0 < W1; i0 += kPFR) {
+  for (int x0 = 0; x0 < W1; x0 += kPFR) {
 #pragma unroll
     for (int k = 0; k < kPFR; ++k) {
-      const int i = i0 + k;
-      if (i < W1) {
-        const int x = W1 - 1 - i;
-        int C[DPL], S[DPL];
+      const int x = x0 + k;
+      if (x < W1) {
+        int C[DPL], a1[DPL], a2[DPL], a3[DPL], a4[DPL];
         rc[k].get(C);
-        rsv[k].get(S);
-        const int in = i + kPFR;
-        if (in < W1) {
-          rc[k].load(c + (size_t)(W1 - 1 - in) * D);
-          rsv[k].load(s1 + (size_t)(W1 - 1 - in) * D);
+        r1[k].get(a1);
+        r2[k].get(a2);
+        r3[k].get(a3);
+        r4[k].get(a4);
+        const int xn = x + kPFR;
+        if (xn < W1) {
+          rc[k].load(c + (size_t)xn * D);
+          r1[k].load(l1 + (size_t)xn * D);
+          r2[k].load(l2 + (size_t)xn * D);
+          r3[k].load(l3 + (size_t)xn * D);
+          r4[k].load(l4 + (size_t)xn * D);
         }
         mp = path_step<DPL>(C, L, mp, g.P1, g.P2);
+        int S[DPL];
         int key = 0x7FFFFFFF;
 #pragma unroll
         for (int q = 0; q < DPL; ++q) {
-          S[q] = sat16(S[q] + L[q]);
+          S[q] = sat16(sat16(L[q] + a1[q] + a2[q] + a3[q]) + a4[q]);
           key = min(key, S[q] * 64 + j * DPL + q);  // first minimum over d
         }
         key = row_min16(key);
@@ -968,6 +947,7 @@ __global__ __launch_bounds__(64) void k_sgbm_row(const int16_t* __restrict__ Cv,
       }
     }
   }
+  __threadfence_block();
   __syncthreads();
   if (!live) return;
   // left-right consistency (disp12MaxDiff 1)
@@ -1068,8 +1048,9 @@ int sgbm_launch(const uint8_t* l, const uint8_t* r, int batch, const SgbmGeom& g
     k_sgbm_vert<D><<<dim3((g.W1 + 15) / 16, batch), kBS, 0, s>>>(hs, gg, C, L2);
     SLAM_LAUNCHED("k_sgbm_vert");
     const int np = g.W1 + g.H - 1;
-    k_sgbm_diag<D><<<dim3((np + 15) / 16, batch, 2), kBS, 0, s>>>(C, gg, L1, L3);
-    SLAM_LAUNCHED("k_sgbm_diag");
+    // L4 (right to left) reuses the horizontal-sum volume, dead after k_sgbm_vert
+    k_sgbm_paths<D><<<dim3((np + 15) / 16, batch, 3), kBS, 0, s>>>(C, gg, L1, L3, hs);
+    SLAM_LAUNCHED("k_sgbm_paths");
 
     const size_t lds = (size_t)4 * g.W * 4;
     k_sgbm_row<D><<<dim3((g.H + 3) / 4, batch), 64, lds, s>>>(C, L1, L2, L3, hs, gg, raw);
