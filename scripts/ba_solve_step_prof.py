@@ -21,4 +21,4 @@ for C, P, k in ((6, 1500, 4), (10, 5000, 6)):
         prob.iterate(1)
         rows.append(prob.t["state"][12:16].cpu().numpy())
     m = np.median(np.array(rows), 0)
-    print(f"C={C}: (a)+barrier {m[0]:.0f} clk, (b) panel {m[1]:.0f} clk, barrier {m[2]:.0f} clk, (c) mfma {m[3]:.0f} clk")
+    print(f"C={C}: (a)+barrier {m[0]:.0f} clk, (b) panel {m[1]:.0f} clk, barrier {m[2]:.0f} clk, (c) mfma {m[3]:.0f} clk  (built with -DSLAM_SOLVE_PROFILE_PANEL: the last two are the panel load and elimination)")

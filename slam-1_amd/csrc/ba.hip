@@ -799,71 +799,79 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
 #ifdef SLAM_SOLVE_PROFILE_STEP
     const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
-    // (b) panel factorisation.  Every participating wave factors the 9x9
-    // diagonal block A_KK = L_K D_K L_K^T redundantly (uniform values, no
-    // cross-lane traffic); then each lane takes one panel row r >= c0 and
-    // solves u = a L_K^-T (u_j = A^{(j)}(r, c0+j), the partially eliminated
-    // entry; for a row inside the panel, r = c0 + m, u_j = L(m, j) D_j for
-    // j < m and u_m = D_m) and l = u D_K^-1.  Rows c0+64w .. +63 go to wave w.
-    const int nw = (n - c0 + 1 + 63) >> 6;  // waves with rows (uniform)
+    // (b) panel factorisation, one panel row per lane: lanes 0..8 of every
+    // participating wave hold the 9 pivot rows r = c0 + m (lower entries),
+    // lanes 9..63 of wave w the rows c0 + 9 + 55 w + (lane - 9) (the rhs row n
+    // included).  Right-looking: at step j the pivot d_j and the column-j
+    // entries of the pivot rows are broadcast with v_readlane, and every lane
+    // eliminates its own row (u_i -= (u_j / d_j) A(c0+i, c0+j)).  Afterwards
+    // u_j is the partially eliminated entry A^{(j)}(r, c0+j), L(r, j) = u_j/d_j.
+    // (Was: every lane factored the whole 9x9 block redundantly, ~3x the
+    // VALU work of this form.)
+    const int nbelow = n + 1 - c0 - kPanelW;             // rows below the panel, rhs included
+    const int nw = max(1, (nbelow + 63 - kPanelW) / (64 - kPanelW));  // uniform
     if (wid < nw) {
-      double A[kPanelW][kPanelW];  // lower triangle of the diagonal block
-#pragma unroll
-      for (int m = 0; m < kPanelW; ++m)
-#pragma unroll
-        for (int i = 0; i <= m; ++i) A[m][i] = Pn[m * kPanelW + i];
-      const int r = c0 + 64 * wid + lane;
-      double u[kPanelW];
+      const bool piv = lane < kPanelW;
+      const int r = piv ? c0 + lane : c0 + kPanelW + (64 - kPanelW) * wid + (lane - kPanelW);
+      const bool valid = r <= n;
       const double* pr = Pn + (r - c0) * kPanelW;
+      double u[kPanelW];
 #pragma unroll
-      for (int j = 0; j < kPanelW; ++j) u[j] = r <= n ? pr[j] : 0.0;
+      for (int j = 0; j < kPanelW; ++j) u[j] = valid && (!piv || j <= lane) ? pr[j] : 0.0;
       double Dinv[kPanelW];
       bool bad = false;
+#ifdef SLAM_SOLVE_PROFILE_PANEL
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t qb1 = __builtin_amdgcn_s_memtime();
+#endif
 #pragma unroll
       for (int j = 0; j < kPanelW; ++j) {
-        const double d = A[j][j];
+        const double d = readlane_d(u[j], j);
         bad |= !(d > 0.0) || !isfinite(d);
         Dinv[j] = rcp_f64(d);
+        const double l = u[j] * Dinv[j];
 #pragma unroll
-        for (int m = j + 1; m < kPanelW; ++m) {
-          const double lmj = A[m][j] * Dinv[j];
-#pragma unroll
-          for (int i = j + 1; i <= m; ++i) A[m][i] = __builtin_fma(-lmj, A[i][j], A[m][i]);
-        }
-#pragma unroll
-        for (int m = j + 1; m < kPanelW; ++m) A[m][j] *= Dinv[j];  // L(m, j)
+        for (int i = j + 1; i < kPanelW; ++i) u[i] = __builtin_fma(-l, readlane_d(u[j], i), u[i]);
       }
-      // right-looking row solve: 9 dependent levels instead of 36
-#pragma unroll
-      for (int i = 0; i < kPanelW; ++i)
-#pragma unroll
-        for (int j = i + 1; j < kPanelW; ++j) u[j] = __builtin_fma(-u[i], A[j][i], u[j]);
-      if (r <= n) {
+#ifdef SLAM_SOLVE_PROFILE_PANEL
+      {
+        double chk = u[kPanelW - 1];
+        __asm__ volatile("" : "+v"(chk));
+        u[kPanelW - 1] = chk;
+      }
+      const uint64_t qb2 = __builtin_amdgcn_s_memtime();
+      if (t == 0 && c0 == 9 * (n / 18)) {
+        p.state[SLAM_BA_ST_SLOTS - 2] = (double)(qb1 - q1);  // replaces barrier / (c)
+        p.state[SLAM_BA_ST_SLOTS - 1] = (double)(qb2 - qb1);
+      }
+#endif
+      // stores grouped so that each lane class takes one exec-mask region
+      if (valid && (wid == 0 || !piv)) {
         double* wl = WL + r * kWLs;
         double* ll = LL + r * kWLs;
+        double* lf = LF + r * (r - 1) / 2 + c0;
+        double lj[kPanelW];
 #pragma unroll
         for (int j = 0; j < kPanelW; ++j) {
+          lj[j] = u[j] * Dinv[j];
           wl[j] = -u[j];
-          ll[j] = u[j] * Dinv[j];
+          ll[j] = lj[j];
         }
         if (r == n) {
 #pragma unroll
           for (int j = 0; j < kPanelW; ++j) Yy[c0 + j] = u[j];
-        } else if (r >= c0 + kPanelW) {
-          double* lf = LF + r * (r - 1) / 2 + c0;
+        } else if (!piv) {
 #pragma unroll
-          for (int j = 0; j < kPanelW; ++j) lf[j] = u[j] * Dinv[j];
-        }
-      }
-      // the panel's own factor rows and D from the diagonal-block factor every
-      // lane holds (one lane stores them: no per-column divergent branches)
-      if (t == 0) {
+          for (int j = 0; j < kPanelW; ++j) lf[j] = lj[j];
+        } else {
+          // pivot row m = lane: D_m and the lower part L(r, c0 + j), j < m
+          double dm = u[0];
 #pragma unroll
-        for (int m = 0; m < kPanelW; ++m) {
-          Dd[c0 + m] = A[m][m];
-          double* lf = LF + (c0 + m) * (c0 + m - 1) / 2 + c0;
+          for (int j = 1; j < kPanelW; ++j) dm = j == lane ? u[j] : dm;
+          Dd[r] = dm;
 #pragma unroll
-          for (int j = 0; j < m; ++j) lf[j] = A[m][j];
+          for (int j = 0; j < kPanelW - 1; ++j)
+            if (j < lane) lf[j] = lj[j];
         }
       }
       if (wid == 0 && lane == 0 && bad) *fail_p = 1;
@@ -909,8 +917,10 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
     if (t == 0 && c0 == 9 * (n / 18)) {
       p.state[12] = (double)(q1 - q0);
       p.state[13] = (double)(q2 - q1);
+#ifndef SLAM_SOLVE_PROFILE_PANEL
       p.state[14] = (double)(q3 - q2);
       p.state[15] = (double)(q4 - q3);
+#endif
     }
 #endif
   }

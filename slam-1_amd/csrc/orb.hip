@@ -33,7 +33,8 @@ constexpr int kOrbWG = 512;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxShapes = 4;
 constexpr int kNMS0 = 29;  // score-map region starts here (needs [30, w-31])
-constexpr int kBl0 = 9;    // blurred region starts here (samples within +-19 of [31, w-32])
+constexpr int kBl0 = 12;   // blurred region starts here (rotated samples within +-18 of [31, w-32])
+constexpr int kFq = (kOrbWG / 64) * 256 * 4;  // FAST survivor queues, bytes
 
 __constant__ int8_t c_pattern[256 * 4];
 __constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
@@ -45,6 +46,7 @@ struct OrbGeom {
   int cand_cap;   // NMS candidates per level (global scratch, worst case 1/4 density)
   int list_cap;   // kept keypoints / retainBest(2n) survivors per level (LDS)
   int lds_a, lds_u, lds_l, lds_s, lds_m;  // byte offsets of the LDS regions
+  int lds_fq, lds_tab;  // FAST queues and resize tables (inside U unless glob)
   int glob;       // level images in global memory (whole images too large for LDS)
   int lvl_bytes;  // global level buffer per image and ping-pong half (glob only)
   int tab_x;      // resize-coefficient slots for x (>= W); y follows
@@ -71,22 +73,23 @@ __device__ __forceinline__ int fdiv(int n, uint32_t m) {
 }
 
 // ------------------------------------------------------------------ FAST
-__device__ __forceinline__ int fast_score(const uint8_t* im, int st, int x, int y) {
-  const uint8_t* c = im + y * st + x;
+// Exact quick reject: any 9 consecutive circle positions contain two
+// adjacent compass points (0,4,8,12), so a corner needs such a pair to be
+// darker (or brighter) than v -/+ t.  p0/p4/p8/p12 are the compass pixels.
+__device__ __forceinline__ bool fast_maybe(int v, int p0, int p4, int p8, int p12) {
+  const int e0 = v - p0, e4 = v - p4, e8 = v - p8, e12 = v - p12;
+  const unsigned dk = (e0 > kFastT ? 1u : 0u) | (e4 > kFastT ? 2u : 0u) |
+                      (e8 > kFastT ? 4u : 0u) | (e12 > kFastT ? 8u : 0u);
+  const unsigned br = (e0 < -kFastT ? 1u : 0u) | (e4 < -kFastT ? 2u : 0u) |
+                      (e8 < -kFastT ? 4u : 0u) | (e12 < -kFastT ? 8u : 0u);
+  const unsigned dk2 = dk & ((dk >> 1) | (dk << 3));  // (0,4) (4,8) (8,12) (12,0)
+  const unsigned br2 = br & ((br >> 1) | (br << 3));
+  return ((dk2 | br2) & 0xFu) != 0u;
+}
+
+// Full segment test + OpenCV cornerScore<16> at c (past the quick reject).
+__device__ __forceinline__ int fast_full(const uint8_t* c, int st) {
   const int v = c[0];
-  // Exact quick reject: any 9 consecutive circle positions contain two
-  // adjacent compass points (0,4,8,12), so a corner needs such a pair to be
-  // darker (or brighter) than v -/+ t.
-  {
-    const int e0 = v - c[3 * st], e4 = v - c[3], e8 = v - c[-3 * st], e12 = v - c[-3];
-    const unsigned dk = (e0 > kFastT ? 1u : 0u) | (e4 > kFastT ? 2u : 0u) |
-                        (e8 > kFastT ? 4u : 0u) | (e12 > kFastT ? 8u : 0u);
-    const unsigned br = (e0 < -kFastT ? 1u : 0u) | (e4 < -kFastT ? 2u : 0u) |
-                        (e8 < -kFastT ? 4u : 0u) | (e12 < -kFastT ? 8u : 0u);
-    const unsigned dk2 = dk & ((dk >> 1) | (dk << 3));  // (0,4) (4,8) (8,12) (12,0)
-    const unsigned br2 = br & ((br >> 1) | (br << 3));
-    if (((dk2 | br2) & 0xFu) == 0u) return 0;
-  }
   int d[16];
   d[0] = v - c[3 * st];
   d[1] = v - c[3 * st + 1];
@@ -216,7 +219,7 @@ struct KP {  // one kept keypoint of the current level (LDS)
 };
 
 template <bool kGlob>
-__global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
+__global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
                                                      float* __restrict__ ws_kp,
                                                      int32_t* __restrict__ ws_oct,
                                                      uint8_t* __restrict__ ws_desc,
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int* hist = reinterpret_cast<int*>(lds + g.lds_m);  // 256 bins of FAST score
   int* ctr = hist + 256;   // 0: candidates, 1: survivors, 2: threshold, 3: kept
-  int* tabx = ctr + 16;    // resize coefficients (tab_x for x, the rest for y)
+  int* tabx = reinterpret_cast<int*>(lds + g.lds_tab);  // resize coefficients (x, then y)
   int* taby = tabx + g.tab_x;
 
   const int tile = blockIdx.x, b = blockIdx.y;
@@ -292,20 +295,36 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
       for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
       __syncthreads();
       const uint32_t mW = div_magic(W);
-      for (int i = t; i < W * H; i += kOrbWG) {
-        const int y = fdiv(i, mW), x = i - y * W;
-        const int cx = tabx[x], cy = taby[y];
-        const int xo = cx >> 9, c1 = cx & 511, c0 = 256 - c1;
-        const int yo = cy >> 9, d1 = cy & 511, d0 = 256 - d1;
-        const uint8_t* r0 = S + yo * SW + xo;
-        int h0 = c0 * r0[0] + (c1 ? c1 * r0[1] : 0);
-        int v = d0 * h0;
-        if (d1) {
-          const uint8_t* r1 = r0 + SW;
-          const int h1 = c0 * r1[0] + (c1 ? c1 * r1[1] : 0);
-          v += d1 * h1;
+      // Four pixels per pass with all LDS reads of the group issued before
+      // any store (the compiler cannot reorder loads over U stores itself).
+      const int WH = W * H;
+      for (int i0 = t; i0 < WH; i0 += 4 * kOrbWG) {
+        int ii[4], cx[4], cy[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ii[q] = min(i0 + q * kOrbWG, WH - 1);
+          const int y = fdiv(ii[q], mW), x = ii[q] - y * W;
+          cx[q] = tabx[x];
+          cy[q] = taby[y];
         }
-        U[i] = (uint8_t)min((v + 32768) >> 16, 255);
+        int p00[4], p01[4], p10[4], p11[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint8_t* r0 = S + (cy[q] >> 9) * SW + (cx[q] >> 9);
+          // the +1 neighbours are only read with a non-zero weight (the
+          // last column / row may sit on the source edge)
+          p00[q] = r0[0];
+          p01[q] = (cx[q] & 511) ? r0[1] : 0;
+          p10[q] = (cy[q] & 511) ? r0[SW] : 0;
+          p11[q] = ((cx[q] & 511) && (cy[q] & 511)) ? r0[SW + 1] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c1 = cx[q] & 511, c0 = 256 - c1;
+          const int d1 = cy[q] & 511, d0 = 256 - d1;
+          const int v = d0 * (c0 * p00[q] + c1 * p01[q]) + d1 * (c0 * p10[q] + c1 * p11[q]);
+          if (i0 + q * kOrbWG < WH) U[ii[q]] = (uint8_t)min((v + 32768) >> 16, 255);
+        }
       }
       __syncthreads();
       if (kGlob) {  // global level buffers: swap roles instead of copying
@@ -327,9 +346,44 @@ __global__ __launch_bounds__(kOrbWG) void k_orb_tile(const uint8_t* __restrict__
     const int SWd = W - 2 * kNMS0, SHd = H - 2 * kNMS0;
     uint8_t* Smap = U;
     const uint32_t mS = div_magic(SWd);
-    for (int i = t; i < SWd * SHd; i += kOrbWG) {
-      const int y = fdiv(i, mS), x = i - y * SWd;
-      Smap[i] = (uint8_t)fast_score(I, W, x + kNMS0, y + kNMS0);
+    // Four pixels per pass: the 20 quick-reject reads of the group are all
+    // issued before any Smap store.  Survivors (~8% of pixels, but present
+    // in ~30% of waves) are queued in a wave-private LDS list (the tail of
+    // U past the score map) and take the full test packed 64 per pass
+    // instead of diverging inside every wave that holds one.
+    const int SN = SWd * SHd;
+    uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * 4 * 64;
+    for (int i0 = t; i0 < SN; i0 += 4 * kOrbWG) {
+      int v[4], p0[4], p4[4], p8[4], p12[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = min(i0 + q * kOrbWG, SN - 1);
+        const int y = fdiv(i, mS), x = i - y * SWd;
+        const uint8_t* c = I + (y + kNMS0) * W + x + kNMS0;
+        v[q] = c[0];
+        p0[q] = c[3 * W];
+        p4[q] = c[3];
+        p8[q] = c[-3 * W];
+        p12[q] = c[-3];
+      }
+      int nq = 0;  // wave-uniform
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * kOrbWG;
+        const bool ok = i < SN && fast_maybe(v[q], p0[q], p4[q], p8[q], p12[q]);
+        if (i < SN && !ok) Smap[i] = 0;
+        const uint64_t m = __ballot(ok);
+        if (ok)
+          fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              (uint32_t)i;
+        nq += __popcll(m);
+      }
+      for (int j = lane; j < nq; j += 64) {
+        const int i = (int)fq[j];
+        const int y = fdiv(i, mS), x = i - y * SWd;
+        Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * W + x + kNMS0, W);
+      }
     }
     for (int i = t; i < 256; i += kOrbWG) hist[i] = 0;
     if (t < 8) ctr[t] = 0;
@@ -756,7 +810,6 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
       g->tile_shape[ty * ntx + tx] = (uint8_t)s;
     }
   auto al = [](int v) { return (v + 15) & ~15; };
-  const int max_u = max(max(max_smap, max_bl), max_b);
   int nmax = 0;
   for (int l = 0; l < kNLev; ++l) nmax = max(nmax, g->nl[l]);
   g->cand_cap = max(max_cand, 1);
@@ -767,26 +820,35 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
     max_h = max(max_h, g->sh[s]);
   }
   g->tab_x = (max_w + 3) & ~3;
-  const int lists = al(g->list_cap * (int)sizeof(KP)) + al(g->list_cap * 8) +
-                    (256 + 16 + g->tab_x + max_h) * 4;
+  // U holds in turn the resize target (+ the resize tables past it), the FAST
+  // score map (+ the survivor queues past it) and the blurred level; sized
+  // so that a 720p tile (192x216 patch) needs <= 80 KiB and two ORB
+  // workgroups share a CU.
+  const int tabs = (g->tab_x + max_h) * 4;
+  const int max_u = max(max(al(max_smap) + kFq, max_bl), al(max_b) + tabs);
+  const int lists = al(g->list_cap * (int)sizeof(KP)) + al(g->list_cap * 8) + (256 + 16) * 4;
   g->glob = al(max_a) + al(max_u) + lists > 160 * 1024;
   if (g->glob) {
     // A patch (a whole image, orb_extraction_detect on a full frame) whose
     // level images do not fit LDS keeps them in two global ping-pong buffers
-    // per image (L2-resident); the keypoint lists stay in LDS.
+    // per image (L2-resident); the lists, queues and tables stay in LDS.
     SLAM_REQUIRE(g->n_tiles == 1, "slam_orb: %d patches of %dx%d do not fit LDS", g->n_tiles, pw, ph);
     g->lvl_bytes = (max(max_a, max_u) + 64 + 255) & ~255;
     g->lds_a = g->lds_u = 0;
-    g->lds_l = 0;
+    g->lds_fq = 0;
+    g->lds_tab = kFq;
+    g->lds_l = kFq + al(tabs);
   } else {
     g->lvl_bytes = 0;
     g->lds_a = 0;
     g->lds_u = al(max_a);
+    g->lds_fq = g->lds_u + al(max_smap);
+    g->lds_tab = g->lds_u + al(max_b);
     g->lds_l = g->lds_u + al(max_u);
   }
   g->lds_s = g->lds_l + al(g->list_cap * (int)sizeof(KP));
   g->lds_m = g->lds_s + al(g->list_cap * 8);
-  g->lds_total = g->lds_m + (256 + 16 + g->tab_x + max_h) * 4;
+  g->lds_total = g->lds_m + (256 + 16) * 4;
   g->tcap = max_kp + 64;
   SLAM_REQUIRE(g->lds_total <= 160 * 1024,
                "slam_orb: patch %dx%d needs %d B of LDS (> 160 KiB)", pw, ph, g->lds_total);
