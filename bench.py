@@ -32,6 +32,8 @@ for _p in (ROOT, os.path.join(ROOT, "slam-1_amd")):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from slam355.pipeline import Tracker  # noqa: E402
+
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
 F64_PEAK_TFLOPS = 78.6        # FP64 vector == FP64 matrix on gfx950 (spec)
@@ -157,17 +159,73 @@ def masked_stream(n_cus):
     return st
 
 
+class FrameFeed:
+    """Host-resident synthetic stereo sequence streamed to the GPU inside the
+    timed region: the sequence lives in pinned host memory, pre-packed per
+    tracking batch as [left_0..left_B, right_0..right_{B-1}] (2B+1 images, so
+    one H2D copy per step), and step k's batch is uploaded on a copy stream
+    into one of two device slots while step k-1 is tracked (double buffering:
+    the copy into a slot waits until the tracking that read it has finished)."""
+
+    def __init__(self, L, R, B, n_windows):
+        self.B, self.n_windows = B, n_windows
+        H, W = L.shape[1:]
+        packs = torch.empty((n_windows, 2 * B + 1, H, W), dtype=torch.uint8).pin_memory()
+        for w in range(n_windows):
+            f0 = w * B
+            packs[w, :B + 1] = L[f0:f0 + B + 1].cpu()
+            packs[w, B + 1:] = R[f0:f0 + B].cpu()
+        self.packs = packs
+        self.slots = [torch.empty((2 * B + 1, H, W), dtype=torch.uint8, device="cuda")
+                      for _ in range(2)]
+        self.copy_stream = torch.cuda.Stream()
+        self.ready = [torch.cuda.Event() for _ in range(2)]
+        self.free = [torch.cuda.Event() for _ in range(2)]
+        self.k = 0
+
+    def upload(self, k):
+        slot = k % 2
+        cs = self.copy_stream
+        cs.wait_event(self.free[slot])
+        with torch.cuda.stream(cs):
+            self.slots[slot].copy_(self.packs[k % self.n_windows], non_blocking=True)
+        self.ready[slot].record(cs)
+
+    def prime(self):
+        for e in self.free:
+            e.record(torch.cuda.current_stream())
+        self.upload(0)
+
+    def next(self, stream):
+        """-> (slot tensor of step k, window index); issues the upload of step
+        k+1; `stream` waits for step k's upload.  Call release(stream) after
+        the launches that read the slot."""
+        k = self.k
+        self.upload(k + 1)
+        stream.wait_event(self.ready[k % 2])
+        return self.slots[k % 2], k % self.n_windows
+
+    def release(self, stream):
+        self.free[self.k % 2].record(stream)
+        self.k += 1
+
+
 def run_tracking(args, world, rank):
     from slam355.ba import BAProblem
-    from slam355.pipeline import Tracker, chain_poses
-    from slam355.synthetic import ba_problem, perturb, stereo_sequence
+    from slam355.synthetic import ba_problem, corridor_sequence, perturb
 
     B = args.batch
-    L, R, poses, rig = stereo_sequence(B + 1, W_IMG, H_IMG, seed=1000 + rank)
+    n_win = args.windows
+    # the sequence: n_win distinct batches of B frame pairs, rendered on the GPU
+    # once (untimed), then held in pinned host memory and streamed back
+    L, R, poses, rig = corridor_sequence(n_win * B + 1, W_IMG, H_IMG, seed=1000 + rank,
+                                         device="cuda", as_numpy=False)
+    feed = FrameFeed(L, R, B, n_win)
+    L_np, R_np = L[:3].cpu().numpy(), R[:2].cpu().numpy()
+    del L, R
     trk_stream = masked_stream(args.track_cus) if args.track_cus else None
-    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=56, seed=rank,
+    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
                   stream=trk_stream)
-    trk.imgs.copy_(torch.from_numpy(np.concatenate([L, R[:B]])))
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
     cams, pts, ci, pi, qs = ba_problem(rng, *C3)
@@ -180,7 +238,9 @@ def run_tracking(args, world, rank):
         ba = BAProblem(c0, p0, ci, pi, qs, stream=ba_stream)
     torch.cuda.synchronize()
     n_solves = max(1, B // args.ba_every)
-    state = {}
+    tstream = trk_stream if trk_stream is not None else stream
+    all_poses = {}
+    feed.prime()
 
     def ev_on(s):
         ev = torch.cuda.Event(enable_timing=True)
@@ -188,12 +248,18 @@ def run_tracking(args, world, rank):
         return ev
 
     def step(marks):
-        with torch.cuda.stream(trk_stream if trk_stream is not None else stream):
+        with torch.cuda.stream(tstream):
             tracked_step(marks)
 
     def tracked_step(marks):
         tmarks = [] if marks is not None else None
-        trk.track(0, marks=tmarks)
+        imgs, win = feed.next(tstream)
+        if win == 0:  # a new pass over the sequence starts at frame 0
+            trk.reset_chain()
+        trk.track(win * B, imgs=imgs, marks=tmarks)
+        feed.release(tstream)
+        if marks is None and args.keep_poses:
+            all_poses[win] = trk.poses.clone()
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
         with torch.cuda.stream(ba_stream):
             for _ in range(n_solves):
@@ -205,23 +271,21 @@ def run_tracking(args, world, rank):
         if marks is not None:
             bmarks.append(("local_ba", ev_on(ba_stream)))
             marks["track"], marks["ba"] = tmarks, bmarks
-        # poses need only the tracking stream; BA of this step overlaps the next
-        # step's tracking (the timed region ends with a device-wide synchronize)
-        rv, tv, n = trk.rvec.cpu().numpy(), trk.tvec.cpu().numpy(), trk.p_ninl.cpu().numpy()
-        state["poses"], _ = chain_poses(np.eye(4), rv, tv, n)  # main.py:120-124 (host)
 
     dt, stages = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
     frames = reduce_scalar(float(B * args.steps), world, "sum")
-    cnt = trk.counters()
-    # accuracy of the tracked trajectory against the synthetic ground truth
-    est = state["poses"]
-    gt = np.stack([np.linalg.inv(poses[0]) @ poses[i + 1] for i in range(B)])
+    cnt = trk.counters()  # raises on any ORB workspace overflow since the start
+    # accuracy of the tracked trajectory (the last tracked window) against ground truth
+    last_win = (args.warmup + args.steps - 1) % n_win
+    est = trk.poses.cpu().numpy()
+    f0 = last_win * B
+    gt = np.stack([np.linalg.inv(poses[f0]) @ poses[f0 + i + 1] for i in range(B)])
     t_err = np.linalg.norm(est[:, :3, 3] - gt[:, :3, 3], axis=1)
 
     # roofline of the dominant stage
     n_img = 2 * B + 1
     patch_bytes = 36 * 216 * 192
-    kp_mean = float(np.mean(np.maximum(cnt["orb"], 0)))
+    kp_mean = float(np.mean(cnt["orb"]))
     orb_bytes = n_img * (patch_bytes + kp_mean * ORB_OUT_BYTES)
     orb_ms = stages.get("orb", float("nan"))
     ba_ms_iter = stages.get("local_ba", float("nan")) / (n_solves * args.ba_iters)
@@ -257,11 +321,14 @@ def run_tracking(args, world, rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8+f32+f64",
-        "data": "synthetic (seeded 1280x720 stereo sequence, 800 textured landmarks, GT poses)",
-        "config": {"workload": "C2 tracking (1280x720, 56 ORB kp/tile = 2016 kp/frame) + "
+        "data": (f"synthetic (seeded textured-corridor stereo sequence, {n_win * B + 1} frames "
+                 "1280x720 in pinned host memory, uploaded inside the timed region; GT poses)"),
+        "config": {"workload": f"C2 tracking (1280x720, {args.kp_per_tile} ORB kp/tile) + "
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
                                f"x {args.ba_iters} LM iters",
+                   "orb_kp_mean": kp_mean,
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
+                   "h2d_upload": "in timed region (pinned, copy stream, double-buffered)",
                    "local_ba_stream": "serial" if args.ba_serial else "concurrent",
                    "tracking_cus": args.track_cus or "all"},
         "roofline": dict(roof[dominant], stage=dominant),
@@ -275,7 +342,7 @@ def run_tracking(args, world, rank):
                      "trajectory_t_err_m_max": float(t_err.max())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline_tracking(L, R, rig, args, C3, (c0, p0, ci, pi, qs))
+        rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, (c0, p0, ci, pi, qs))
     del trk, ba  # their kernels' buffers, then the masked stream itself
     if trk_stream is not None:
         trk_stream.destroy()
@@ -339,15 +406,16 @@ def cpu_baseline_tracking(L, R, rig, args, C3, ba_in, pairs=2):
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     t0 = time.perf_counter()
     cache = {}
-    kp, octv, desc, cnt = oracle.orb_tiles_batch(np.concatenate([L[:pairs + 1], R[:pairs]]), 56,
-                                                 1 << 13)
+    kp, octv, desc, cnt = oracle.orb_tiles_batch(np.concatenate([L[:pairs + 1], R[:pairs]]),
+                                                 args.kp_per_tile, 1 << 13)
     for i in range(pairs + 1):
         cache[("L", i)] = (kp[i, :cnt[i]], octv[i, :cnt[i]], desc[i, :cnt[i]])
     for i in range(pairs):
         j = pairs + 1 + i
         cache[("R", i)] = (kp[j, :cnt[j]], octv[j, :cnt[j]], desc[j, :cnt[j]])
     for i in range(pairs):
-        opl.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, seed=0, frame=i, orb_cache=cache)
+        opl.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, max_kp=args.kp_per_tile, seed=0,
+                       frame=i, orb_cache=cache)
     t_track = (time.perf_counter() - t0) / pairs
     c0, p0, ci, pi, qs = ba_in
     pr = oba._obs_pairs(ci, pi)
@@ -586,6 +654,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="tracking", choices=["tracking", "ba", "matcher", "vo"])
     ap.add_argument("--batch", type=int, default=32, help="frame pairs per GPU per step")
+    ap.add_argument("--kp-per-tile", type=int, default=64,
+                    help="ORB max_number_of_kp per tile: 64 -> ~2090 kp/frame (levels 6-7 of a "
+                         "216x192 patch cannot hold keypoints, so 56 gives only ~1780)")
+    ap.add_argument("--windows", type=int, default=8,
+                    help="distinct tracking batches in the streamed sequence")
+    ap.add_argument("--keep-poses", action="store_true")
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")

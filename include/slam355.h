@@ -142,6 +142,15 @@ int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count
                     double reproj_thresh, int hyp_iters, int refine_iters, double* d_rvec,
                     double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, void* stream);
 
+/* Pose chain of main.py:94-98, 120-124 (pose_{b+1} = pose_b @ T_b with
+ * T_b = [Rodrigues(-rvec_b) | -tvec_b], transformation.py:15-19; when
+ * d_ninliers[b] < 0 -- PnP skipped, main.py:94 -- the previous T is reused).
+ * d_state [32] f64 = (pose, T) 4x4 row-major, read and updated in place so
+ * consecutive batches chain on the device; d_poses [batch][16] f64 out.
+ * Replaces the host loop slam355.pipeline.chain_poses. */
+int slam_pose_chain(const double* d_rvec, const double* d_tvec, const int32_t* d_ninliers,
+                    int batch, double* d_state, double* d_poses, void* stream);
+
 /* The reference's stereo visual-odometry pose estimator
  * (visual_odometry.py:135-157 estimate_pose over the residuals of :65-81),
  * restated deterministically (oracle/vo.c): dof = (rotvec, t), T = [R | t];

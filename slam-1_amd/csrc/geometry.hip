@@ -824,6 +824,48 @@ __global__ __launch_bounds__(kBS) void k_vo_residuals(
 }
 }  // namespace
 
+// --------------------------------------------------------------- pose chain
+// main.py:94-98, 120-124 on the device: T_b = [Rodrigues(-rvec_b) | -tvec_b]
+// (transformation.py:15-19's sign flip) when PnP ran (ninl >= 0), else the
+// previous T is reused (stale); pose_{b+1} = pose_b @ T_b.  state [32] =
+// (pose 4x4, T 4x4) row-major carries the chain across calls, so consecutive
+// tracking batches chain without a host round trip.  One lane: B 4x4 products.
+__global__ void k_pose_chain(const double* __restrict__ rvec, const double* __restrict__ tvec,
+                             const int32_t* __restrict__ ninl, int B, double* __restrict__ state,
+                             double* __restrict__ poses) {
+  if (threadIdx.x != 0) return;
+  double P[16], T[16];
+  for (int i = 0; i < 16; ++i) {
+    P[i] = state[i];
+    T[i] = state[16 + i];
+  }
+  for (int b = 0; b < B; ++b) {
+    if (ninl[b] >= 0) {
+      const double r[3] = {-rvec[3 * b], -rvec[3 * b + 1], -rvec[3 * b + 2]};
+      double R[9];
+      rodrigues(r, R);
+      for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) T[4 * i + j] = R[3 * i + j];
+        T[4 * i + 3] = -tvec[3 * b + i];
+      }
+      T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
+    }
+    double N[16];
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j)
+        N[4 * i + j] = P[4 * i] * T[j] + P[4 * i + 1] * T[4 + j] + P[4 * i + 2] * T[8 + j] +
+                       P[4 * i + 3] * T[12 + j];
+    for (int i = 0; i < 16; ++i) {
+      P[i] = N[i];
+      poses[16 * b + i] = N[i];
+    }
+  }
+  for (int i = 0; i < 16; ++i) {
+    state[i] = P[i];
+    state[16 + i] = T[i];
+  }
+}
+
 extern "C" int slam_gather_matches(const float* d_kpq, int kq_cap, const float* d_kpt, int kt_cap,
                                    const uint8_t* d_desq, const uint8_t* d_dest,
                                    const int32_t* d_pairs, const int32_t* d_count, int p_cap,
@@ -950,5 +992,17 @@ extern "C" int slam_vo_residuals(const double* d_dof, const double* d_q1, const 
   k_vo_residuals<<<grid, kBS, 0, slam::as_stream(stream)>>>(d_dof, d_q1, d_q2, d_Q1, d_Q2,
                                                            d_count, cap, d_P, d_res);
   SLAM_LAUNCHED("k_vo_residuals");
+  return SLAM_OK;
+}
+
+extern "C" int slam_pose_chain(const double* d_rvec, const double* d_tvec,
+                               const int32_t* d_ninliers, int batch, double* d_state,
+                               double* d_poses, void* stream) {
+  SLAM_REQUIRE(batch >= 0, "slam_pose_chain: batch < 0");
+  if (batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_rvec && d_tvec && d_ninliers && d_state && d_poses, "slam_pose_chain: null pointer");
+  k_pose_chain<<<1, 64, 0, slam::as_stream(stream)>>>(d_rvec, d_tvec, d_ninliers, batch, d_state,
+                                                     d_poses);
+  SLAM_LAUNCHED("k_pose_chain");
   return SLAM_OK;
 }

@@ -59,6 +59,7 @@ SIGNATURES = {
     "slam_triangulate": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "slam_pnp_ransac": [c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int, c_double, c_int,
                         c_int, c_p, c_p, c_p, c_p, c_p],
+    "slam_pose_chain": [c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_vo_estimate_pose": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int,
                               c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_size_t, c_p],
     "slam_vo_pose_workspace_bytes": [c_int, c_int, ctypes.POINTER(c_size_t)],

@@ -17,8 +17,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import geometry, matcher, orb
-from .device import require_gpu
+from . import _lib, geometry, matcher, orb
+from .device import ptr, require_gpu, stream_ptr
 
 
 class Tracker:
@@ -75,14 +75,25 @@ class Tracker:
         self.p_ninl = torch.zeros((B,), **i32)
         self.p_mask = torch.zeros((B, cap), **u8)
         self.imgs = torch.zeros((2 * B + 1, H, W), **u8)
+        # device pose chain (main.py:120-124): (pose, T) carried across batches
+        self.chain_state = torch.zeros((32,), **f64)
+        self.reset_chain()
+        self.poses = torch.zeros((B, 4, 4), **f64)
+        # running minimum of the ORB counts since the last check(): k_orb_compact
+        # writes a negative count when a tile's retained ties exceed the
+        # workspace (OpenCV keeps every tie); such a frame must not silently
+        # degrade into "no matches" + a stale pose
+        self.orb_min = torch.full((1,), 1 << 30, **i32)
 
     # ------------------------------------------------------------------ device step
-    def track(self, frame0: int, imgs: torch.Tensor | None = None, marks=None):
+    def track(self, frame0: int, imgs: torch.Tensor | None = None, marks=None, chain=True):
         """Run the B frame pairs (frame0 + b, frame0 + b + 1), b < B, on device.
 
         `imgs` [2B+1, H, W] u8 = left_{frame0..frame0+B}, right_{frame0..frame0+B-1}
         (defaults to self.imgs, filled by the caller).  Asynchronous: returns
-        device tensors (rvec, tvec, n_inliers)."""
+        device tensors (rvec, tvec, n_inliers); with `chain` the absolute poses
+        of frames frame0+1 .. frame0+B are chained on the device into
+        self.poses [B,4,4] (main.py:120-124), continuing from the previous call."""
         B, st = self.B, self.stream
         im = self.imgs if imgs is None else imgs
 
@@ -94,6 +105,8 @@ class Tracker:
 
         mark("start")
         kp, octv, desc, cnt = self.ows.run(im, st)
+        with torch.cuda.stream(st if st is not None else torch.cuda.current_stream()):
+            torch.minimum(self.orb_min, cnt.amin(), out=self.orb_min)
         mark("orb")
         kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
@@ -130,9 +143,32 @@ class Tracker:
         geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,
                             out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st)
         mark("pnp")
+        if chain:
+            _lib.call("slam_pose_chain", ptr(self.rvec), ptr(self.tvec), ptr(self.p_ninl), B,
+                      ptr(self.chain_state), ptr(self.poses), stream_ptr(st))
+            mark("pose_chain")
         return self.rvec, self.tvec, self.p_ninl
 
+    def reset_chain(self, pose0=None, T0=None):
+        """Start the device pose chain at pose0 (default identity) with T0 as the
+        stale transform (default identity)."""
+        st = np.concatenate([np.eye(4) if pose0 is None else np.asarray(pose0, float),
+                             np.eye(4) if T0 is None else np.asarray(T0, float)]).ravel()
+        self.chain_state.copy_(torch.from_numpy(st))
+
+    def check(self):
+        """Synchronises: raise if any ORB count since the last check was negative
+        (keypoint workspace overflow: too many tied responses in a tile, or more
+        keypoints than kp_cap), then reset the flag."""
+        m = int(self.orb_min.item())
+        self.orb_min.fill_(1 << 30)
+        if m < 0:
+            raise _lib.SlamError("Tracker: ORB keypoint workspace overflow (a tile kept more tied "
+                                 "responses than the workspace holds, or kp_cap was exceeded); "
+                                 "the frame would have been tracked with no matches")
+
     def counters(self):
+        self.check()
         return dict(orb=self.ows.count.cpu().numpy(), stereo=self.s_cnt.cpu().numpy(),
                     f_inliers=self.f_cnt.cpu().numpy(), temporal=self.t_cnt.cpu().numpy(),
                     pnp_inliers=self.p_ninl.cpu().numpy())

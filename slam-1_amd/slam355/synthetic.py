@@ -252,3 +252,88 @@ def stereo_sequence(n_frames, W=1280, H=720, seed=0, n_landmarks=800):
         left[i] = render(world, Tinv, rig, rng, 0.0, bg)
         right[i] = render(world, Tinv, rig, rng, rig.baseline, bg)
     return left, right, poses, rig
+
+
+# ----------------------------------------------------------------------------- textured corridor
+# The landmark-sprite scene above is sparse (<= ~1200 ORB keypoints per
+# 1280x720 frame); packing more sprites turns corners into occlusion junctions
+# that differ between the stereo views.  The headline config (BASELINE C2:
+# 2000 kp/frame) uses a textured corridor instead: every pixel lies on a
+# plane (two walls, floor, ceiling, an end wall), textured with hashed random
+# intensity cells fixed in world coordinates, so corners are geometrically
+# consistent between views and frames.  2x2 supersampling anti-aliases far
+# cells; Gaussian noise sigma 2 as in render().  Written in torch so the bench
+# renders its sequence on the GPU in milliseconds per view (the CPU path is
+# the same code; tests render a few views there).
+CORRIDOR = dict(half_width=7.0, floor=2.0, ceiling=5.0, end=400.0, cell=0.3)
+
+
+def _hash_cells(i, j, k: int):
+    import torch
+
+    h = (i * 73856093) ^ (j * 19349663) ^ (k * 83492791)
+    h = (h ^ (h >> 13)) * 0x5BD1E995
+    h = h ^ (h >> 15)
+    return (h & 255).to(torch.float64)
+
+
+def render_corridor(T_cw, rig: StereoRig, gen, x_offset=0.0, ss=2, noise=2.0, device="cpu",
+                    **kw):
+    """One grayscale view (uint8 torch tensor [H, W] on `device`) of the
+    textured corridor from camera-to-world pose T_cw; x_offset shifts the camera
+    along its x axis (right camera = +baseline).  `gen`: torch.Generator of the
+    noise, on `device`."""
+    import torch
+
+    geo = dict(CORRIDOR, **kw)
+    H, W, K = rig.H, rig.W, rig.K
+    f64 = dict(dtype=torch.float64, device=device)
+    o = (torch.arange(ss, **f64) + 0.5) / ss - 0.5
+    vv = torch.arange(H, **f64)[:, None, None, None] + o[None, :, None, None]
+    uu = torch.arange(W, **f64)[None, None, :, None] + o[None, None, None, :]
+    x = ((uu - K[0, 2]) / K[0, 0]).expand(H, ss, W, ss)
+    y = ((vv - K[1, 2]) / K[1, 1]).expand(H, ss, W, ss)
+    Rn = np.asarray(T_cw, np.float64)[:3, :3]
+    R = torch.as_tensor(Rn, **f64)
+    c = torch.as_tensor(np.asarray(T_cw, np.float64)[:3, 3] + Rn @ np.array([x_offset, 0.0, 0.0]),
+                        **f64)
+    d = [R[a, 0] * x + R[a, 1] * y + R[a, 2] for a in range(3)]
+    best = torch.full((H, ss, W, ss), float("inf"), **f64)
+    val = torch.zeros((H, ss, W, ss), **f64)
+    planes = [(0, -geo["half_width"], 0), (0, geo["half_width"], 1), (1, geo["floor"], 2),
+              (1, -geo["ceiling"], 3), (2, geo["end"], 4)]
+    for ax, pos, pid in planes:
+        t = (pos - c[ax]) / d[ax]
+        ok = (t > 0) & (t < best)
+        a1, a2 = [a for a in range(3) if a != ax]
+        cells = []
+        for a in (a1, a2):
+            q = torch.floor((c[a] + t * d[a]) / geo["cell"])
+            cells.append(torch.nan_to_num(q, 0.0, 0.0, 0.0).clamp(-2.0 ** 40, 2.0 ** 40)
+                         .to(torch.int64))
+        v = _hash_cells(cells[0], cells[1], pid)
+        best = torch.where(ok, t, best)
+        val = torch.where(ok, v, val)
+    img = val.mean(dim=(1, 3))
+    img = img + noise * torch.randn((H, W), generator=gen, **f64)
+    return torch.clamp(torch.round(img), 0, 255).to(torch.uint8)
+
+
+def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=True):
+    """(left [F,H,W] u8, right [F,H,W] u8, poses [F,4,4] camera-to-world, rig) of
+    the textured corridor; the trajectory is trajectory() (1 m/frame, yaw
+    jitter 0.2 deg).  torch tensors on `device` unless as_numpy."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    rig = StereoRig(W, H)
+    poses = trajectory(rng, n_frames)
+    gen = torch.Generator(device=device).manual_seed(seed)
+    left = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
+    right = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
+    for i in range(n_frames):
+        left[i] = render_corridor(poses[i], rig, gen, 0.0, device=device)
+        right[i] = render_corridor(poses[i], rig, gen, rig.baseline, device=device)
+    if as_numpy:
+        return left.cpu().numpy(), right.cpu().numpy(), poses, rig
+    return left, right, poses, rig

@@ -59,3 +59,114 @@ def test_gpu_tracker_matches_oracle_chain(seq):
         assert c["temporal"][i] == e["n_temporal"], i
         assert n[i] == e["n_pnp"], i
         assert np.allclose(rv[i], e["rvec"], atol=1e-8) and np.allclose(tv[i], e["tvec"], atol=1e-8)
+
+
+@pytest.fixture(scope="module")
+def corridor():
+    from slam355.synthetic import corridor_sequence
+
+    return corridor_sequence(4, 1280, 720, seed=21)
+
+
+def test_corridor_scene_reaches_c2_keypoint_count(corridor):
+    """BASELINE C2 = 2000 ORB kp/frame: with 64 kp per tile the textured corridor
+    fills every tile's level budgets (levels 6-7 of a 216x192 patch cannot
+    hold keypoints, so 56 per tile caps at ~1780)."""
+    import oracle
+
+    L, R, poses, rig = corridor
+    _, _, _, cnt = oracle.orb_tiles_batch(np.concatenate([L[:2], R[:1]]), 64, 1 << 13)
+    assert cnt.min() >= 2000, cnt
+    out = op.track_pair(L[0], R[0], L[1], rig.P_l, rig.P_r, max_kp=64, seed=1, frame=0)
+    assert out["n_stereo"] >= 400 and out["n_pnp"] >= 50, (out["n_stereo"], out["n_pnp"])
+    rel = np.linalg.inv(poses[1]) @ poses[0]
+    assert np.allclose(out["tvec"], rel[:3, 3], atol=0.05)
+
+
+@pytest.mark.gpu
+def test_gpu_tracker_corridor_c2_matches_oracle_and_chains_on_device(corridor):
+    """C2 shape (2000+ kp/frame): per pair counts, masks and PnP equal the oracle
+    chain; the device pose chain (k_pose_chain) equals the host chain_poses and
+    continues across two track() calls."""
+    import torch
+    from slam355.pipeline import Tracker, chain_poses
+
+    L, R, poses, rig = corridor
+    B = 3
+    trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=2)
+    trk.imgs.copy_(torch.from_numpy(np.concatenate([L[:B + 1], R[:B]])))
+    rv, tv, n = trk.track(0)
+    P1 = trk.poses.cpu().numpy()
+    c = trk.counters()
+    assert c["orb"].min() >= 2000
+    rv, tv, n = rv.cpu().numpy(), tv.cpu().numpy(), n.cpu().numpy()
+    cache = {}
+    for i in range(B):
+        e = op.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, max_kp=64, seed=2, frame=i,
+                          orb_cache=cache)
+        assert c["orb"][i] == len(cache[("L", i)][0])
+        assert c["stereo"][i] == e["n_stereo"] and c["f_inliers"][i] == e["n_f"], i
+        assert c["temporal"][i] == e["n_temporal"] and n[i] == e["n_pnp"], i
+        assert np.allclose(rv[i], e["rvec"], atol=1e-8) and np.allclose(tv[i], e["tvec"], atol=1e-8)
+    Ph, T = chain_poses(np.eye(4), rv, tv, n)
+    assert np.allclose(P1, Ph, rtol=0, atol=1e-12)
+    # second call continues the chain from the last pose (same frames again)
+    trk.track(0)
+    P2 = trk.poses.cpu().numpy()
+    Ph2, _ = chain_poses(Ph[-1], rv, tv, n, T_prev=T)
+    assert np.allclose(P2, Ph2, rtol=0, atol=1e-10)
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[i + 1] for i in range(B)])
+    assert np.abs(P1[:, :3, 3] - gt[:, :3, 3]).max() < 0.1
+
+
+@pytest.mark.gpu
+def test_gpu_device_chain_stale_transform():
+    """ninl < 0 (PnP skipped, main.py:94) reuses the previous T on the device too."""
+    import torch
+    from slam355 import _lib
+    from slam355.device import ptr, stream_ptr
+    from slam355.pipeline import chain_poses
+
+    r = np.array([[0.0, 0.01, 0.0], [0, 0, 0], [0.0, -0.02, 0.001], [0.3, -0.2, 0.1]])
+    t = np.array([[0.0, 0.0, -1.0], [1, 1, 1], [0.1, 0.0, -1.0], [2.0, -1.0, 0.5]])
+    n = np.array([50, -1, 40, -1], np.int32)
+    dev = torch.device("cuda")
+    st = torch.from_numpy(np.concatenate([np.eye(4), np.eye(4)]).ravel()).to(dev)
+    out = torch.zeros((4, 16), dtype=torch.float64, device=dev)
+    _lib.call("slam_pose_chain", ptr(torch.from_numpy(r).to(dev)), ptr(torch.from_numpy(t).to(dev)),
+              ptr(torch.from_numpy(n).to(dev)), 4, ptr(st), ptr(out), stream_ptr())
+    P, T = chain_poses(np.eye(4), r, t, n)
+    assert np.allclose(out.cpu().numpy().reshape(4, 4, 4), P, rtol=0, atol=1e-12)
+    assert np.allclose(st.cpu().numpy()[16:].reshape(4, 4), T, rtol=0, atol=1e-14)
+
+
+def _tie_frame(H=720, W=1280):
+    """A grid of identical isolated bright pixels: every dot has the same FAST
+    score and Harris response, so retainBest keeps all ~340 tied level-0
+    keypoints of a tile (the oracle, like OpenCV, keeps every tie), more than
+    the per-tile keypoint workspace (max_kp + 64) holds."""
+    img = np.full((H, W), 40, np.uint8)
+    img[::8, ::8] = 220
+    return img
+
+
+@pytest.mark.gpu
+def test_gpu_tracker_raises_on_orb_overflow(corridor):
+    """an overflowing ORB tile must not silently become a frame
+    with no matches and a stale pose -- Tracker.check() raises."""
+    import torch
+    from slam355 import _lib
+    from slam355.pipeline import Tracker
+
+    L, R, poses, rig = corridor
+    B = 1
+    trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=2)
+    tie = _tie_frame()
+    trk.imgs.copy_(torch.from_numpy(np.stack([L[0], tie, R[0]])))
+    trk.track(0)
+    assert int(trk.ows.count[1].item()) < 0  # the tie frame overflowed
+    with pytest.raises(_lib.SlamError, match="overflow"):
+        trk.check()
+    trk.imgs.copy_(torch.from_numpy(np.stack([L[0], L[1], R[0]])))
+    trk.track(0)
+    trk.check()  # flag was reset; a normal batch passes
