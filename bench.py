@@ -211,7 +211,7 @@ class FrameFeed:
 
 
 def run_tracking(args, world, rank):
-    from slam355.ba import BAProblem
+    from slam355.ba import BABatch, BAProblem
     from slam355.synthetic import ba_problem, corridor_sequence, perturb
 
     B = args.batch
@@ -228,16 +228,19 @@ def run_tracking(args, world, rank):
                   stream=trk_stream)
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
-    cams, pts, ci, pi, qs = ba_problem(rng, *C3)
-    c0, p0 = perturb(rng, cams, pts)
+    n_solves = max(1, B // args.ba_every)
+    windows = []
+    for _ in range(n_solves):  # one C3 window per `ba_every` frames, each its own problem
+        cams, pts, ci, pi, qs = ba_problem(rng, *C3)
+        c0, p0 = perturb(rng, cams, pts)
+        windows.append((c0, p0, ci, pi, qs))
     stream = torch.cuda.current_stream()
     # local mapping (BA) on its own HIP stream, concurrent with tracking, unless --ba-serial
     # (high priority: its short latency-bound kernels go ahead of queued ORB tiles)
     ba_stream = stream if args.ba_serial else torch.cuda.Stream(priority=-1)
     with torch.cuda.stream(ba_stream):
-        ba = BAProblem(c0, p0, ci, pi, qs, stream=ba_stream)
+        ba = BABatch([BAProblem(*w, stream=ba_stream) for w in windows], stream=ba_stream)
     torch.cuda.synchronize()
-    n_solves = max(1, B // args.ba_every)
     tstream = trk_stream if trk_stream is not None else stream
     all_poses = {}
     feed.prime()
@@ -262,12 +265,13 @@ def run_tracking(args, world, rank):
             all_poses[win] = trk.poses.clone()
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
         with torch.cuda.stream(ba_stream):
-            for _ in range(n_solves):
+            # the step's local-BA windows, all advanced together (one launch set
+            # per LM iteration; windows restored to their initial state first)
+            if args.no_graph:
                 ba.restore()
-                if args.no_graph:
-                    ba.iterate(args.ba_iters)
-                else:
-                    ba.iterate_graphed(args.ba_iters)
+                ba.iterate(args.ba_iters)
+            else:
+                ba.iterate_graphed(args.ba_iters, with_restore=True)
         if marks is not None:
             bmarks.append(("local_ba", ev_on(ba_stream)))
             marks["track"], marks["ba"] = tmarks, bmarks
@@ -275,11 +279,12 @@ def run_tracking(args, world, rank):
     dt, stages = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
     frames = reduce_scalar(float(B * args.steps), world, "sum")
     cnt = trk.counters()  # raises on any ORB workspace overflow since the start
-    # accuracy of the tracked trajectory (the last tracked window) against ground truth
+    # accuracy of the tracked trajectory (the last tracked window; the device
+    # chain restarts at frame 0 of the sequence with window 0) against ground truth
     last_win = (args.warmup + args.steps - 1) % n_win
     est = trk.poses.cpu().numpy()
     f0 = last_win * B
-    gt = np.stack([np.linalg.inv(poses[f0]) @ poses[f0 + i + 1] for i in range(B)])
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[f0 + i + 1] for i in range(B)])
     t_err = np.linalg.norm(est[:, :3, 3] - gt[:, :3, 3], axis=1)
 
     # roofline of the dominant stage
@@ -288,14 +293,15 @@ def run_tracking(args, world, rank):
     kp_mean = float(np.mean(cnt["orb"]))
     orb_bytes = n_img * (patch_bytes + kp_mean * ORB_OUT_BYTES)
     orb_ms = stages.get("orb", float("nan"))
-    ba_ms_iter = stages.get("local_ba", float("nan")) / (n_solves * args.ba_iters)
-    ba_flops = ba_flops_per_iter(*C3[:2], C3[1] * C3[2], C3[2])
+    # one batched LM iteration advances all n_solves windows
+    ba_ms_iter = stages.get("local_ba", float("nan")) / args.ba_iters
+    ba_flops = n_solves * ba_flops_per_iter(*C3[:2], C3[1] * C3[2], C3[2])
     roof = {
         "orb": {"bound": "hbm", "achieved": orb_bytes / (orb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": "LM iteration: k_linearize + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_solves} C3 windows: k_linearize + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     pmc = pmc_traffic()
@@ -325,7 +331,7 @@ def run_tracking(args, world, rank):
                  "1280x720 in pinned host memory, uploaded inside the timed region; GT poses)"),
         "config": {"workload": f"C2 tracking (1280x720, {args.kp_per_tile} ORB kp/tile) + "
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
-                               f"x {args.ba_iters} LM iters",
+                               f"x {args.ba_iters} LM iters ({n_solves} windows per step, batched)",
                    "orb_kp_mean": kp_mean,
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
                    "h2d_upload": "in timed region (pinned, copy stream, double-buffered)",
@@ -342,7 +348,7 @@ def run_tracking(args, world, rank):
                      "trajectory_t_err_m_max": float(t_err.max())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, (c0, p0, ci, pi, qs))
+        rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, windows[0])
     del trk, ba  # their kernels' buffers, then the masked stream itself
     if trk_stream is not None:
         trk_stream.destroy()

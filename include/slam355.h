@@ -318,6 +318,9 @@ typedef struct slam_ba_problem {
   uint32_t* ticket;             /* [1] zero-initialised completion counter     */
 } slam_ba_problem;
 
+/* Problems per batched launch (slam_ba_iterate_batch splits larger batches). */
+#define SLAM_BA_MAX_BATCH 8
+
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);
 /* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120). */
@@ -340,6 +343,15 @@ int slam_ba_decide(const slam_ba_problem* prob, void* stream);
 int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream);
 /* Reset the LM state: lambda0, nu = 2, cur = 0, counters = 0. */
 int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream);
+/* Batched local BA: n_probs independent problems (e.g. the local-BA windows
+ * of a tracking batch; the reference solves one BAL problem per call,
+ * BundleAdjustment.py:397-402) advance n_iter LM iterations through shared
+ * launches, up to SLAM_BA_MAX_BATCH problems per launch (one problem per
+ * grid row).  Every problem keeps its own buffers and LM state: its iterates
+ * are the ones slam_ba_iterate gives it alone.  Batched problems must use the
+ * one-workgroup solver (9C <= 120); a packed problem iterates on its own. */
+int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, int n_iter, void* stream);
+int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0, void* stream);
 
 /* ------------------------------------------------------------------ pose chain
  * The live pose-chain optimisation of BundleAdjustment.py:79-183 (loop

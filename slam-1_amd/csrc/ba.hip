@@ -51,6 +51,16 @@ constexpr double kDiagMin = 1e-6, kDiagMax = 1e32;
 constexpr double kLamMin = 1e-16, kLamMax = 1e32;
 constexpr int kBS = 256;   // block size of the element-wise kernels
 
+// Batched LM: independent problems (local-BA windows) advance through one set
+// of launches, one problem per blockIdx.y; each keeps its own buffers and LM
+// state, so the iterates of a batched problem equal its solo iterates.  The
+// problem descriptors travel by value in the kernel arguments (8 x 296 B).
+constexpr int kBaMaxBatch = SLAM_BA_MAX_BATCH;
+struct BaBatch {
+  slam_ba_problem p[kBaMaxBatch];
+};
+#define BA_PROB(b) const slam_ba_problem& p = (b).p[blockIdx.y]
+
 // The LM kernels are short and latency-bound and usually share their CUs with
 // the (throughput-bound) ORB workgroups of the concurrent tracking stream: they
 // raise their waves' issue priority so their dependent chains are issued first
@@ -389,11 +399,13 @@ __device__ __forceinline__ void lin_slots(const slam_ba_problem& p, LinLds& L, i
 #else
 #define LIN_T(i) (void)0
 #endif
-__global__ __launch_bounds__(kLinWG) void k_linearize(slam_ba_problem p) {
+__global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
+  BA_PROB(bat);
+  const int g = blockIdx.x;
+  if (g >= p.n_grps) return;  // batch: grid.x covers the largest problem
   lm_wave_priority();
   __shared__ LinLds L;
   LIN_T(0);
-  const int g = blockIdx.x;
   const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
   const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
   const int t = threadIdx.x;
@@ -544,7 +556,9 @@ __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, in
 // Dense layout: blocks without common points are written as zeros, so sys
 // needs no separate clearing.  Packed layout: each listed block is written
 // once, full 9x9, at sys + 81 * blk.
-__global__ __launch_bounds__(kAsmWG) void k_assemble(slam_ba_problem p) {
+__global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
+  BA_PROB(bat);
+  if ((int)blockIdx.x >= p.n_blocks) return;
   lm_wave_priority();
   __shared__ double red[kAsmWG / 81][kCPart];
   __shared__ double sh[kCPart];
@@ -708,7 +722,8 @@ struct BlkLds {
   }
 };
 
-__global__ __launch_bounds__(kBlkWG) void k_solve_blk(slam_ba_problem p) {
+__global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
+  BA_PROB(bat);
   lm_wave_priority();
   extern __shared__ __attribute__((aligned(16))) double lds[];
   double* red = lds;
@@ -1506,13 +1521,16 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
 // fixed order into small[0..1] and, when DECIDE (single rank), applies the LM
 // decision.
 template <bool DECIDE>
-__global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* __restrict__ part) {
+__global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
+  BA_PROB(bat);
+  const int g = blockIdx.x, G = p.n_grps;
+  if (g >= G) return;  // batch: grid.x covers the largest problem (not in the ticket count)
+  double* __restrict__ part = p.red_part;
   lm_wave_priority();
   __shared__ double sdy[kGrp][3];
   __shared__ double snp[kGrp][3];
   __shared__ double red[kGrp / 64];
   __shared__ int last;
-  const int g = blockIdx.x, G = gridDim.x;
   const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
   const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
   const int t = threadIdx.x;
@@ -1597,8 +1615,9 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(slam_ba_problem p, double* 
   }
 }
 
-__global__ void k_decide(double* __restrict__ state, const double* __restrict__ small) {
-  if (threadIdx.x == 0) lm_decide(state, small);
+__global__ void k_decide(BaBatch bat) {
+  BA_PROB(bat);
+  if (threadIdx.x == 0) lm_decide(p.state, p.small);
 }
 
 __device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small) {
@@ -1630,7 +1649,8 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
   state[SLAM_BA_ST_ITERS] += 1.0;
 }
 
-__global__ void k_reset(slam_ba_problem p, double lam0) {
+__global__ void k_reset(BaBatch bat, double lam0) {
+  BA_PROB(bat);
   const int t = threadIdx.x;
   double* state = p.state;
   if (t < SLAM_BA_ST_SLOTS) state[t] = 0.0;
@@ -1704,60 +1724,135 @@ extern "C" int slam_ba_jacobian(const double* d_cams, const double* d_pts,
   return SLAM_OK;
 }
 
-extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream) {
-  if (int rc = check_problem(prob)) return rc;
-  k_reset<<<1, 64, 0, slam::as_stream(stream)>>>(*prob, lambda0);
+namespace {
+
+// Descriptor batch of problems [i0, i0 + n) (n <= kBaMaxBatch) and the launch
+// extents that cover the largest of them.
+struct Launch {
+  BaBatch b;
+  int n, max_grps, max_blocks;
+  size_t solve_lds;
+  bool dense;
+};
+
+static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
+  SLAM_REQUIRE(n >= 1 && n <= kBaMaxBatch, "slam_ba: batch of %d problems (1..%d)", n, kBaMaxBatch);
+  SLAM_REQUIRE(probs != nullptr, "slam_ba: null problem array");
+  L->n = n;
+  L->max_grps = L->max_blocks = 0;
+  L->solve_lds = 0;
+  L->dense = true;
+  for (int i = 0; i < n; ++i) {
+    if (int rc = check_problem(probs + i)) return rc;
+    for (int j = 0; j < i; ++j)
+      SLAM_REQUIRE(probs[j].state != probs[i].state && probs[j].sys != probs[i].sys,
+                   "slam_ba: problems %d and %d of a batch share buffers", j, i);
+    L->b.p[i] = probs[i];
+    L->max_grps = max(L->max_grps, probs[i].n_grps);
+    L->max_blocks = max(L->max_blocks, probs[i].n_blocks);
+    L->solve_lds = std::max(L->solve_lds, sizeof(double) * BlkLds(9 * probs[i].n_cams).total);
+    L->dense = L->dense && !sys_packed(probs[i].n_cams);
+  }
+  SLAM_REQUIRE(n == 1 || L->dense,
+               "slam_ba: batched problems must use the one-workgroup solver (9C <= %d)", kLdsMaxN);
+  return SLAM_OK;
+}
+
+static int launch_reset(const Launch& L, double lam0, hipStream_t s) {
+  k_reset<<<dim3(1, L.n), 64, 0, s>>>(L.b, lam0);
   SLAM_LAUNCHED("k_reset");
   return SLAM_OK;
 }
 
-extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
-  if (int rc = check_problem(prob)) return rc;
-  const slam_ba_problem& p = *prob;
-  hipStream_t s = slam::as_stream(stream);
+static int launch_build(const Launch& L, hipStream_t s) {
   // every entry of sys is written by k_assemble (all upper blocks), so no clearing
-  k_linearize<<<p.n_grps, kLinWG, 0, s>>>(p);
+  k_linearize<<<dim3(L.max_grps, L.n), kLinWG, 0, s>>>(L.b);
   SLAM_LAUNCHED("k_linearize");
-  k_assemble<<<p.n_blocks, kAsmWG, 0, s>>>(p);
+  k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
   SLAM_LAUNCHED("k_assemble");
   return SLAM_OK;
 }
 
-static int solve_step(const slam_ba_problem* prob, bool fuse_decide, void* stream) {
-  if (int rc = check_problem(prob)) return rc;
-  const slam_ba_problem& p = *prob;
-  hipStream_t s = slam::as_stream(stream);
-  const int C9 = 9 * p.n_cams;
-  if (!sys_packed(p.n_cams)) {
-    k_solve_blk<<<1, kBlkWG, sizeof(double) * BlkLds(C9).total, s>>>(p);
+static int launch_solve(const Launch& L, bool fuse_decide, hipStream_t s) {
+  if (L.dense) {
+    k_solve_blk<<<dim3(1, L.n), kBlkWG, L.solve_lds, s>>>(L.b);
     SLAM_LAUNCHED("k_solve_blk");
   } else {
-    tl_solve(p, s);
+    tl_solve(L.b.p[0], s);
     SLAM_LAUNCHED("k_tl_*");
   }
   if (fuse_decide)
-    k_back_trial<true><<<p.n_grps, kGrp, 0, s>>>(p, p.red_part);
+    k_back_trial<true><<<dim3(L.max_grps, L.n), kGrp, 0, s>>>(L.b);
   else
-    k_back_trial<false><<<p.n_grps, kGrp, 0, s>>>(p, p.red_part);
+    k_back_trial<false><<<dim3(L.max_grps, L.n), kGrp, 0, s>>>(L.b);
   SLAM_LAUNCHED("k_back_trial");
   return SLAM_OK;
 }
 
+}  // namespace
+
+extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream) {
+  return slam_ba_reset_batch(prob, 1, lambda0, stream);
+}
+
+extern "C" int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0,
+                                   void* stream) {
+  SLAM_REQUIRE(n_probs >= 0, "slam_ba_reset_batch: n_probs < 0");
+  for (int i0 = 0; i0 < n_probs; i0 += kBaMaxBatch) {
+    Launch L;
+    const int n = min(kBaMaxBatch, n_probs - i0);
+    for (int i = 0; i < n; ++i)
+      if (int rc = check_problem(probs + i0 + i)) return rc;
+    L.n = n;
+    for (int i = 0; i < n; ++i) L.b.p[i] = probs[i0 + i];
+    if (int rc = launch_reset(L, lambda0, slam::as_stream(stream))) return rc;
+  }
+  return SLAM_OK;
+}
+
+extern "C" int slam_ba_build_system(const slam_ba_problem* prob, void* stream) {
+  Launch L;
+  if (int rc = make_launch(prob, 1, &L)) return rc;
+  return launch_build(L, slam::as_stream(stream));
+}
+
 extern "C" int slam_ba_solve_step(const slam_ba_problem* prob, void* stream) {
-  return solve_step(prob, false, stream);
+  Launch L;
+  if (int rc = make_launch(prob, 1, &L)) return rc;
+  return launch_solve(L, false, slam::as_stream(stream));
 }
 
 extern "C" int slam_ba_decide(const slam_ba_problem* prob, void* stream) {
-  if (int rc = check_problem(prob)) return rc;
-  k_decide<<<1, 64, 0, slam::as_stream(stream)>>>(prob->state, prob->small);
+  Launch L;
+  if (int rc = make_launch(prob, 1, &L)) return rc;
+  k_decide<<<dim3(1, 1), 64, 0, slam::as_stream(stream)>>>(L.b);
   SLAM_LAUNCHED("k_decide");
   return SLAM_OK;
 }
 
 extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* stream) {
-  for (int i = 0; i < n_iter; ++i) {
-    if (int rc = slam_ba_build_system(prob, stream)) return rc;
-    if (int rc = solve_step(prob, true, stream)) return rc;  // decide fused into the last group
+  return slam_ba_iterate_batch(prob, 1, n_iter, stream);
+}
+
+extern "C" int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, int n_iter,
+                                     void* stream) {
+  SLAM_REQUIRE(n_probs >= 0 && n_iter >= 0, "slam_ba_iterate_batch: negative count");
+  hipStream_t s = slam::as_stream(stream);
+  // dense problems in chunks of kBaMaxBatch share launches; a packed (tiled
+  // solver) problem iterates on its own
+  int i0 = 0;
+  while (i0 < n_probs) {
+    int n = 0;
+    while (n < kBaMaxBatch && i0 + n < n_probs && (n == 0 || !sys_packed(probs[i0 + n].n_cams)) &&
+           !(n > 0 && sys_packed(probs[i0].n_cams)))
+      ++n;
+    Launch L;
+    if (int rc = make_launch(probs + i0, n, &L)) return rc;
+    for (int it = 0; it < n_iter; ++it) {
+      if (int rc = launch_build(L, s)) return rc;
+      if (int rc = launch_solve(L, true, s)) return rc;  // decide fused into the last group
+    }
+    i0 += n;
   }
   return SLAM_OK;
 }

@@ -80,6 +80,8 @@ SIGNATURES = {
     "slam_ba_decide": [_PROB, c_p],
     "slam_ba_iterate": [_PROB, c_int, c_p],
     "slam_ba_reset": [_PROB, c_double, c_p],
+    "slam_ba_iterate_batch": [_PROB, c_int, c_int, c_p],
+    "slam_ba_reset_batch": [_PROB, c_int, c_double, c_p],
     "slam_pose_chain_objective": [c_p, c_int, c_int, c_int, c_p, c_p],
     "slam_bow_histograms": [c_p, c_p, c_int, c_int, c_int, c_p, c_int, c_p, c_p, c_p],
     "slam_bow_query": [c_p, c_int, c_p, c_p, c_int, c_p, c_p, c_p],

@@ -334,14 +334,20 @@ class BAProblem:
             graphs[n].replay()
 
     def step_distributed(self, group=None):
-        """One LM iteration with RCCL all-reduce of the camera system (multi-rank)."""
+        """One LM iteration with RCCL all-reduce of the camera system (multi-rank).
+
+        The kernels and the collectives are ordered on one stream: the body runs
+        with self.stream current (torch.distributed orders its work against the
+        current stream)."""
         import torch.distributed as dist
 
-        self.build_system()
-        dist.all_reduce(self.t["sys"], group=group)
-        self.solve_step()
-        dist.all_reduce(self.t["small"], group=group)
-        self.decide()
+        with torch.cuda.stream(self.stream if self.stream is not None
+                               else torch.cuda.current_stream()):
+            self.build_system()
+            dist.all_reduce(self.t["sys"], group=group)
+            self.solve_step()
+            dist.all_reduce(self.t["small"], group=group)
+            self.decide()
 
     # -- host views ---------------------------------------------------------------
     def state(self) -> dict:
@@ -356,20 +362,93 @@ class BAProblem:
         return self.state()["COST"]
 
     def solve(self, max_iters=100, ftol=1e-10, check_every=5):
-        """Iterate until the relative cost decrease of an accepted step is < ftol
-        or max_iters.  Returns the final state dict."""
+        """Iterate until a batch of `check_every` iterations that accepted at
+        least one step lowered the cost by less than ftol (relative), until
+        lambda saturates (no step can be accepted any more), or max_iters.
+        A batch whose steps were all rejected leaves the cost unchanged and
+        says nothing about convergence, so it never stops the solve.
+        Returns the final state dict."""
         done = 0
-        last = None
+        st = self.state()
         while done < max_iters:
             k = min(check_every, max_iters - done)
+            c0, n0 = st["COST"], st["NACCEPT"]
             self.iterate(k)
             done += k
             st = self.state()
-            c = st["COST"]
-            if last is not None and abs(last - c) <= ftol * max(c, 1e-300) and st["LAMBDA"] < 1e8:
+            if st["LAMBDA"] >= 1e30:
                 break
-            last = c
-        return self.state()
+            if st["NACCEPT"] > n0 and abs(c0 - st["COST"]) <= ftol * max(st["COST"], 1e-300):
+                break
+        return st
+
+
+class BABatch:
+    """Independent BA problems (e.g. the local-BA windows of one tracking
+    batch) advanced together: each LM iteration of all of them is one set of
+    launches (slam_ba_iterate_batch: one problem per grid row, up to
+    SLAM_BA_MAX_BATCH per launch), so B windows cost about one window's
+    latency instead of B.  Every problem keeps its own device buffers and LM
+    state; its iterates equal the ones BAProblem.iterate gives it alone."""
+
+    MAX_BATCH = 8  # SLAM_BA_MAX_BATCH
+
+    def __init__(self, problems, stream=None):
+        self.problems = list(problems)
+        if not self.problems:
+            raise ValueError("BABatch needs at least one problem")
+        if len(self.problems) > 1 and any(packed(p.C) for p in self.problems):
+            raise ValueError(f"batched problems must have 9C <= {LDS_MAX_N} (one-workgroup solver)")
+        self.stream = stream
+        arr = (_Prob * len(self.problems))()
+        for i, p in enumerate(self.problems):
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(p._s), ctypes.sizeof(_Prob))
+        self._arr = arr
+        self._graphs = {}
+
+    def _sp(self):
+        return stream_ptr(self.stream)
+
+    def reset(self, lam0=1e-4):
+        _lib.call("slam_ba_reset_batch", self._arr, len(self.problems), float(lam0), self._sp())
+
+    def restore(self, lam0=1e-4):
+        """Reload every problem's initial parameters, reset every LM state."""
+        with torch.cuda.stream(self.stream if self.stream is not None
+                               else torch.cuda.current_stream()):
+            for p in self.problems:
+                p.t["cams0"].copy_(p._init[0])
+                p.t["pts0"].copy_(p._init[1])
+        self.reset(lam0)
+
+    def iterate(self, n: int = 1):
+        _lib.call("slam_ba_iterate_batch", self._arr, len(self.problems), int(n), self._sp())
+
+    def iterate_graphed(self, n: int = 1, with_restore=False):
+        """n LM iterations of every problem (optionally preceded by restore())
+        replayed from one captured HIP graph."""
+        key = (n, with_restore)
+        if key not in self._graphs:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            saved = self.stream
+            self.stream = s
+            try:
+                with torch.cuda.graph(g, stream=s):
+                    if with_restore:
+                        self.restore()
+                    self.iterate(n)
+            finally:
+                self.stream = saved
+            torch.cuda.current_stream().wait_stream(s)
+            self._graphs[key] = g
+        with torch.cuda.stream(self.stream if self.stream is not None else
+                               torch.cuda.current_stream()):
+            self._graphs[key].replay()
+
+    def states(self):
+        return [p.state() for p in self.problems]
 
 
 # ----------------------------------------------------------------------------- kernels

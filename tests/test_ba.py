@@ -326,3 +326,119 @@ def test_planner_packed_block_list():
     assert len(pl2["blocks"]) == C * (C + 1) // 2
     with pytest.raises(ValueError):
         ba.plan(C, len(pts), ci, pi, block_list=ba.block_index(np.arange(C), np.arange(C), C))
+
+
+# ----------------------------------------------------------------------------- batched windows
+def _window(seed, C, P, k):
+    cams, pts, ci, pi, qs = make_problem(seed, C, P, k)
+    rng = np.random.default_rng(seed + 100)
+    cams0 = cams.copy()
+    cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
+    return cams0, pts + rng.normal(0, 0.05, pts.shape), ci, pi, qs
+
+
+WINDOWS = [(31, 10, 5000, 6), (32, 8, 1200, 5), (33, 6, 700, 4), (34, 10, 3000, 6), (35, 12, 900, 3)]
+
+
+@pytest.mark.gpu
+def test_gpu_batched_windows_equal_solo_iterates():
+    """slam_ba_iterate_batch: windows of different shapes (C3 = 10 x 5000 x 30k
+    among them) advanced together give, bit for bit, the LM state and
+    parameters each gets from solo iterations; graph replay with restore too."""
+    import torch
+    from slam355 import ba
+
+    wins = [_window(*w) for w in WINDOWS]
+    solo = [ba.BAProblem(*w) for w in wins]
+    for p in solo:
+        p.iterate(6)
+    batch = ba.BABatch([ba.BAProblem(*w) for w in wins])
+    batch.iterate(4)
+    batch.iterate(2)
+    for a, b in zip(solo, batch.problems):
+        assert a.state() == b.state()
+        for x, y in zip(a.params(), b.params()):
+            assert np.array_equal(x, y)
+    for _ in range(2):  # replayed graph of (restore + 6 iterations), twice
+        batch.iterate_graphed(6, with_restore=True)
+    torch.cuda.synchronize()
+    for a, b in zip(solo, batch.problems):
+        assert a.state() == b.state()
+
+
+@pytest.mark.gpu
+def test_gpu_batched_windows_match_oracle_schur_lm():
+    """Per window of a batch, 3 LM iterations (C3 included) equal the oracle's
+    Schur LM (oracle.ba.lm_iteration_schur): accept flags, costs 1e-9, lambda,
+    parameters 1e-6."""
+    from slam355 import ba
+
+    wins = [_window(*w) for w in WINDOWS[:4]]
+    batch = ba.BABatch([ba.BAProblem(*w) for w in wins])
+    ost = [oba.LMState(1e-4) for _ in wins]
+    cur = [(w[0].copy(), w[1].copy()) for w in wins]
+    pairs = [oba._obs_pairs(w[2], w[3]) for w in wins]
+    for it in range(3):
+        batch.iterate(1)
+        for i, w in enumerate(wins):
+            oc, op, info = oba.lm_iteration_schur(cur[i][0], cur[i][1], w[2], w[3], w[4], ost[i],
+                                                  pairs[i])
+            cur[i] = (oc, op)
+            s = batch.problems[i].state()
+            assert bool(s["ACCEPTED"]) == bool(info["accepted"]), (i, it)
+            assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-9 * info["cost_new"], (i, it)
+            assert abs(s["LAMBDA"] - ost[i].lam) <= 1e-6 * ost[i].lam, (i, it)
+            gc, gp = batch.problems[i].params()
+            assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9), (i, it)
+            assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), (i, it)
+
+
+@pytest.mark.gpu
+def test_gpu_c4_window_iterates_match_oracle():
+    """BASELINE C4 shape on one GPU (64 KF x 50k points x 300k obs, the tiled
+    solver on the packed 576-unknown system): 2 LM iterations equal the
+    oracle's Schur LM."""
+    from slam355 import ba
+    from slam355.synthetic import ba_problem, perturb
+
+    rng = np.random.default_rng(7)
+    cams, pts, ci, pi, qs = ba_problem(rng, 64, 50000, 6)
+    c0, p0 = perturb(rng, cams, pts)
+    prob = ba.BAProblem(c0, p0, ci, pi, qs)
+    st = oba.LMState(1e-4)
+    oc, op = c0.copy(), p0.copy()
+    pairs = oba._obs_pairs(ci, pi)
+    for it in range(2):
+        prob.iterate(1)
+        oc, op, info = oba.lm_iteration_schur(oc, op, ci, pi, qs, st, pairs)
+        s = prob.state()
+        assert s["CHOL_FAIL"] == 0.0 and bool(s["ACCEPTED"]) == bool(info["accepted"]), it
+        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-9 * info["cost_new"], it
+        gc, gp = prob.params()
+        assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9), it
+        assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), it
+
+
+@pytest.mark.gpu
+def test_gpu_c5_global_ba_first_iteration_matches_oracle():
+    """BASELINE C5 shape (loop-closure global BA, 500 KF x 200k points x 1.2M
+    obs, 4500-unknown reduced system): the first LM iteration's accept flag,
+    trial cost and camera step equal the oracle's Schur LM."""
+    from slam355 import ba
+    from slam355.synthetic import ba_problem_loop, perturb
+
+    rng = np.random.default_rng(7)
+    cams, pts, ci, pi, qs = ba_problem_loop(rng, 500, 200000, 6)
+    c0, p0 = perturb(rng, cams, pts)
+    prob = ba.BAProblem(c0, p0, ci, pi, qs)
+    prob.iterate(1)
+    st = oba.LMState(1e-4)
+    oc, op, info = oba.lm_iteration_schur(c0, p0, ci, pi, qs, st, oba._obs_pairs(ci, pi))
+    s = prob.state()
+    assert s["CHOL_FAIL"] == 0.0 and bool(s["ACCEPTED"]) == bool(info["accepted"])
+    assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-9 * info["cost_new"]
+    assert abs(s["COST"] - info["cost_new" if info["accepted"] else "cost"]) <= 1e-9 * s["COST"]
+    gc, gp = prob.params()
+    assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9)
+    assert np.allclose(gp, op, rtol=1e-6, atol=1e-9)

@@ -133,8 +133,8 @@ def test_gpu_device_chain_stale_transform():
     dev = torch.device("cuda")
     st = torch.from_numpy(np.concatenate([np.eye(4), np.eye(4)]).ravel()).to(dev)
     out = torch.zeros((4, 16), dtype=torch.float64, device=dev)
-    _lib.call("slam_pose_chain", ptr(torch.from_numpy(r).to(dev)), ptr(torch.from_numpy(t).to(dev)),
-              ptr(torch.from_numpy(n).to(dev)), 4, ptr(st), ptr(out), stream_ptr())
+    tr, tt, tn = (torch.from_numpy(a).to(dev) for a in (r, t, n))  # alive until the kernel ran
+    _lib.call("slam_pose_chain", ptr(tr), ptr(tt), ptr(tn), 4, ptr(st), ptr(out), stream_ptr())
     P, T = chain_poses(np.eye(4), r, t, n)
     assert np.allclose(out.cpu().numpy().reshape(4, 4, 4), P, rtol=0, atol=1e-12)
     assert np.allclose(st.cpu().numpy()[16:].reshape(4, 4), T, rtol=0, atol=1e-14)
