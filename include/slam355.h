@@ -284,6 +284,10 @@ typedef struct slam_ba_problem {
                             common point (across all ranks), sorted          */
   int32_t n_cslots;      /* (group, camera) slots                             */
   int32_t n_bslots;      /* (group, camera-pair block) slots                  */
+  int32_t lin_mode;      /* 0: slot linearisation (k_linearize; groups = point
+                            groups); 1: camera-union linearisation
+                            (k_lin_mfma; grp_* = chunks, slots per supergroup) */
+  int32_t n_sgrps;       /* lin_mode 1: supergroups (>= 1)                    */
   int32_t reserved;
   double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
   double* pts[2];               /* [P][3]                                      */
@@ -316,6 +320,15 @@ typedef struct slam_ba_problem {
   double* small;                /* [4] trial |r|^2, sum pred_p (all-reduced)   */
   double* state;                /* [SLAM_BA_ST_SLOTS]                          */
   uint32_t* ticket;             /* [1] zero-initialised completion counter     */
+  /* lin_mode 1 only (else may be null): points renumbered by camera span;
+   * grp_ptr = chunks (<= 128 obs, <= 16 points); grp_cslot / grp_bslot are
+   * indexed by supergroup. */
+  const int32_t* sg_ptr;        /* [n_sgrps+1] chunk range of each supergroup    */
+  const int32_t* sg_cams;       /* [n_sgrps][8] its cameras (<= 7, sorted, -1 padded) */
+  const int32_t* obs_la;        /* [O] position of the obs's camera in sg_cams  */
+  const int32_t* chk_cobs;      /* [O] chunk-local obs indices sorted by (la, obs) */
+  const int32_t* chk_cptr;      /* [n_grps][8] start of each camera's run in chk_cobs */
+  const int32_t* bslot_ab;      /* [n_bslots] camera pair a | b << 8 (a < b) of a block slot */
 } slam_ba_problem;
 
 /* Problems per batched launch (slam_ba_iterate_batch splits larger batches). */

@@ -515,6 +515,248 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 #endif
 }
 
+// ---------------------------------------------------------------- camera-union linearisation
+// lin_mode 1 (planner ba.plan_mfma): a workgroup owns a supergroup -- a run of
+// chunks (<= kMObs observations, <= kMPts whole points each) whose points
+// together see m <= kMCams cameras -- and forms its whole share of the reduced
+// camera system as ONE dense (9m x 9m) matrix:
+//   Schur part  T = sum_p Y_p W_p^T  (W_p: the point's 9m x 3 camera-block
+//               column, W~_{p,a} = sum of Jc_o^T Jp_o over its observations by
+//               camera a, zero for cameras that do not see p; Y_p = W_p V*_p^-1)
+//               on the f64 matrix cores: per point, one v_mfma_f64_16x16x4_f64
+//               per upper 16x16 tile of T (K = the point's 3 coordinates + 0);
+//   U part      U_a = sum_o Jc_o^T Jc_o, Jc^T r, Jc^T u, diag U, |r|^2 per camera
+//               on the vector ALUs (waves 2 and 3, beside their MFMAs),
+// accumulated in registers across the supergroup's chunks and written once:
+// per camera a one cpart row (U_a - T_aa, ...), per co-observed camera pair
+// a < b one bpart row (T_ab) -- the rows k_assemble sums.  Per point: V, g,
+// V*, V*^-1, e as k_linearize (ptdata).
+constexpr int kMObs = 128, kMPts = 16, kMCams = 7, kMRows = 64;
+constexpr int kMWG = 256;
+struct MLds {
+  double jc[kMObs][18];          // Jc rows (2 x 9)
+  double jp[kMObs][6];           // Jp rows (2 x 3)
+  double ru[kMObs][4];           // r0 r1 u0 u1
+  double vi[kMPts][6];           // V*^-1 (i00 i01 i02 i11 i12 i22)
+  double e[kMPts][3];
+  double yt[kMPts][3][kMRows];   // Y_p, [point][k][row]: the MFMA A operand
+  double wt[kMPts][3][kMRows];   // W_p, [point][k][row]: the MFMA B operand
+  int lpt[kMObs];                // chunk-local point of each observation
+  int la[kMObs];                 // supergroup-local camera of each observation
+  int cobs[kMObs];               // chunk-local observations sorted by camera
+  int cptr[8];                   // their per-camera runs
+};
+static_assert(sizeof(MLds) <= 80 * 1024, "k_lin_mfma: two workgroups per CU");
+static_assert(9 * kMCams <= kMRows, "k_lin_mfma: 9m rows in 4 tile rows");
+static_assert(2 * kMPts * 3 * kMRows >= kMRows * kMRows, "T staging aliases yt/wt");
+
+__global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
+  BA_PROB(bat);
+  const int sg = blockIdx.x;
+  if (sg >= p.n_sgrps) return;  // batch: grid.x covers the largest problem
+  lm_wave_priority();
+  __shared__ MLds L;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ch0 = p.sg_ptr[sg], ch1 = p.sg_ptr[sg + 1];
+  const int cs0 = p.grp_cslot[sg], m = p.grp_cslot[sg + 1] - cs0;
+  const int nt = (9 * m + 15) >> 4;  // tile rows of T
+  const int cur = cur_of(p.state);
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  // rows >= 9m of Y/W stay zero for the whole supergroup
+  for (int i = t; i < 2 * kMPts * 3 * kMRows; i += kMWG) (&L.yt[0][0][0])[i] = 0.0;
+  // this wave's upper tiles (I <= J), dealt round-robin: <= 3 per wave
+  int tI[3], tJ[3];
+  int ntl = 0;
+  {
+    int s = 0;
+    for (int I = 0; I < nt; ++I)
+      for (int J = I; J < nt; ++J, ++s)
+        if ((s & 3) == wid && ntl < 3) {
+          tI[ntl] = I;
+          tJ[ntl] = J;
+          ++ntl;
+        }
+  }
+  d4 acc[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  // U item of this lane: waves 2, 3 (lanes 0..31) -> (camera a, row i)
+  const int uq = (wid - 2) * 32 + lane;
+  const bool uown = wid >= 2 && lane < 32 && uq < 9 * m;
+  const int ua = uown ? uq / 9 : 0, ui = uown ? uq - 9 * (uq / 9) : 0;
+  double uacc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) uacc[j] = 0.0;
+  double ujr = 0.0, uju = 0.0, udg = 0.0, ucost = 0.0;
+  const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
+
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int p0 = p.grp_ptr[ch], p1 = p.grp_ptr[ch + 1];
+    const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
+    const int nobs = o1 - o0, npts = p1 - p0;
+    __syncthreads();  // the previous chunk's readers are done with L
+    // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350)
+    if (t < nobs) {
+      const int o = o0 + t;
+      const int pt = p.obs_pt[o];
+      double r[2], J[2][12];
+      reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
+                          p.obs_q + 2 * o, r, J);
+      clamp_rows<true>(r, J);
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) L.jc[t][9 * a + i] = J[a][i];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) L.jp[t][3 * a + c] = J[a][9 + c];
+        L.ru[t][a] = r[a];
+      }
+      L.lpt[t] = pt - p0;
+      L.la[t] = p.obs_la[o];
+      L.cobs[t] = p.chk_cobs[o];
+    }
+    if (t < 8) L.cptr[t] = p.chk_cptr[8 * ch + t];
+    __syncthreads();
+    // (B) per point: V, g, V* = V + lam diag(V), V*^-1 (cofactors), e = V*^-1 g
+    if (t < npts) {
+      const int pt = p0 + t;
+      double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+      for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const double j0 = L.jp[k][3 * a], j1 = L.jp[k][3 * a + 1], j2 = L.jp[k][3 * a + 2];
+          const double rr = L.ru[k][a];
+          V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
+          V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
+          g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
+        }
+      }
+      const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
+      const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
+      const double a01 = V01, a02 = V02, a12 = V12;
+      const double c00 = a11 * a22 - a12 * a12;
+      const double c01 = a02 * a12 - a01 * a22;
+      const double c02 = a01 * a12 - a02 * a11;
+      const double c11 = a00 * a22 - a02 * a02;
+      const double c12 = a01 * a02 - a00 * a12;
+      const double c22 = a00 * a11 - a01 * a01;
+      const double det = a00 * c00 + a01 * c01 + a02 * c02;
+      const double id = det != 0.0 ? 1.0 / det : 0.0;
+      const double iv[6] = {c00 * id, c01 * id, c02 * id, c11 * id, c12 * id, c22 * id};
+      const double e0 = iv[0] * g0 + iv[1] * g1 + iv[2] * g2;
+      const double e1 = iv[1] * g0 + iv[3] * g1 + iv[4] * g2;
+      const double e2 = iv[2] * g0 + iv[4] * g1 + iv[5] * g2;
+      double* pd = p.ptdata + (size_t)pt * kPtData;
+      pd[0] = e0; pd[1] = e1; pd[2] = e2;
+      pd[3] = g0; pd[4] = g1; pd[5] = g2;
+      pd[6] = d0; pd[7] = d1; pd[8] = d2;
+      L.e[t][0] = e0; L.e[t][1] = e1; L.e[t][2] = e2;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        pd[9 + k] = iv[k];
+        L.vi[t][k] = iv[k];
+      }
+    }
+    __syncthreads();
+    // (C) lanes 0..127: u_o = Jp_o e_p; lanes 128..: (point, camera) items ->
+    //     W~_{p,a} (9x3) and Y = W~ V*^-1 into the MFMA operand planes
+    if (t < nobs) {
+      const double* e = L.e[L.lpt[t]];
+      L.ru[t][2] = L.jp[t][0] * e[0] + L.jp[t][1] * e[1] + L.jp[t][2] * e[2];
+      L.ru[t][3] = L.jp[t][3] * e[0] + L.jp[t][4] * e[1] + L.jp[t][5] * e[2];
+    } else if (t >= kMObs && t - kMObs < npts * m) {
+      const int q = t - kMObs, lp = q / m, a = q - m * (q / m);
+      double W[9][3];
+#pragma unroll
+      for (int i = 0; i < 9; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
+      const int kb = p.pt_ptr[p0 + lp] - o0, ke = p.pt_ptr[p0 + lp + 1] - o0;
+      for (int k = kb; k < ke; ++k) {
+        if (L.la[k] != a) continue;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            W[i][c] += L.jc[k][i] * L.jp[k][c] + L.jc[k][9 + i] * L.jp[k][3 + c];
+      }
+      const double* vi = L.vi[lp];
+      const double V[3][3] = {{vi[0], vi[1], vi[2]}, {vi[1], vi[3], vi[4]}, {vi[2], vi[4], vi[5]}};
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        const int row = 9 * a + i;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          L.wt[lp][c][row] = W[i][c];
+          L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
+        }
+      }
+    }
+    __syncthreads();
+    // (D) T += Y_p W_p^T on the matrix cores, one MFMA per point and tile:
+    //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0
+    for (int lp = 0; lp < npts; ++lp) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        if (s >= ntl) break;  // uniform per wave
+        const double av = L.yt[lp][mkc][16 * tI[s] + mi];
+        const double bv = L.wt[lp][mkc][16 * tJ[s] + mi];
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(mk < 3 ? av : 0.0, mk < 3 ? bv : 0.0,
+                                                     acc[s], 0, 0, 0);
+      }
+    }
+    //     U part: lane (a, i) over the chunk's observations by camera a
+    if (uown) {
+      for (int q = L.cptr[ua]; q < L.cptr[ua + 1]; ++q) {
+        const int k = L.cobs[q];
+        const double* jc = L.jc[k];
+        const double a0 = jc[ui], a1 = jc[9 + ui];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) uacc[j] = __builtin_fma(a0, jc[j], __builtin_fma(a1, jc[9 + j], uacc[j]));
+        const double r0 = L.ru[k][0], r1 = L.ru[k][1];
+        ujr = __builtin_fma(a0, r0, __builtin_fma(a1, r1, ujr));
+        uju = __builtin_fma(a0, L.ru[k][2], __builtin_fma(a1, L.ru[k][3], uju));
+        udg = __builtin_fma(a0, a0, __builtin_fma(a1, a1, udg));
+        ucost = __builtin_fma(r0, r0, __builtin_fma(r1, r1, ucost));
+      }
+    }
+  }
+  // (E) T -> LDS staging (aliases the operand planes), then the partial rows
+  __syncthreads();
+  double* T = &L.yt[0][0][0];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    if (s >= ntl) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      T[(16 * tI[s] + mk + 4 * r) * kMRows + 16 * tJ[s] + mi] = acc[s][r];
+  }
+  __syncthreads();
+  if (uown) {
+    // T is symmetric; only upper tiles were formed
+    double* out = p.cpart + (size_t)p.cslot_row[cs0 + ua] * kCPart;
+    const int row = 9 * ua + ui;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int col = 9 * ua + j;
+      const double tv = (row >> 4) <= (col >> 4) ? T[row * kMRows + col] : T[col * kMRows + row];
+      out[9 * ui + j] = uacc[j] - tv;
+    }
+    out[81 + ui] = ujr;
+    out[90 + ui] = uju;
+    out[99 + ui] = udg;
+    if (ui == 0) out[108] = ucost;
+  }
+  const int bs0 = p.grp_bslot[sg], nb = p.grp_bslot[sg + 1] - bs0;
+  for (int q = t; q < 81 * nb; q += kMWG) {
+    const int pr = q / 81, e = q - 81 * (q / 81);
+    const int ab = p.bslot_ab[bs0 + pr], a = ab & 255, b = ab >> 8;
+    const int i = e / 9, j = e - 9 * (e / 9);
+    p.bpart[(size_t)p.bslot_row[bs0 + pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
+  }
+}
+
 // Column sums of the n-wide rows [rb, re) of part (row stride `stride`): the
 // workgroup's lanes are (part k, column e) pairs; part k takes rows rb + k,
 // rb + k + nparts, ... with 8 loads in flight, then the parts are added in
@@ -1673,6 +1915,10 @@ int check_problem(const slam_ba_problem* p) {
                    p->small && p->red_part && p->delta_c,
                "slam_ba: null buffer");
   SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
+  SLAM_REQUIRE(p->lin_mode == 0 || p->lin_mode == 1, "slam_ba: lin_mode must be 0 or 1");
+  SLAM_REQUIRE(p->lin_mode == 0 || (p->n_sgrps >= 1 && p->sg_ptr && p->sg_cams && p->obs_la &&
+                                     p->chk_cobs && p->chk_cptr && p->bslot_ab),
+               "slam_ba: lin_mode 1 needs n_sgrps >= 1 and the supergroup tables");
   SLAM_REQUIRE(sys_packed(p->n_cams) ? (p->n_blocks >= p->n_cams &&
                                         p->n_blocks <= p->n_cams * (p->n_cams + 1) / 2)
                                      : p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
@@ -1730,7 +1976,7 @@ namespace {
 // extents that cover the largest of them.
 struct Launch {
   BaBatch b;
-  int n, max_grps, max_blocks;
+  int n, max_grps, max_blocks, max_sgrps, mode;
   size_t solve_lds;
   bool dense;
 };
@@ -1739,7 +1985,8 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
   SLAM_REQUIRE(n >= 1 && n <= kBaMaxBatch, "slam_ba: batch of %d problems (1..%d)", n, kBaMaxBatch);
   SLAM_REQUIRE(probs != nullptr, "slam_ba: null problem array");
   L->n = n;
-  L->max_grps = L->max_blocks = 0;
+  L->max_grps = L->max_blocks = L->max_sgrps = 0;
+  L->mode = probs[0].lin_mode;
   L->solve_lds = 0;
   L->dense = true;
   for (int i = 0; i < n; ++i) {
@@ -1747,8 +1994,11 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
     for (int j = 0; j < i; ++j)
       SLAM_REQUIRE(probs[j].state != probs[i].state && probs[j].sys != probs[i].sys,
                    "slam_ba: problems %d and %d of a batch share buffers", j, i);
+    SLAM_REQUIRE(probs[i].lin_mode == L->mode,
+                 "slam_ba: problems of one batch must share lin_mode");
     L->b.p[i] = probs[i];
     L->max_grps = max(L->max_grps, probs[i].n_grps);
+    L->max_sgrps = max(L->max_sgrps, probs[i].n_sgrps);
     L->max_blocks = max(L->max_blocks, probs[i].n_blocks);
     L->solve_lds = std::max(L->solve_lds, sizeof(double) * BlkLds(9 * probs[i].n_cams).total);
     L->dense = L->dense && !sys_packed(probs[i].n_cams);
@@ -1766,8 +2016,13 @@ static int launch_reset(const Launch& L, double lam0, hipStream_t s) {
 
 static int launch_build(const Launch& L, hipStream_t s) {
   // every entry of sys is written by k_assemble (all upper blocks), so no clearing
-  k_linearize<<<dim3(L.max_grps, L.n), kLinWG, 0, s>>>(L.b);
-  SLAM_LAUNCHED("k_linearize");
+  if (L.mode == 1) {
+    k_lin_mfma<<<dim3(L.max_sgrps, L.n), kMWG, 0, s>>>(L.b);
+    SLAM_LAUNCHED("k_lin_mfma");
+  } else {
+    k_linearize<<<dim3(L.max_grps, L.n), kLinWG, 0, s>>>(L.b);
+    SLAM_LAUNCHED("k_linearize");
+  }
   k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
   SLAM_LAUNCHED("k_assemble");
   return SLAM_OK;

@@ -27,7 +27,8 @@ class BAProblemStruct(ctypes.Structure):
     """Mirror of `slam_ba_problem` (include/slam355.h)."""
     _fields_ = [
         ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_grps", c_i32),
-        ("n_blocks", c_i32), ("n_cslots", c_i32), ("n_bslots", c_i32), ("reserved", c_i32),
+        ("n_blocks", c_i32), ("n_cslots", c_i32), ("n_bslots", c_i32), ("lin_mode", c_i32),
+        ("n_sgrps", c_i32), ("reserved", c_i32),
         ("cams", c_p * 2), ("pts", c_p * 2), ("camrec", c_p * 2),
         ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p), ("grp_ptr", c_p),
         ("grp_cslot", c_p), ("cslot_cam", c_p), ("cslot_obs_ptr", c_p), ("cslot_obs", c_p),
@@ -36,6 +37,8 @@ class BAProblemStruct(ctypes.Structure):
         ("bslot_row", c_p), ("ptdata", c_p), ("cpart", c_p), ("bpart", c_p),
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
         ("state", c_p), ("ticket", c_p),
+        ("sg_ptr", c_p), ("sg_cams", c_p), ("obs_la", c_p), ("chk_cobs", c_p), ("chk_cptr", c_p),
+        ("bslot_ab", c_p),
     ]
 
 

@@ -202,6 +202,195 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, block_list=None):
         n_obs=O)
 
 
+# Camera-union linearisation (csrc/ba.hip k_lin_mfma): points ordered by their
+# camera span, cut into chunks and the chunks into supergroups whose points
+# together see at most MF_CAMS cameras, so a supergroup's share of the
+# reduced camera system is one dense (9m x 9m, m <= 7) matrix: the Schur term
+# sum_p Y_p W_p^T on the f64 matrix cores, U on the vector ALUs.
+MF_CHUNK_OBS = 128  # kMObs: observations per chunk (also k_back_trial's group cap)
+MF_CHUNK_PTS = 16   # kMPts: points per chunk
+MF_CAMS = 7         # kMCams: cameras per supergroup (9m <= 63 rows: 4 MFMA tile rows)
+
+
+def _popcount(x: int) -> int:
+    return bin(x).count("1")
+
+
+def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=None):
+    """Index tables for the camera-union linearisation, or None when a point
+    sees more than MF_CAMS cameras (then `plan` and the slot kernel are used).
+
+    Points are renumbered: sorted by (first camera, last camera, index), so
+    points with the same camera span are adjacent; `perm` [P] maps the new
+    index to the caller's.  Observations are sorted by (new point, camera) and
+    cut into chunks (grp_ptr: whole points, <= MF_CHUNK_OBS observations and
+    <= MF_CHUNK_PTS points); consecutive chunks form supergroups (sg_ptr: a
+    chunk range, <= chunks_per_wg chunks) of at most MF_CAMS distinct cameras
+    (sg_cams, sorted; obs_la = position of each observation's camera in its
+    supergroup's list).  Camera slots are (supergroup, camera) -- grp_cslot
+    indexes supergroups here -- and block slots (supergroup, a < b) for every
+    pair of its cameras that share a point (bslot_ab = a | b << 8)."""
+    O, C, P = len(cam_idx), n_cams, n_pts
+    cam_idx = np.asarray(cam_idx, np.int64)
+    pt_idx = np.asarray(pt_idx, np.int64)
+    order0 = np.lexsort((cam_idx, pt_idx))
+    oc, op = cam_idx[order0], pt_idx[order0]
+    cnt = np.bincount(op, minlength=P)
+    if P and cnt.max() > MF_CHUNK_OBS:
+        return None
+    first = np.ones(O, bool)
+    first[1:] = (oc[1:] != oc[:-1]) | (op[1:] != op[:-1])
+    ndist = np.bincount(op[first], minlength=P)
+    if P and ndist.max() > MF_CAMS:
+        return None
+    ptr0 = np.zeros(P + 1, np.int64)
+    np.cumsum(cnt, out=ptr0[1:])
+    has = cnt > 0
+    lo = np.full(P, C, np.int64)
+    hi = np.full(P, C, np.int64)
+    if O:
+        lo[has] = np.minimum.reduceat(oc, ptr0[:-1][has])
+        hi[has] = np.maximum.reduceat(oc, ptr0[:-1][has])
+    perm = np.lexsort((np.arange(P), hi, lo))  # new -> old
+    inv = np.empty(P, np.int64)
+    inv[perm] = np.arange(P)
+    npt = inv[pt_idx] if O else pt_idx
+    order = np.lexsort((cam_idx, npt))
+    obs_cam = cam_idx[order]
+    obs_pt = npt[order]
+    pt_ptr = np.zeros(P + 1, np.int64)
+    np.cumsum(np.bincount(obs_pt, minlength=P), out=pt_ptr[1:])
+    # camera-set bitmask per (new) point
+    fst = np.ones(O, bool)
+    fst[1:] = (obs_cam[1:] != obs_cam[:-1]) | (obs_pt[1:] != obs_pt[:-1])
+    masks = [0] * P
+    for q, c in zip(obs_pt[fst].tolist(), obs_cam[fst].tolist()):
+        masks[q] |= 1 << c
+    cntn = np.diff(pt_ptr).tolist()
+    n_chunks_est = max(1, -(-O // MF_CHUNK_OBS))
+    if chunks_per_wg is None:  # enough workgroups to cover the chip, fewer partial rows
+        chunks_per_wg = int(min(8, max(1, n_chunks_est // 512)))
+    S = max(1, int(chunks_per_wg))
+    grp = [0]
+    sg = [0]
+    sg_masks = []
+    union = 0
+    ch_obs = ch_pts = 0
+    sg_ch = 1
+    for q in range(P):
+        n, mk = cntn[q], masks[q]
+        if _popcount(union | mk) > MF_CAMS:  # new supergroup (and chunk)
+            grp.append(q)
+            sg.append(len(grp) - 1)
+            sg_masks.append(union)
+            union, ch_obs, ch_pts, sg_ch = 0, 0, 0, 1
+        elif ch_obs + n > MF_CHUNK_OBS or ch_pts + 1 > MF_CHUNK_PTS:  # new chunk
+            grp.append(q)
+            ch_obs = ch_pts = 0
+            if sg_ch == S:
+                sg.append(len(grp) - 1)
+                sg_masks.append(union)
+                union, sg_ch = 0, 1
+            else:
+                sg_ch += 1
+        union |= mk
+        ch_obs += n
+        ch_pts += 1
+    grp.append(P)
+    sg.append(len(grp) - 1)
+    sg_masks.append(union)
+    grp_ptr = np.asarray(grp, np.int64)
+    sg_ptr = np.asarray(sg, np.int64)
+    G, NS = len(grp_ptr) - 1, len(sg_ptr) - 1
+    sg_cams = np.full((NS, 8), -1, np.int64)
+    ms = np.zeros(NS, np.int64)
+    for k, mk in enumerate(sg_masks):
+        cs = [c for c in range(C) if (mk >> c) & 1] if mk else []
+        ms[k] = len(cs)
+        sg_cams[k, :len(cs)] = cs
+    # supergroup / chunk of every observation and its camera's position in the union
+    chunk_of_pt = np.repeat(np.arange(G), np.diff(grp_ptr))
+    sg_of_chunk = np.repeat(np.arange(NS), np.diff(sg_ptr))
+    obs_chunk = chunk_of_pt[obs_pt] if O else np.zeros(0, np.int64)
+    obs_sg = sg_of_chunk[obs_chunk] if O else np.zeros(0, np.int64)
+    # position of obs_cam in sg_cams[obs_sg] (sorted rows, -1 padded at the end)
+    rowc = np.where(sg_cams < 0, C + 1, sg_cams)
+    obs_la = (rowc[obs_sg] < obs_cam[:, None]).sum(1) if O else np.zeros(0, np.int64)
+    # chunk-local observation lists sorted by (la, obs)
+    loc = np.arange(O) - pt_ptr[grp_ptr[:-1]][obs_chunk] if O else np.zeros(0, np.int64)
+    so = np.lexsort((loc, obs_la, obs_chunk)) if O else np.zeros(0, np.int64)
+    chk_cobs = loc[so]
+    chk_cptr = np.zeros((G, 8), np.int64)
+    o_start = pt_ptr[grp_ptr[:-1]]
+    nob = pt_ptr[grp_ptr[1:]] - o_start
+    for a in range(8):
+        # number of obs of the chunk with la < a
+        chk_cptr[:, a] = np.bincount(obs_chunk[obs_la < a], minlength=G) if O else 0
+    chk_cptr = np.minimum(chk_cptr, nob[:, None])
+    # camera slots: (supergroup, a), rows camera-major in supergroup order
+    grp_cslot = np.zeros(NS + 1, np.int64)
+    np.cumsum(ms, out=grp_cslot[1:])
+    cslot_sg = np.repeat(np.arange(NS), ms)
+    cslot_cam = sg_cams[cslot_sg, np.arange(len(cslot_sg)) - grp_cslot[cslot_sg]]
+    cam_cslots = np.lexsort((cslot_sg, cslot_cam))
+    cslot_row = np.empty(len(cam_cslots), np.int64)
+    cslot_row[cam_cslots] = np.arange(len(cam_cslots))
+    cam_cslot_ptr = np.zeros(C + 1, np.int64)
+    np.cumsum(np.bincount(cslot_cam, minlength=C), out=cam_cslot_ptr[1:])
+    # block slots: (supergroup, a < b) co-observed within the supergroup
+    o1s, o2s = [], []
+    cnt_n = np.diff(pt_ptr)
+    for n in np.unique(cnt_n):
+        if n < 2:
+            continue
+        base = pt_ptr[np.nonzero(cnt_n == n)[0]][:, None]
+        ii, jj = np.triu_indices(n, 1)
+        o1s.append((base + ii[None]).ravel())
+        o2s.append((base + jj[None]).ravel())
+    o1 = np.concatenate(o1s) if o1s else np.zeros(0, np.int64)
+    o2 = np.concatenate(o2s) if o2s else np.zeros(0, np.int64)
+    keep = obs_cam[o1] != obs_cam[o2]
+    o1, o2 = o1[keep], o2[keep]
+    key = (obs_sg[o1] * 8 + obs_la[o1]) * 8 + obs_la[o2]
+    ukey = np.unique(key)
+    bslot_sg = ukey // 64
+    bslot_a, bslot_b = (ukey // 8) % 8, ukey % 8
+    grp_bslot = np.searchsorted(bslot_sg, np.arange(NS + 1))
+    bc1 = sg_cams[bslot_sg, bslot_a]
+    bc2 = sg_cams[bslot_sg, bslot_b]
+    NB = C * (C + 1) // 2
+    blk = block_index(bc1, bc2, C)
+    if packed(C):
+        diag = np.arange(C)
+        own = np.unique(np.concatenate([block_index(diag, diag, C), blk]))
+        blist = own if block_list is None else np.unique(np.asarray(block_list, np.int64))
+        if block_list is not None and not np.all(np.isin(own, blist)):
+            raise ValueError("block_list misses a camera block with common points")
+        blk = np.searchsorted(blist, blk)
+        NB = len(blist)
+    else:
+        blist = np.arange(NB)
+    blk_bslots = np.lexsort((bslot_sg, blk))
+    bslot_row = np.empty(len(blk_bslots), np.int64)
+    bslot_row[blk_bslots] = np.arange(len(blk_bslots))
+    blk_bslot_ptr = np.zeros(NB + 1, np.int64)
+    np.cumsum(np.bincount(blk, minlength=NB), out=blk_bslot_ptr[1:])
+    c1, c2 = np.triu_indices(C)
+    c1, c2 = c1[blist], c2[blist]
+    i32 = lambda a: np.asarray(a, np.int32)  # noqa: E731
+    one = np.zeros(1, np.int32)
+    return dict(
+        mode=1, perm=perm, order=order, obs_cam=i32(obs_cam), obs_pt=i32(obs_pt),
+        pt_ptr=i32(pt_ptr), grp_ptr=i32(grp_ptr), grp_cslot=i32(grp_cslot),
+        cslot_cam=i32(cslot_cam), cslot_obs_ptr=one, cslot_obs=one, grp_bslot=i32(grp_bslot),
+        bslot_blk=i32(blk), bslot_pair_ptr=one, bslot_pairs=one,
+        blocks=i32(np.stack([c1, c2], 1)), cam_cslot_ptr=i32(cam_cslot_ptr),
+        cslot_row=i32(cslot_row), blk_bslot_ptr=i32(blk_bslot_ptr), bslot_row=i32(bslot_row),
+        sg_ptr=i32(sg_ptr), sg_cams=i32(sg_cams), obs_la=i32(obs_la), chk_cobs=i32(chk_cobs),
+        chk_cptr=i32(chk_cptr), bslot_ab=i32(bslot_a | (bslot_b << 8)),
+        n_obs=O, n_grps=G, n_sgrps=NS, chunks_per_wg=S)
+
+
 def tiled_solve_flops(n_cams, blocks, tb=64):
     """Flops of the tiled Cholesky (csrc/ba.hip k_tl_*) for a packed block list
     [n_blocks, 2]: the 64x64 tiles it factors, solves and updates, with the
@@ -227,6 +416,7 @@ def tiled_solve_flops(n_cams, blocks, tb=64):
     return flops
 
 
+_MFMA_TABLES = ("sg_ptr", "sg_cams", "obs_la", "chk_cobs", "chk_cptr", "bslot_ab")
 _INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
                  "cslot_obs_ptr", "cslot_obs", "grp_bslot", "bslot_blk", "bslot_pair_ptr",
                  "bslot_pairs", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
@@ -237,14 +427,32 @@ class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
-                 block_list=None):
+                 block_list=None, lin_mode="auto", chunks_per_wg=None):
+        """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
+        contraction on the f64 matrix cores; points renumbered internally),
+        "slot" (k_linearize, any observation structure) or "auto" (mfma when
+        every point is seen by <= MF_CAMS cameras)."""
         dev = require_gpu()
         cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
         C, P = len(cams), len(pts)
         cam_idx, pt_idx, qs = _check_indices(C, P, cam_idx, pt_idx, qs)
-        pl = plan(C, P, cam_idx, pt_idx, block_list)
+        pl = None
+        if lin_mode in ("auto", "mfma"):
+            pl = plan_mfma(C, P, cam_idx, pt_idx, block_list, chunks_per_wg)
+            if pl is None and lin_mode == "mfma":
+                raise ValueError(f"lin_mode 'mfma': a point is seen by more than {MF_CAMS} cameras")
+        elif lin_mode != "slot":
+            raise ValueError(f"lin_mode must be 'auto', 'mfma' or 'slot', not {lin_mode!r}")
+        if pl is None:
+            pl = plan(C, P, cam_idx, pt_idx, block_list)
+            pl["mode"], pl["perm"] = 0, None
+            pl["n_grps"], pl["n_sgrps"] = len(pl["grp_ptr"]) - 1, 0
         self.plan = pl
+        self.lin_mode = "mfma" if pl["mode"] == 1 else "slot"
+        self.perm = pl["perm"]  # device point k = caller's point perm[k] (None: identity)
+        if self.perm is not None:
+            pts = pts[self.perm]
         self.C, self.P, self.O = C, P, pl["n_obs"]
         self.stream = stream
         T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -253,7 +461,7 @@ class BAProblem:
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
         t["camrec0"], t["camrec1"] = z(C * 32), z(C * 32)
-        for k in _INDEX_TABLES:
+        for k in _INDEX_TABLES + (_MFMA_TABLES if pl["mode"] == 1 else ()):
             arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
             t[k] = T(arr.astype(np.int32))
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
@@ -266,7 +474,7 @@ class BAProblem:
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
         t["delta_c"] = z(C9)
-        G = len(pl["grp_ptr"]) - 1
+        G = pl["n_grps"]
         t["red_part"] = z(_lib.lib.slam_ba_red_slots(G))
         t["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
         t["small"] = z(4)
@@ -275,11 +483,13 @@ class BAProblem:
         s.n_cams, s.n_pts, s.n_obs, s.n_grps = C, P, self.O, G
         s.n_blocks = len(pl["blocks"])
         s.n_cslots, s.n_bslots = n_cs, n_bs
+        s.lin_mode, s.n_sgrps = pl["mode"], pl["n_sgrps"]
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
         for k in _INDEX_TABLES + ("obs_q", "ptdata", "cpart", "bpart", "sys", "chol", "delta_c",
-                                  "red_part", "small", "state", "ticket"):
+                                  "red_part", "small", "state", "ticket") + \
+                (_MFMA_TABLES if pl["mode"] == 1 else ()):
             setattr(s, k, t[k].data_ptr())
         self._s = s
         self.reset(lam0)
@@ -355,8 +565,15 @@ class BAProblem:
         return {k: float(s[v]) for k, v in ST.items()}
 
     def params(self):
+        """(cams [C,9], pts [P,3]) at the live parameters, points in the caller's order."""
         cur = int(self.t["state"][ST["CUR"]].item() != 0)
-        return (self.t[f"cams{cur}"].cpu().numpy().copy(), self.t[f"pts{cur}"].cpu().numpy().copy())
+        cams = self.t[f"cams{cur}"].cpu().numpy().copy()
+        pts = self.t[f"pts{cur}"].cpu().numpy()
+        if self.perm is not None:
+            out = np.empty_like(pts)
+            out[self.perm] = pts
+            pts = out
+        return cams, pts.copy()
 
     def cost(self) -> float:
         return self.state()["COST"]

@@ -442,3 +442,128 @@ def test_gpu_c5_global_ba_first_iteration_matches_oracle():
     gc, gp = prob.params()
     assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9)
     assert np.allclose(gp, op, rtol=1e-6, atol=1e-9)
+
+
+# ----------------------------------------------------------------------------- camera-union plan
+def _emulate_union_linearisation(pl, C, cams, pts_new, qs_sorted, lam):
+    """numpy restatement of csrc/ba.hip k_lin_mfma + k_assemble over the
+    plan_mfma tables -> dense undamped reduced system S [9C, 9C], b [9C]."""
+    ci = pl["obs_cam"].astype(np.int64)
+    pi = pl["obs_pt"].astype(np.int64)
+    r, J = oba.residual_and_jacobian(cams, pts_new, ci, pi, qs_sorted)
+    Jc, Jp = J[:, :, :9], J[:, :, 9:]
+    P = len(pts_new)
+    V = np.zeros((P, 3, 3))
+    np.add.at(V, pi, np.einsum("oai,oaj->oij", Jp, Jp))
+    g = np.zeros((P, 3))
+    np.add.at(g, pi, -np.einsum("oai,oa->oi", Jp, r))
+    D = np.clip(np.diagonal(V, axis1=1, axis2=2), oba.DIAG_MIN, oba.DIAG_MAX)
+    Vi = np.linalg.inv(V + lam * D[:, :, None] * np.eye(3)[None])
+    e = np.einsum("pij,pj->pi", Vi, g)
+    u = np.einsum("oai,oi->oa", Jp, e[pi])
+    cpart = np.zeros((len(pl["cslot_cam"]), 112))
+    bpart = np.zeros((len(pl["bslot_blk"]), 81))
+    for sg in range(len(pl["sg_ptr"]) - 1):
+        cams_sg = pl["sg_cams"][sg][pl["sg_cams"][sg] >= 0]
+        m = len(cams_sg)
+        T = np.zeros((9 * m, 9 * m))
+        Ua = np.zeros((m, 9, 9))
+        vec = np.zeros((m, 28))
+        for ch in range(pl["sg_ptr"][sg], pl["sg_ptr"][sg + 1]):
+            p0, p1 = pl["grp_ptr"][ch], pl["grp_ptr"][ch + 1]
+            o0, o1 = pl["pt_ptr"][p0], pl["pt_ptr"][p1]
+            assert o1 - o0 <= 128 and p1 - p0 <= 16
+            for q in range(p0, p1):
+                Wp = np.zeros((9 * m, 3))
+                for o in range(pl["pt_ptr"][q], pl["pt_ptr"][q + 1]):
+                    a = pl["obs_la"][o]
+                    assert cams_sg[a] == ci[o]
+                    Wp[9 * a:9 * a + 9] += Jc[o].T @ Jp[o]
+                T += (Wp @ Vi[q]) @ Wp.T
+            cp = pl["chk_cptr"][ch]
+            for a in range(m):
+                for k in pl["chk_cobs"][o0 + cp[a]:o0 + cp[a + 1]]:
+                    o = o0 + k
+                    assert pl["obs_la"][o] == a
+                    Ua[a] += Jc[o].T @ Jc[o]
+                    vec[a, :9] += Jc[o].T @ r[o]
+                    vec[a, 9:18] += Jc[o].T @ u[o]
+                    vec[a, 18:27] += np.einsum("ai,ai->i", Jc[o], Jc[o])
+                    vec[a, 27] += r[o] @ r[o]
+        for a in range(m):
+            row = pl["cslot_row"][pl["grp_cslot"][sg] + a]
+            cpart[row, :81] = (Ua[a] - T[9 * a:9 * a + 9, 9 * a:9 * a + 9]).ravel()
+            cpart[row, 81:109] = vec[a]
+        for s in range(pl["grp_bslot"][sg], pl["grp_bslot"][sg + 1]):
+            a, b = pl["bslot_ab"][s] & 255, pl["bslot_ab"][s] >> 8
+            bpart[pl["bslot_row"][s]] = T[9 * a:9 * a + 9, 9 * b:9 * b + 9].ravel()
+    S = np.zeros((9 * C, 9 * C))
+    bvec = np.zeros(9 * C)
+    for k, (c1, c2) in enumerate(pl["blocks"]):
+        rows_b = bpart[pl["blk_bslot_ptr"][k]:pl["blk_bslot_ptr"][k + 1]].sum(0).reshape(9, 9)
+        if c1 == c2:
+            cp = cpart[pl["cam_cslot_ptr"][c1]:pl["cam_cslot_ptr"][c1 + 1]].sum(0)
+            S[9 * c1:9 * c1 + 9, 9 * c1:9 * c1 + 9] = cp[:81].reshape(9, 9)
+            bvec[9 * c1:9 * c1 + 9] = -cp[81:90] - cp[90:99]
+        else:
+            S[9 * c1:9 * c1 + 9, 9 * c2:9 * c2 + 9] = -rows_b
+            S[9 * c2:9 * c2 + 9, 9 * c1:9 * c1 + 9] = -rows_b.T
+    return S, bvec
+
+
+def _dense_reduced_system(cams, pts, ci, pi, qs, lam):
+    r, J = oba.residual_and_jacobian(cams, pts, ci, pi, qs)
+    C = len(cams)
+    Jc, Jp = J[:, :, :9], J[:, :, 9:]
+    Jd = np.zeros((2 * len(ci), 9 * C + 3 * len(pts)))
+    for o in range(len(ci)):
+        Jd[2 * o:2 * o + 2, 9 * ci[o]:9 * ci[o] + 9] = Jc[o]
+        Jd[2 * o:2 * o + 2, 9 * C + 3 * pi[o]:9 * C + 3 * pi[o] + 3] = Jp[o]
+    H = Jd.T @ Jd
+    gr = -Jd.T @ r.ravel()
+    n = 9 * C
+    A, Bm, Dm = H[:n, :n], H[:n, n:], H[n:, n:]
+    Dd = np.clip(np.diag(Dm), oba.DIAG_MIN, oba.DIAG_MAX)
+    Dinv = np.linalg.inv(Dm + lam * np.diag(Dd))
+    return A - Bm @ Dinv @ Bm.T, gr[:n] - Bm @ Dinv @ gr[n:]
+
+
+@pytest.mark.parametrize("case", ["local", "dup", "packed", "loop"])
+def test_union_plan_assembles_the_reduced_system(case):
+    """ba.plan_mfma's chunks / supergroups / slot rows, run through a numpy
+    restatement of k_lin_mfma + k_assemble, give the Schur-reduced camera
+    system of the dense normal equations (points renumbered by camera span)."""
+    from slam355 import ba
+    from slam355.synthetic import ba_problem_loop
+
+    if case == "loop":
+        cams, pts, ci, pi, qs = ba_problem_loop(np.random.default_rng(3), 16, 120, 4)
+    else:
+        C = 16 if case == "packed" else 7
+        cams, pts, ci, pi, qs = make_problem(3, C, 90, 4)
+    if case == "dup":
+        k = np.random.default_rng(1).choice(len(ci), 6, replace=False)
+        ci, pi, qs = np.append(ci, ci[k]), np.append(pi, pi[k]), np.vstack([qs, qs[k] + 0.3])
+    C = len(cams)
+    pts = pts + np.random.default_rng(2).normal(0, 0.05, pts.shape)
+    pl = ba.plan_mfma(C, len(pts), ci, pi, chunks_per_wg=2)
+    assert pl is not None
+    perm = pl["perm"]
+    assert np.array_equal(np.sort(perm), np.arange(len(pts)))
+    assert all((pl["sg_cams"][s] >= 0).sum() <= ba.MF_CAMS for s in range(pl["n_sgrps"]))
+    S, b = _emulate_union_linearisation(pl, C, cams, pts[perm], qs[pl["order"]], 1e-3)
+    Sr, br = _dense_reduced_system(cams, pts, ci, pi, qs, 1e-3)
+    scale = np.abs(Sr).max()
+    assert np.abs(S - Sr).max() <= 1e-9 * scale
+    assert np.abs(b - br).max() <= 1e-9 * max(1.0, np.abs(br).max())
+
+
+def test_union_plan_falls_back_for_wide_tracks():
+    """A point seen by more than MF_CAMS cameras: no camera-union plan (the
+    slot linearisation takes such problems)."""
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(4, 10, 50, 8)
+    assert ba.plan_mfma(10, 50, ci, pi) is None
+    cams, pts, ci, pi, qs = make_problem(4, 10, 50, 7)
+    assert ba.plan_mfma(10, 50, ci, pi) is not None
