@@ -513,7 +513,8 @@ def run_ba_batch(args, world, rank):
     for _ in range(args.ba_batch):
         cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
         c0, p0 = perturb(rng, cams, pts)
-        probs.append(BAProblem(c0, p0, ci, pi, qs))
+        probs.append(BAProblem(c0, p0, ci, pi, qs, lin_mode=args.lin_mode,
+                               chunks_per_wg=args.chunks_per_wg))
     bat = BABatch(probs)
 
     def step(marks):
@@ -715,6 +716,10 @@ def main():
     ap.add_argument("--keep-poses", action="store_true")
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
+    ap.add_argument("--lin-mode", default="auto", choices=["auto", "mfma", "slot"],
+                    help="BA linearisation: camera-union MFMA kernel or the slot kernel")
+    ap.add_argument("--chunks-per-wg", type=int, default=None,
+                    help="camera-union linearisation: chunks per workgroup (default: auto)")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")

@@ -325,8 +325,10 @@ typedef struct slam_ba_problem {
    * indexed by supergroup. */
   const int32_t* sg_ptr;        /* [n_sgrps+1] chunk range of each supergroup    */
   const int32_t* sg_cams;       /* [n_sgrps][8] its cameras (<= 7, sorted, -1 padded) */
-  const int32_t* obs_la;        /* [O] position of the obs's camera in sg_cams  */
-  const int32_t* chk_cobs;      /* [O] chunk-local obs indices sorted by (la, obs) */
+  const int32_t* obs_meta;      /* [O] lpt | la << 8 | cobs << 16: chunk-local point,
+                                   position of the obs's camera in sg_cams, and the
+                                   chunk-local obs list sorted by (la, obs)      */
+  const int32_t* chk_optr;      /* [n_grps+1] first observation of each chunk    */
   const int32_t* chk_cptr;      /* [n_grps][8] start of each camera's run in chk_cobs */
   const int32_t* bslot_ab;      /* [n_bslots] camera pair a | b << 8 (a < b) of a block slot */
 } slam_ba_problem;

@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 // per camera a one cpart row (U_a - T_aa, ...), per co-observed camera pair
 // a < b one bpart row (T_ab) -- the rows k_assemble sums.  Per point: V, g,
 // V*, V*^-1, e as k_linearize (ptdata).
-constexpr int kMObs = 128, kMPts = 16, kMCams = 7, kMRows = 64;
+constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
 struct MLds {
   double jc[kMObs][18];          // Jc rows (2 x 9)
@@ -541,6 +541,9 @@ struct MLds {
   double e[kMPts][3];
   double yt[kMPts][3][kMRows];   // Y_p, [point][k][row]: the MFMA A operand
   double wt[kMPts][3][kMRows];   // W_p, [point][k][row]: the MFMA B operand
+  double cam[kMCams][kCamRec];   // the supergroup's camera records (live parameters)
+  double X[kMPts][3];            // the chunk's points
+  int optr[kMPts + 1];           // chunk-local observation range of each point
   int lpt[kMObs];                // chunk-local point of each observation
   int la[kMObs];                 // supergroup-local camera of each observation
   int cobs[kMObs];               // chunk-local observations sorted by camera
@@ -563,8 +566,17 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   const int nt = (9 * m + 15) >> 4;  // tile rows of T
   const int cur = cur_of(p.state);
   const double lam = p.state[SLAM_BA_ST_LAMBDA];
-  // rows >= 9m of Y/W stay zero for the whole supergroup
-  for (int i = t; i < 2 * kMPts * 3 * kMRows; i += kMWG) (&L.yt[0][0][0])[i] = 0.0;
+  // the supergroup's camera records -> LDS (one load per lane)
+  if (t < kMCams * kCamRec) {
+    const int a = t / kCamRec, k = t - kCamRec * (t / kCamRec);
+    const int c = a < m ? p.sg_cams[8 * sg + a] : -1;
+    if (c >= 0) L.cam[a][k] = p.camrec[cur][(size_t)kCamRec * c + k];
+  }
+  // rows [9m, 16 nt) of Y/W are never written: zero them once
+  for (int i = t; i < 2 * kMPts * 3 * 16; i += kMWG) {
+    const int row = 9 * m + (i & 15);
+    if (row < 16 * nt) (&L.yt[0][0][0])[(i >> 4) * kMRows + row] = 0.0;
+  }
   // this wave's upper tiles (I <= J), dealt round-robin: <= 3 per wave
   int tI[3], tJ[3];
   int ntl = 0;
@@ -592,17 +604,38 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
 
   for (int ch = ch0; ch < ch1; ++ch) {
+    // chunk extents: four independent loads
     const int p0 = p.grp_ptr[ch], p1 = p.grp_ptr[ch + 1];
-    const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
+    const int o0 = p.chk_optr[ch], o1 = p.chk_optr[ch + 1];
     const int nobs = o1 - o0, npts = p1 - p0;
+    // this chunk's inputs, all issued before any is used
+    double q0 = 0.0, q1 = 0.0;
+    int meta = 0;
+    if (t < nobs) {
+      q0 = p.obs_q[2 * (o0 + t)];
+      q1 = p.obs_q[2 * (o0 + t) + 1];
+      meta = p.obs_meta[o0 + t];
+    }
+    double xv = 0.0;
+    if (t < 3 * npts) xv = p.pts[cur][3 * p0 + t];
+    int pp = 0;
+    if (t >= 128 && t - 128 <= npts) pp = p.pt_ptr[p0 + t - 128] - o0;
+    const int cp = t < 8 ? p.chk_cptr[8 * ch + t] : 0;
     __syncthreads();  // the previous chunk's readers are done with L
+    if (t < nobs) {
+      L.lpt[t] = meta & 255;
+      L.la[t] = (meta >> 8) & 255;
+      L.cobs[t] = meta >> 16;
+    }
+    if (t < 3 * npts) (&L.X[0][0])[t] = xv;
+    if (t >= 128 && t - 128 <= npts) L.optr[t - 128] = pp;
+    if (t < 8) L.cptr[t] = cp;
+    __syncthreads();
     // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350)
     if (t < nobs) {
-      const int o = o0 + t;
-      const int pt = p.obs_pt[o];
+      const double q[2] = {q0, q1};
       double r[2], J[2][12];
-      reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
-                          p.obs_q + 2 * o, r, J);
+      reproject_pre<true>(L.cam[L.la[t]], L.X[L.lpt[t]], q, r, J);
       clamp_rows<true>(r, J);
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
@@ -612,17 +645,13 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
         for (int c = 0; c < 3; ++c) L.jp[t][3 * a + c] = J[a][9 + c];
         L.ru[t][a] = r[a];
       }
-      L.lpt[t] = pt - p0;
-      L.la[t] = p.obs_la[o];
-      L.cobs[t] = p.chk_cobs[o];
     }
-    if (t < 8) L.cptr[t] = p.chk_cptr[8 * ch + t];
     __syncthreads();
     // (B) per point: V, g, V* = V + lam diag(V), V*^-1 (cofactors), e = V*^-1 g
     if (t < npts) {
       const int pt = p0 + t;
       double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
-      for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
+      for (int k = L.optr[t]; k < L.optr[t + 1]; ++k) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
           const double j0 = L.jp[k][3 * a], j1 = L.jp[k][3 * a + 1], j2 = L.jp[k][3 * a + 2];
@@ -665,15 +694,14 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       const double* e = L.e[L.lpt[t]];
       L.ru[t][2] = L.jp[t][0] * e[0] + L.jp[t][1] * e[1] + L.jp[t][2] * e[2];
       L.ru[t][3] = L.jp[t][3] * e[0] + L.jp[t][4] * e[1] + L.jp[t][5] * e[2];
-    } else if (t >= kMObs && t - kMObs < npts * m) {
-      const int q = t - kMObs, lp = q / m, a = q - m * (q / m);
+    } else if (t >= 128 && t - 128 < npts * m) {
+      const int q = t - 128, lp = q / m, a = q - m * (q / m);
       double W[9][3];
 #pragma unroll
       for (int i = 0; i < 9; ++i)
 #pragma unroll
         for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
-      const int kb = p.pt_ptr[p0 + lp] - o0, ke = p.pt_ptr[p0 + lp + 1] - o0;
-      for (int k = kb; k < ke; ++k) {
+      for (int k = L.optr[lp]; k < L.optr[lp + 1]; ++k) {
         if (L.la[k] != a) continue;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
@@ -1916,8 +1944,8 @@ int check_problem(const slam_ba_problem* p) {
                "slam_ba: null buffer");
   SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
   SLAM_REQUIRE(p->lin_mode == 0 || p->lin_mode == 1, "slam_ba: lin_mode must be 0 or 1");
-  SLAM_REQUIRE(p->lin_mode == 0 || (p->n_sgrps >= 1 && p->sg_ptr && p->sg_cams && p->obs_la &&
-                                     p->chk_cobs && p->chk_cptr && p->bslot_ab),
+  SLAM_REQUIRE(p->lin_mode == 0 || (p->n_sgrps >= 1 && p->sg_ptr && p->sg_cams && p->obs_meta &&
+                                     p->chk_optr && p->chk_cptr && p->bslot_ab),
                "slam_ba: lin_mode 1 needs n_sgrps >= 1 and the supergroup tables");
   SLAM_REQUIRE(sys_packed(p->n_cams) ? (p->n_blocks >= p->n_cams &&
                                         p->n_blocks <= p->n_cams * (p->n_cams + 1) / 2)

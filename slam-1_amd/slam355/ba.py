@@ -207,7 +207,7 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, block_list=None):
 # together see at most MF_CAMS cameras, so a supergroup's share of the
 # reduced camera system is one dense (9m x 9m, m <= 7) matrix: the Schur term
 # sum_p Y_p W_p^T on the f64 matrix cores, U on the vector ALUs.
-MF_CHUNK_OBS = 128  # kMObs: observations per chunk (also k_back_trial's group cap)
+MF_CHUNK_OBS = 120  # kMObs: observations per chunk (<= k_back_trial's group cap 128)
 MF_CHUNK_PTS = 16   # kMPts: points per chunk
 MF_CAMS = 7         # kMCams: cameras per supergroup (9m <= 63 rows: 4 MFMA tile rows)
 
@@ -387,7 +387,9 @@ def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=Non
         blocks=i32(np.stack([c1, c2], 1)), cam_cslot_ptr=i32(cam_cslot_ptr),
         cslot_row=i32(cslot_row), blk_bslot_ptr=i32(blk_bslot_ptr), bslot_row=i32(bslot_row),
         sg_ptr=i32(sg_ptr), sg_cams=i32(sg_cams), obs_la=i32(obs_la), chk_cobs=i32(chk_cobs),
-        chk_cptr=i32(chk_cptr), bslot_ab=i32(bslot_a | (bslot_b << 8)),
+        obs_meta=i32((obs_pt - grp_ptr[obs_chunk]) | (obs_la << 8) | (chk_cobs << 16))
+        if O else np.zeros(0, np.int32),
+        chk_optr=i32(pt_ptr[grp_ptr]), chk_cptr=i32(chk_cptr), bslot_ab=i32(bslot_a | (bslot_b << 8)),
         n_obs=O, n_grps=G, n_sgrps=NS, chunks_per_wg=S)
 
 
@@ -416,7 +418,7 @@ def tiled_solve_flops(n_cams, blocks, tb=64):
     return flops
 
 
-_MFMA_TABLES = ("sg_ptr", "sg_cams", "obs_la", "chk_cobs", "chk_cptr", "bslot_ab")
+_MFMA_TABLES = ("sg_ptr", "sg_cams", "obs_meta", "chk_optr", "chk_cptr", "bslot_ab")
 _INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
                  "cslot_obs_ptr", "cslot_obs", "grp_bslot", "bslot_blk", "bslot_pair_ptr",
                  "bslot_pairs", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
