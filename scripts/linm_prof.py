@@ -1,0 +1,42 @@
+"""Phase split of k_lin_mfma per workgroup (library built by build_linm_prof.sh):
+staging loads, projections (A), points (B), W/Y (C), MFMA + U (D), write-out (E)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "slam-1_amd")]
+os.environ["SLAM355_LIB"] = os.path.join(ROOT, "slam-1_amd", "prof", "libslam355_linm.so")
+
+import torch  # noqa: E402
+from slam355 import _lib  # noqa: E402
+from slam355.ba import BABatch, BAProblem  # noqa: E402
+from slam355.synthetic import ba_problem, perturb  # noqa: E402
+
+nb = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+rng = np.random.default_rng(0)
+probs = []
+for _ in range(nb):
+    cams, pts, ci, pi, qs = ba_problem(rng, 10, 5000, 6)
+    c0, p0 = perturb(rng, cams, pts)
+    probs.append(BAProblem(c0, p0, ci, pi, qs))
+bat = BABatch(probs)
+fn = _lib.lib.slam_linm_stamps
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+names = ["loads", "A proj", "B points", "C W/Y", "D mfma+U", "E write"]
+for it in range(5):
+    bat.iterate(1)
+    torch.cuda.synchronize()
+    n = probs[0].plan["n_sgrps"]
+    buf = (ctypes.c_ulonglong * (4096 * 8))()
+    fn(buf, 4096)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
+    rows = np.concatenate([a[1024 * y:1024 * y + n] for y in range(nb)])
+    d = np.diff(rows[:, :7], axis=1)
+    span = rows[:, 6].max() - rows[:, 0].min()
+    st = rows[:, 0] - rows[:, 0].min()
+    print(f"iter {it}: WGs {len(rows)} span {span} clk; start spread {st.max()} clk; per-WG total "
+          f"median {np.median(rows[:, 6] - rows[:, 0]):.0f}")
+    print("   " + "  ".join(f"{nm} {np.median(d[:, k]):.0f}/{d[:, k].max()}" for k, nm in enumerate(names)))

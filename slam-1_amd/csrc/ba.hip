@@ -519,18 +519,21 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 // lin_mode 1 (planner ba.plan_mfma): a workgroup owns a supergroup -- a run of
 // chunks (<= kMObs observations, <= kMPts whole points each) whose points
 // together see m <= kMCams cameras -- and forms its whole share of the reduced
-// camera system as ONE dense (9m x 9m) matrix:
-//   Schur part  T = sum_p Y_p W_p^T  (W_p: the point's 9m x 3 camera-block
-//               column, W~_{p,a} = sum of Jc_o^T Jp_o over its observations by
-//               camera a, zero for cameras that do not see p; Y_p = W_p V*_p^-1)
-//               on the f64 matrix cores: per point, one v_mfma_f64_16x16x4_f64
-//               per upper 16x16 tile of T (K = the point's 3 coordinates + 0);
-//   U part      U_a = sum_o Jc_o^T Jc_o, Jc^T r, Jc^T u, diag U, |r|^2 per camera
-//               on the vector ALUs (waves 2 and 3, beside their MFMAs),
+// camera system as ONE dense (9m x 9m) matrix, on the f64 matrix cores
+// (v_mfma_f64_16x16x4_f64):
+//   Schur part  T = sum_p Y_p W_p^T: W_p is the point's 9m x 3 column of camera
+//               blocks (W~_{p,a} = sum of Jc_o^T Jp_o over its observations by
+//               camera a; zero for cameras that do not see p), Y_p = W_p V*_p^-1;
+//               one MFMA per point and upper 16x16 tile of T (K = the point's
+//               3 coordinates, padded to 4);
+//   camera part Z_a = sum over the observation rows of camera a of z^T z with
+//               z = [Jc row (9) | r | u | 0]: one 16x16 tile per camera holding
+//               U_a = Jc^T Jc, Jc^T r, Jc^T u, diag U and |r|^2 (K = 2 rows of
+//               2 observations per MFMA);
 // accumulated in registers across the supergroup's chunks and written once:
-// per camera a one cpart row (U_a - T_aa, ...), per co-observed camera pair
-// a < b one bpart row (T_ab) -- the rows k_assemble sums.  Per point: V, g,
-// V*, V*^-1, e as k_linearize (ptdata).
+// per camera a one cpart row (U_a - T_aa, Jc^T r, Jc^T u, diag U, |r|^2), per
+// co-observed camera pair a < b one bpart row (T_ab) -- the rows k_assemble
+// sums.  Per point: V, g, V*, V*^-1, e as k_linearize (ptdata).
 constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
 struct MLds {
@@ -543,6 +546,7 @@ struct MLds {
   double wt[kMPts][3][kMRows];   // W_p, [point][k][row]: the MFMA B operand
   double cam[kMCams][kCamRec];   // the supergroup's camera records (live parameters)
   double X[kMPts][3];            // the chunk's points
+  double zero;                   // operand of padded MFMA lanes
   int optr[kMPts + 1];           // chunk-local observation range of each point
   int lpt[kMObs];                // chunk-local point of each observation
   int la[kMObs];                 // supergroup-local camera of each observation
@@ -551,12 +555,24 @@ struct MLds {
 };
 static_assert(sizeof(MLds) <= 80 * 1024, "k_lin_mfma: two workgroups per CU");
 static_assert(9 * kMCams <= kMRows, "k_lin_mfma: 9m rows in 4 tile rows");
-static_assert(2 * kMPts * 3 * kMRows >= kMRows * kMRows, "T staging aliases yt/wt");
+static_assert(2 * kMPts * 3 * kMRows >= kMRows * kMRows + kMCams * 256, "staging aliases yt/wt");
+
+#ifdef SLAM_LINM_PROFILE
+__device__ unsigned long long g_linm_stamp[4096][8];
+#define LINM_T(i)                                                                   \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x + 1024 * blockIdx.y < 4096)                  \
+      g_linm_stamp[blockIdx.x + 1024 * blockIdx.y][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define LINM_T(i) (void)0
+#endif
 
 __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   BA_PROB(bat);
   const int sg = blockIdx.x;
   if (sg >= p.n_sgrps) return;  // batch: grid.x covers the largest problem
+  LINM_T(0);
   lm_wave_priority();
   __shared__ MLds L;
   const int t = threadIdx.x, lane = t & 63;
@@ -572,12 +588,9 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     const int c = a < m ? p.sg_cams[8 * sg + a] : -1;
     if (c >= 0) L.cam[a][k] = p.camrec[cur][(size_t)kCamRec * c + k];
   }
-  // rows [9m, 16 nt) of Y/W are never written: zero them once
-  for (int i = t; i < 2 * kMPts * 3 * 16; i += kMWG) {
-    const int row = 9 * m + (i & 15);
-    if (row < 16 * nt) (&L.yt[0][0][0])[(i >> 4) * kMRows + row] = 0.0;
-  }
-  // this wave's upper tiles (I <= J), dealt round-robin: <= 3 per wave
+  if (t == 0) L.zero = 0.0;
+  // this wave's upper tiles of T (I <= J), dealt round-robin: <= 3 per wave;
+  // its cameras a = wid, wid + 4 (<= 2)
   int tI[3], tJ[3];
   int ntl = 0;
   {
@@ -590,17 +603,12 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
           ++ntl;
         }
   }
-  d4 acc[3];
+  const int nza = (m > wid) + (m > wid + 4);
+  d4 acc[3], zacc[2];
 #pragma unroll
   for (int s = 0; s < 3; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
-  // U item of this lane: waves 2, 3 (lanes 0..31) -> (camera a, row i)
-  const int uq = (wid - 2) * 32 + lane;
-  const bool uown = wid >= 2 && lane < 32 && uq < 9 * m;
-  const int ua = uown ? uq / 9 : 0, ui = uown ? uq - 9 * (uq / 9) : 0;
-  double uacc[9];
 #pragma unroll
-  for (int j = 0; j < 9; ++j) uacc[j] = 0.0;
-  double ujr = 0.0, uju = 0.0, udg = 0.0, ucost = 0.0;
+  for (int s = 0; s < 2; ++s) zacc[s] = d4{0.0, 0.0, 0.0, 0.0};
   const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
 
   for (int ch = ch0; ch < ch1; ++ch) {
@@ -630,7 +638,15 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     if (t < 3 * npts) (&L.X[0][0])[t] = xv;
     if (t >= 128 && t - 128 <= npts) L.optr[t - 128] = pp;
     if (t < 8) L.cptr[t] = cp;
+    // Y/W operand planes of the chunk's points start at zero (rows of cameras
+    // a point is not seen by, rows >= 9m)
+    for (int i = t; i < npts * 3 * 16 * nt; i += kMWG) {
+      const int row = i % (16 * nt), pk = i / (16 * nt);
+      (&L.yt[0][0][0])[pk * kMRows + row] = 0.0;
+      (&L.wt[0][0][0])[pk * kMRows + row] = 0.0;
+    }
     __syncthreads();
+    LINM_T(1);
     // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350)
     if (t < nobs) {
       const double q[2] = {q0, q1};
@@ -647,6 +663,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       }
     }
     __syncthreads();
+    LINM_T(2);
     // (B) per point: V, g, V* = V + lam diag(V), V*^-1 (cofactors), e = V*^-1 g
     if (t < npts) {
       const int pt = p0 + t;
@@ -688,41 +705,54 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       }
     }
     __syncthreads();
-    // (C) lanes 0..127: u_o = Jp_o e_p; lanes 128..: (point, camera) items ->
-    //     W~_{p,a} (9x3) and Y = W~ V*^-1 into the MFMA operand planes
-    if (t < nobs) {
-      const double* e = L.e[L.lpt[t]];
-      L.ru[t][2] = L.jp[t][0] * e[0] + L.jp[t][1] * e[1] + L.jp[t][2] * e[2];
-      L.ru[t][3] = L.jp[t][3] * e[0] + L.jp[t][4] * e[1] + L.jp[t][5] * e[2];
-    } else if (t >= 128 && t - 128 < npts * m) {
-      const int q = t - 128, lp = q / m, a = q - m * (q / m);
-      double W[9][3];
+    LINM_T(3);
+    // (C) per observation, rows i of W~ split over two lanes (lane t: rows
+    //     0..4, lane t + 128: rows 5..8): W~_{p,a} rows summed over the run of
+    //     observations of the same (point, camera) (adjacent: obs are sorted by
+    //     point, then camera), Y = W~ V*^-1, into the operand planes; u_o.
+    {
+      const int h = t >> 7, k0 = t & 127;
+      const bool lead = k0 < nobs && (k0 == 0 || L.lpt[k0 - 1] != L.lpt[k0] ||
+                                      L.la[k0 - 1] != L.la[k0]);
+      if (lead) {
+        const int lp = L.lpt[k0], a = L.la[k0];
+        const int ib = h ? 5 : 0, ie = h ? 9 : 5;
+        double W[5][3];
 #pragma unroll
-      for (int i = 0; i < 9; ++i)
+        for (int i = 0; i < 5; ++i)
 #pragma unroll
-        for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
-      for (int k = L.optr[lp]; k < L.optr[lp + 1]; ++k) {
-        if (L.la[k] != a) continue;
+          for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
+        for (int k = k0; k < nobs && L.lpt[k] == lp && L.la[k] == a; ++k) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i)
+          for (int i = 0; i < 5; ++i) {
+            if (ib + i >= ie) break;
 #pragma unroll
-          for (int c = 0; c < 3; ++c)
-            W[i][c] += L.jc[k][i] * L.jp[k][c] + L.jc[k][9 + i] * L.jp[k][3 + c];
-      }
-      const double* vi = L.vi[lp];
-      const double V[3][3] = {{vi[0], vi[1], vi[2]}, {vi[1], vi[3], vi[4]}, {vi[2], vi[4], vi[5]}};
-#pragma unroll
-      for (int i = 0; i < 9; ++i) {
-        const int row = 9 * a + i;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          L.wt[lp][c][row] = W[i][c];
-          L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
+            for (int c = 0; c < 3; ++c)
+              W[i][c] += L.jc[k][ib + i] * L.jp[k][c] + L.jc[k][9 + ib + i] * L.jp[k][3 + c];
+          }
         }
+        const double* vi = L.vi[lp];
+        const double V[3][3] = {{vi[0], vi[1], vi[2]}, {vi[1], vi[3], vi[4]}, {vi[2], vi[4], vi[5]}};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          if (ib + i >= ie) break;
+          const int row = 9 * a + ib + i;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            L.wt[lp][c][row] = W[i][c];
+            L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
+          }
+        }
+      }
+      if (h == 0 && k0 < nobs) {
+        const double* e = L.e[L.lpt[k0]];
+        L.ru[k0][2] = L.jp[k0][0] * e[0] + L.jp[k0][1] * e[1] + L.jp[k0][2] * e[2];
+        L.ru[k0][3] = L.jp[k0][3] * e[0] + L.jp[k0][4] * e[1] + L.jp[k0][5] * e[2];
       }
     }
     __syncthreads();
-    // (D) T += Y_p W_p^T on the matrix cores, one MFMA per point and tile:
+    LINM_T(4);
+    // (D) T += Y_p W_p^T, one MFMA per point and tile:
     //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0
     for (int lp = 0; lp < npts; ++lp) {
 #pragma unroll
@@ -734,25 +764,31 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
                                                      acc[s], 0, 0, 0);
       }
     }
-    //     U part: lane (a, i) over the chunk's observations by camera a
-    if (uown) {
-      for (int q = L.cptr[ua]; q < L.cptr[ua + 1]; ++q) {
-        const int k = L.cobs[q];
-        const double* jc = L.jc[k];
-        const double a0 = jc[ui], a1 = jc[9 + ui];
+    //     Z_a += z^T z over camera a's observation rows, 2 observations per MFMA:
+    //     lane (i = lane & 15, k = lane >> 4) supplies z[row k & 1 of obs k >> 1][i]
+    //     as both operands (A[i][k] and B[k][i] take the same value)
 #pragma unroll
-        for (int j = 0; j < 9; ++j) uacc[j] = __builtin_fma(a0, jc[j], __builtin_fma(a1, jc[9 + j], uacc[j]));
-        const double r0 = L.ru[k][0], r1 = L.ru[k][1];
-        ujr = __builtin_fma(a0, r0, __builtin_fma(a1, r1, ujr));
-        uju = __builtin_fma(a0, L.ru[k][2], __builtin_fma(a1, L.ru[k][3], uju));
-        udg = __builtin_fma(a0, a0, __builtin_fma(a1, a1, udg));
-        ucost = __builtin_fma(r0, r0, __builtin_fma(r1, r1, ucost));
+    for (int s = 0; s < 2; ++s) {
+      if (s >= nza) break;  // uniform per wave
+      const int a = wid + 4 * s;
+      const int qb = L.cptr[a], qe = L.cptr[a + 1];
+      for (int q = qb; q < qe; q += 2) {
+        const int qq = q + (mk >> 1);
+        const int k = L.cobs[qq < qe ? qq : qb];
+        const int row = mk & 1;
+        const double* src = mi < 9 ? &L.jc[k][9 * row + mi]
+                            : mi < 11 ? &L.ru[k][row + 2 * (mi - 9)] : &L.zero;
+        const double z = qq < qe ? *src : 0.0;
+        zacc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, zacc[s], 0, 0, 0);
       }
     }
   }
-  // (E) T -> LDS staging (aliases the operand planes), then the partial rows
+  // (E) T and the Z_a tiles -> LDS staging (aliases the operand planes), then
+  //     the partial rows
   __syncthreads();
+  LINM_T(5);
   double* T = &L.yt[0][0][0];
+  double* Z = T + kMRows * kMRows;  // [kMCams][16][16]
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     if (s >= ntl) break;
@@ -760,21 +796,33 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     for (int r = 0; r < 4; ++r)
       T[(16 * tI[s] + mk + 4 * r) * kMRows + 16 * tJ[s] + mi] = acc[s][r];
   }
-  __syncthreads();
-  if (uown) {
-    // T is symmetric; only upper tiles were formed
-    double* out = p.cpart + (size_t)p.cslot_row[cs0 + ua] * kCPart;
-    const int row = 9 * ua + ui;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int col = 9 * ua + j;
+  for (int s = 0; s < 2; ++s) {
+    if (s >= nza) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Z[(wid + 4 * s) * 256 + (mk + 4 * r) * 16 + mi] = zacc[s][r];
+  }
+  __syncthreads();
+  // camera rows: items (a, 112-wide row entry)
+  for (int q = t; q < m * 109; q += kMWG) {
+    const int a = q / 109, e = q - 109 * (q / 109);
+    const double* Za = Z + a * 256;
+    double v;
+    if (e < 81) {
+      const int i = e / 9, j = e - 9 * (e / 9);
+      const int row = 9 * a + i, col = 9 * a + j;  // T is symmetric; upper tiles were formed
       const double tv = (row >> 4) <= (col >> 4) ? T[row * kMRows + col] : T[col * kMRows + row];
-      out[9 * ui + j] = uacc[j] - tv;
+      v = Za[i * 16 + j] - tv;
+    } else if (e < 90) {
+      v = Za[(e - 81) * 16 + 9];   // Jc^T r
+    } else if (e < 99) {
+      v = Za[(e - 90) * 16 + 10];  // Jc^T u
+    } else if (e < 108) {
+      v = Za[(e - 99) * 17];       // diag U
+    } else {
+      v = Za[9 * 16 + 9];          // |r|^2
     }
-    out[81 + ui] = ujr;
-    out[90 + ui] = uju;
-    out[99 + ui] = udg;
-    if (ui == 0) out[108] = ucost;
+    p.cpart[(size_t)p.cslot_row[cs0 + a] * kCPart + e] = v;
   }
   const int bs0 = p.grp_bslot[sg], nb = p.grp_bslot[sg + 1] - bs0;
   for (int q = t; q < 81 * nb; q += kMWG) {
@@ -783,6 +831,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     const int i = e / 9, j = e - 9 * (e / 9);
     p.bpart[(size_t)p.bslot_row[bs0 + pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
   }
+  LINM_T(6);
 }
 
 // Column sums of the n-wide rows [rb, re) of part (row stride `stride`): the
@@ -2139,6 +2188,14 @@ extern "C" int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, 
   }
   return SLAM_OK;
 }
+
+#ifdef SLAM_LINM_PROFILE
+extern "C" int slam_linm_stamps(unsigned long long* out, int n) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_linm_stamp), (size_t)n * 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif
 
 #ifdef SLAM_TL_PROFILE
 extern "C" int slam_tl_stamps(unsigned long long* out8) {
