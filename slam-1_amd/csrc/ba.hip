@@ -552,6 +552,8 @@ struct MLds {
   int la[kMObs];                 // supergroup-local camera of each observation
   int cobs[kMObs];               // chunk-local observations sorted by camera
   int cptr[8];                   // their per-camera runs
+  int crow[kMCams];              // cpart row of each camera slot
+  int bab[kMCams * (kMCams - 1) / 2], brow[kMCams * (kMCams - 1) / 2];  // block slots
 };
 static_assert(sizeof(MLds) <= 80 * 1024, "k_lin_mfma: two workgroups per CU");
 static_assert(9 * kMCams <= kMRows, "k_lin_mfma: 9m rows in 4 tile rows");
@@ -589,6 +591,13 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     if (c >= 0) L.cam[a][k] = p.camrec[cur][(size_t)kCamRec * c + k];
   }
   if (t == 0) L.zero = 0.0;
+  // output rows of this supergroup (read at the end; loaded now, off the tail)
+  const int bs0 = p.grp_bslot[sg], nb = p.grp_bslot[sg + 1] - bs0;
+  if (t < m) L.crow[t] = p.cslot_row[cs0 + t];
+  if (t >= 64 && t - 64 < nb) {
+    L.bab[t - 64] = p.bslot_ab[bs0 + t - 64];
+    L.brow[t - 64] = p.bslot_row[bs0 + t - 64];
+  }
   // this wave's upper tiles of T (I <= J), dealt round-robin: <= 3 per wave;
   // its cameras a = wid, wid + 4 (<= 2)
   int tI[3], tJ[3];
@@ -604,6 +613,12 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
         }
   }
   const int nza = (m > wid) + (m > wid + 4);
+  int tRow[3], tCol[3];  // operand rows of this lane for each tile slot
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    tRow[s] = 16 * (s < ntl ? tI[s] : 0) + (lane & 15);
+    tCol[s] = 16 * (s < ntl ? tJ[s] : 0) + (lane & 15);
+  }
   d4 acc[3], zacc[2];
 #pragma unroll
   for (int s = 0; s < 3; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
@@ -753,33 +768,69 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     __syncthreads();
     LINM_T(4);
     // (D) T += Y_p W_p^T, one MFMA per point and tile:
-    //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0
-    for (int lp = 0; lp < npts; ++lp) {
+    //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0.
+    //     Every wave issues 3 tile MFMAs per point (a wave with 2 tiles feeds
+    //     its third accumulator zeros), so the accumulators stay in their own
+    //     AGPRs with no control flow around the MFMAs; operands of 4 points are
+    //     loaded before their MFMAs are issued (points past npts: zeros).
+    for (int lp0 = 0; lp0 < npts; lp0 += 4) {
+      double av[4][3], bv[4][3];
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        if (s >= ntl) break;  // uniform per wave
-        const double av = L.yt[lp][mkc][16 * tI[s] + mi];
-        const double bv = L.wt[lp][mkc][16 * tJ[s] + mi];
-        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(mk < 3 ? av : 0.0, mk < 3 ? bv : 0.0,
-                                                     acc[s], 0, 0, 0);
+      for (int u = 0; u < 4; ++u) {
+        const int lp = min(lp0 + u, kMPts - 1);
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          av[u][s] = L.yt[lp][mkc][tRow[s]];
+          bv[u][s] = L.wt[lp][mkc][tCol[s]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool on = mk < 3 && lp0 + u < npts;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool o = on && s < ntl;
+          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(o ? av[u][s] : 0.0, o ? bv[u][s] : 0.0,
+                                                       acc[s], 0, 0, 0);
+        }
       }
     }
     //     Z_a += z^T z over camera a's observation rows, 2 observations per MFMA:
     //     lane (i = lane & 15, k = lane >> 4) supplies z[row k & 1 of obs k >> 1][i]
-    //     as both operands (A[i][k] and B[k][i] take the same value)
+    //     as both operands (A[i][k] and B[k][i] take the same value).  The
+    //     wave's two cameras (a = wid, wid + 4) advance together, 4 MFMAs each
+    //     per step, operands loaded ahead; missing cameras / observations: zeros.
+    {
+      const int row = mk & 1;
+      int qb[2], qe[2];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      if (s >= nza) break;  // uniform per wave
-      const int a = wid + 4 * s;
-      const int qb = L.cptr[a], qe = L.cptr[a + 1];
-      for (int q = qb; q < qe; q += 2) {
-        const int qq = q + (mk >> 1);
-        const int k = L.cobs[qq < qe ? qq : qb];
-        const int row = mk & 1;
-        const double* src = mi < 9 ? &L.jc[k][9 * row + mi]
-                            : mi < 11 ? &L.ru[k][row + 2 * (mi - 9)] : &L.zero;
-        const double z = qq < qe ? *src : 0.0;
-        zacc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(z, z, zacc[s], 0, 0, 0);
+      for (int s = 0; s < 2; ++s) {
+        const int a = wid + 4 * s;
+        qb[s] = s < nza ? L.cptr[a] : 0;
+        qe[s] = s < nza ? L.cptr[a + 1] : 0;
+      }
+      const int nsteps = max(qe[0] - qb[0], qe[1] - qb[1]);
+      for (int q = 0; q < nsteps; q += 8) {
+        double z[2][4];
+        bool ok[2][4];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int qq = qb[s] + q + 2 * u + (mk >> 1);
+            ok[s][u] = qq < qe[s];
+            const int k = L.cobs[ok[s][u] ? qq : 0];
+            const double* src = mi < 9 ? &L.jc[k][9 * row + mi]
+                                : mi < 11 ? &L.ru[k][row + 2 * (mi - 9)] : &L.zero;
+            z[s][u] = *src;
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const double zv = ok[s][u] ? z[s][u] : 0.0;
+            zacc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(zv, zv, zacc[s], 0, 0, 0);
+          }
       }
     }
   }
@@ -822,14 +873,13 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     } else {
       v = Za[9 * 16 + 9];          // |r|^2
     }
-    p.cpart[(size_t)p.cslot_row[cs0 + a] * kCPart + e] = v;
+    p.cpart[(size_t)L.crow[a] * kCPart + e] = v;
   }
-  const int bs0 = p.grp_bslot[sg], nb = p.grp_bslot[sg + 1] - bs0;
   for (int q = t; q < 81 * nb; q += kMWG) {
     const int pr = q / 81, e = q - 81 * (q / 81);
-    const int ab = p.bslot_ab[bs0 + pr], a = ab & 255, b = ab >> 8;
+    const int ab = L.bab[pr], a = ab & 255, b = ab >> 8;
     const int i = e / 9, j = e - 9 * (e / 9);
-    p.bpart[(size_t)p.bslot_row[bs0 + pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
+    p.bpart[(size_t)L.brow[pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
   }
   LINM_T(6);
 }
