@@ -324,11 +324,15 @@ typedef struct slam_ba_problem {
    * grp_ptr = chunks (<= 128 obs, <= 16 points); grp_cslot / grp_bslot are
    * indexed by supergroup. */
   const int32_t* sg_ptr;        /* [n_sgrps+1] chunk range of each supergroup    */
-  const int32_t* sg_cams;       /* [n_sgrps][8] its cameras (<= 7, sorted, -1 padded) */
+  const int32_t* sg_meta;       /* [n_sgrps][24] ch0 ch1 (chunk range), cslot start, m
+                                   (cameras), bslot start, count, the first chunk's
+                                   point and obs range, its cameras[8] (<= 7, sorted,
+                                   -1 padded), pad                              */
   const int32_t* obs_meta;      /* [O] lpt | la << 8 | cobs << 16: chunk-local point,
                                    position of the obs's camera in sg_cams, and the
                                    chunk-local obs list sorted by (la, obs)      */
-  const int32_t* chk_optr;      /* [n_grps+1] first observation of each chunk    */
+  const int32_t* chk_optr;      /* [n_grps+1] first observation of each group /
+                                   chunk (= pt_ptr[grp_ptr]); required in both modes */
   const int32_t* chk_cptr;      /* [n_grps][8] start of each camera's run in chk_cobs */
   const int32_t* bslot_ab;      /* [n_bslots] camera pair a | b << 8 (a < b) of a block slot */
 } slam_ba_problem;

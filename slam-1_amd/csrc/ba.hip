@@ -536,6 +536,7 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 // sums.  Per point: V, g, V*, V*^-1, e as k_linearize (ptdata).
 constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
+constexpr int kSgMeta = 24;  // sg_meta record: ch0 ch1 cs0 m bs0 nb p0 p1 o0 o1 cams[8] pad
 struct MLds {
   double jc[kMObs][18];          // Jc rows (2 x 9)
   double jp[kMObs][6];           // Jp rows (2 x 3)
@@ -579,20 +580,21 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   __shared__ MLds L;
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int ch0 = p.sg_ptr[sg], ch1 = p.sg_ptr[sg + 1];
-  const int cs0 = p.grp_cslot[sg], m = p.grp_cslot[sg + 1] - cs0;
+  // the supergroup record (one hop): chunk range, slot ranges, the first
+  // chunk's extents, its cameras
+  const int* sm = p.sg_meta + kSgMeta * sg;
+  const int ch0 = sm[0], ch1 = sm[1], cs0 = sm[2], m = sm[3], bs0 = sm[4], nb = sm[5];
   const int nt = (9 * m + 15) >> 4;  // tile rows of T
   const int cur = cur_of(p.state);
   const double lam = p.state[SLAM_BA_ST_LAMBDA];
   // the supergroup's camera records -> LDS (one load per lane)
   if (t < kMCams * kCamRec) {
     const int a = t / kCamRec, k = t - kCamRec * (t / kCamRec);
-    const int c = a < m ? p.sg_cams[8 * sg + a] : -1;
+    const int c = a < m ? sm[10 + a] : -1;
     if (c >= 0) L.cam[a][k] = p.camrec[cur][(size_t)kCamRec * c + k];
   }
   if (t == 0) L.zero = 0.0;
   // output rows of this supergroup (read at the end; loaded now, off the tail)
-  const int bs0 = p.grp_bslot[sg], nb = p.grp_bslot[sg + 1] - bs0;
   if (t < m) L.crow[t] = p.cslot_row[cs0 + t];
   if (t >= 64 && t - 64 < nb) {
     L.bab[t - 64] = p.bslot_ab[bs0 + t - 64];
@@ -626,11 +628,17 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   for (int s = 0; s < 2; ++s) zacc[s] = d4{0.0, 0.0, 0.0, 0.0};
   const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
 
+  // chunk extents: the first from the record, the next loaded one chunk ahead
+  int p0 = sm[6], p1 = sm[7], o0 = sm[8], o1 = sm[9];
   for (int ch = ch0; ch < ch1; ++ch) {
-    // chunk extents: four independent loads
-    const int p0 = p.grp_ptr[ch], p1 = p.grp_ptr[ch + 1];
-    const int o0 = p.chk_optr[ch], o1 = p.chk_optr[ch + 1];
     const int nobs = o1 - o0, npts = p1 - p0;
+    int np0 = 0, np1 = 0, no0 = 0, no1 = 0;
+    if (ch + 1 < ch1) {
+      np0 = p.grp_ptr[ch + 1];
+      np1 = p.grp_ptr[ch + 2];
+      no0 = p.chk_optr[ch + 1];
+      no1 = p.chk_optr[ch + 2];
+    }
     // this chunk's inputs, all issued before any is used
     double q0 = 0.0, q1 = 0.0;
     int meta = 0;
@@ -833,6 +841,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
           }
       }
     }
+    p0 = np0; p1 = np1; o0 = no0; o1 = no1;
   }
   // (E) T and the Z_a tiles -> LDS staging (aliases the operand planes), then
   //     the partial rows
@@ -1900,13 +1909,27 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
   __shared__ double snp[kGrp][3];
   __shared__ double red[kGrp / 64];
   __shared__ int last;
+  // group extents in one hop (chk_optr = pt_ptr[grp_ptr])
   const int p0 = p.grp_ptr[g], p1 = p.grp_ptr[g + 1];
-  const int o0 = p.pt_ptr[p0], o1 = p.pt_ptr[p1];
+  const int o0 = p.chk_optr[g], o1 = p.chk_optr[g + 1];
   const int t = threadIdx.x;
   const int o = o0 + t;
   const bool has = o < o1;
   const int cur = cur_of(p.state);
   const bool fail = p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0;
+  // the point lanes' inputs, loaded before the observation phase
+  const bool ptl = t < p1 - p0;
+  double pdv[9], xv[3];
+  int kb = 0, ke = 0;
+  if (ptl) {
+    const double* pd = p.ptdata + (size_t)(p0 + t) * kPtData;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) pdv[k] = pd[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) xv[k] = p.pts[cur][3 * (p0 + t) + k];
+    kb = p.pt_ptr[p0 + t] - o0;
+    ke = p.pt_ptr[p0 + t + 1] - o0;
+  }
   if (has) {
     // dy_o = Y_o^T dc = V*^-1 (W_o^T dc), W_o = Jc^T Jp re-derived from the
     // Jacobian at the live parameters (the one k_linearize used)
@@ -1931,17 +1954,17 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
   }
   __syncthreads();
   double pred = 0.0;
-  if (t < p1 - p0) {
+  if (ptl) {
     const int pt = p0 + t;
     const double lam = p.state[SLAM_BA_ST_LAMBDA];
-    const double* pd = p.ptdata + (size_t)pt * kPtData;
+    const double* pd = pdv;
     double d0 = pd[0], d1 = pd[1], d2 = pd[2];
-    for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
+    for (int k = kb; k < ke; ++k) {
       d0 -= sdy[k][0];
       d1 -= sdy[k][1];
       d2 -= sdy[k][2];
     }
-    const double* x = p.pts[cur] + 3 * pt;
+    const double* x = xv;
     double* xn = p.pts[1 - cur] + 3 * pt;
     snp[t][0] = xn[0] = x[0] + d0;
     snp[t][1] = xn[1] = x[1] + d1;
@@ -2043,8 +2066,9 @@ int check_problem(const slam_ba_problem* p) {
                "slam_ba: null buffer");
   SLAM_REQUIRE(p->n_grps >= 1, "slam_ba: n_grps must be >= 1 (an empty group for P = 0)");
   SLAM_REQUIRE(p->lin_mode == 0 || p->lin_mode == 1, "slam_ba: lin_mode must be 0 or 1");
-  SLAM_REQUIRE(p->lin_mode == 0 || (p->n_sgrps >= 1 && p->sg_ptr && p->sg_cams && p->obs_meta &&
-                                     p->chk_optr && p->chk_cptr && p->bslot_ab),
+  SLAM_REQUIRE(p->chk_optr != nullptr, "slam_ba: chk_optr (= pt_ptr[grp_ptr]) required");
+  SLAM_REQUIRE(p->lin_mode == 0 || (p->n_sgrps >= 1 && p->sg_ptr && p->sg_meta && p->obs_meta &&
+                                     p->chk_cptr && p->bslot_ab),
                "slam_ba: lin_mode 1 needs n_sgrps >= 1 and the supergroup tables");
   SLAM_REQUIRE(sys_packed(p->n_cams) ? (p->n_blocks >= p->n_cams &&
                                         p->n_blocks <= p->n_cams * (p->n_cams + 1) / 2)

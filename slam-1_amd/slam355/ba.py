@@ -199,7 +199,7 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, block_list=None):
         bslot_blk=i32(bslot_blk), bslot_pair_ptr=i32(bslot_pair_ptr), bslot_pairs=i32(bslot_pairs),
         blocks=i32(np.stack([c1, c2], 1)), cam_cslot_ptr=i32(cam_cslot_ptr),
         cslot_row=i32(cslot_row), blk_bslot_ptr=i32(blk_bslot_ptr), bslot_row=i32(bslot_row),
-        n_obs=O)
+        chk_optr=i32(pt_ptr[grp_ptr]), n_obs=O)
 
 
 # Camera-union linearisation (csrc/ba.hip k_lin_mfma): points ordered by their
@@ -379,8 +379,18 @@ def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=Non
     c1, c2 = c1[blist], c2[blist]
     i32 = lambda a: np.asarray(a, np.int32)  # noqa: E731
     one = np.zeros(1, np.int32)
+    # one record per supergroup (csrc/ba.hip kSgMeta): everything k_lin_mfma
+    # needs before its first chunk's loads, in one hop
+    sg_meta = np.zeros((NS, 24), np.int64)
+    fch = sg_ptr[:-1]
+    sg_meta[:, 0], sg_meta[:, 1] = sg_ptr[:-1], sg_ptr[1:]
+    sg_meta[:, 2], sg_meta[:, 3] = grp_cslot[:-1], ms
+    sg_meta[:, 4], sg_meta[:, 5] = grp_bslot[:-1], np.diff(grp_bslot)
+    sg_meta[:, 6], sg_meta[:, 7] = grp_ptr[fch], grp_ptr[fch + 1]
+    sg_meta[:, 8], sg_meta[:, 9] = pt_ptr[grp_ptr[fch]], pt_ptr[grp_ptr[fch + 1]]
+    sg_meta[:, 10:18] = sg_cams
     return dict(
-        mode=1, perm=perm, order=order, obs_cam=i32(obs_cam), obs_pt=i32(obs_pt),
+        mode=1, sg_meta=i32(sg_meta), perm=perm, order=order, obs_cam=i32(obs_cam), obs_pt=i32(obs_pt),
         pt_ptr=i32(pt_ptr), grp_ptr=i32(grp_ptr), grp_cslot=i32(grp_cslot),
         cslot_cam=i32(cslot_cam), cslot_obs_ptr=one, cslot_obs=one, grp_bslot=i32(grp_bslot),
         bslot_blk=i32(blk), bslot_pair_ptr=one, bslot_pairs=one,
@@ -418,8 +428,8 @@ def tiled_solve_flops(n_cams, blocks, tb=64):
     return flops
 
 
-_MFMA_TABLES = ("sg_ptr", "sg_cams", "obs_meta", "chk_optr", "chk_cptr", "bslot_ab")
-_INDEX_TABLES = ("obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
+_MFMA_TABLES = ("sg_ptr", "sg_meta", "obs_meta", "chk_cptr", "bslot_ab")
+_INDEX_TABLES = ("chk_optr", "obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
                  "cslot_obs_ptr", "cslot_obs", "grp_bslot", "bslot_blk", "bslot_pair_ptr",
                  "bslot_pairs", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
                  "bslot_row")
