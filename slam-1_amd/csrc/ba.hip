@@ -534,25 +534,17 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 // per camera a one cpart row (U_a - T_aa, Jc^T r, Jc^T u, diag U, |r|^2), per
 // co-observed camera pair a < b one bpart row (T_ab) -- the rows k_assemble
 // sums.  Per point: V, g, V*, V*^-1, e as k_linearize (ptdata).
-constexpr int kMObs = 64, kMPts = 8, kMCams = 7, kMRows = 64;
+constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
 constexpr int kSgMeta = 24;  // sg_meta record: ch0 ch1 cs0 m bs0 nb p0 p1 o0 o1 cams[8] pad
 struct MLds {
-  union {
-    struct {
-      double jc[kMObs][18];          // Jc rows (2 x 9)
-      double jp[kMObs][6];           // Jp rows (2 x 3)
-      double ru[kMObs][4];           // r0 r1 u0 u1
-      double vi[kMPts][6];           // V*^-1 (i00 i01 i02 i11 i12 i22)
-      double e[kMPts][3];
-      double yt[kMPts][3][kMRows];   // Y_p, [point][k][row]: the MFMA A operand
-      double wt[kMPts][3][kMRows];   // W_p, [point][k][row]: the MFMA B operand
-    };
-    struct {                         // write-out staging (after the last chunk)
-      double Tt[10][256];            // the upper 16x16 tiles of T, row-major tile order
-      double Zt[kMCams][256];        // Z_a
-    };
-  };
+  double jc[kMObs][18];          // Jc rows (2 x 9)
+  double jp[kMObs][6];           // Jp rows (2 x 3)
+  double ru[kMObs][4];           // r0 r1 u0 u1
+  double vi[kMPts][6];           // V*^-1 (i00 i01 i02 i11 i12 i22)
+  double e[kMPts][3];
+  double yt[kMPts][3][kMRows];   // Y_p, [point][k][row]: the MFMA A operand
+  double wt[kMPts][3][kMRows];   // W_p, [point][k][row]: the MFMA B operand
   double cam[kMCams][kCamRec];   // the supergroup's camera records (live parameters)
   double X[kMPts][3];            // the chunk's points
   double zero;                   // operand of padded MFMA lanes
@@ -564,12 +556,9 @@ struct MLds {
   int crow[kMCams];              // cpart row of each camera slot
   int bab[kMCams * (kMCams - 1) / 2], brow[kMCams * (kMCams - 1) / 2];  // block slots
 };
-// three workgroups per CU: LDS <= 160 KiB / 3 and <= 168 VGPRs (launch bounds)
-static_assert(sizeof(MLds) <= 53 * 1024, "k_lin_mfma: three workgroups per CU");
+static_assert(sizeof(MLds) <= 80 * 1024, "k_lin_mfma: two workgroups per CU");
 static_assert(9 * kMCams <= kMRows, "k_lin_mfma: 9m rows in 4 tile rows");
-
-// upper tile (I <= J) of an nt x nt tile grid -> its slot in Tt
-__device__ __forceinline__ int tslot(int I, int J, int nt) { return I * nt - I * (I - 1) / 2 + (J - I); }
+static_assert(2 * kMPts * 3 * kMRows >= kMRows * kMRows + kMCams * 256, "staging aliases yt/wt");
 
 #ifdef SLAM_LINM_PROFILE
 __device__ unsigned long long g_linm_stamp[4096][8];
@@ -582,7 +571,7 @@ __device__ unsigned long long g_linm_stamp[4096][8];
 #define LINM_T(i) (void)0
 #endif
 
-__global__ __launch_bounds__(kMWG, 3) void k_lin_mfma(BaBatch bat) {
+__global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   BA_PROB(bat);
   const int sg = blockIdx.x;
   if (sg >= p.n_sgrps) return;  // batch: grid.x covers the largest problem
@@ -740,44 +729,45 @@ __global__ __launch_bounds__(kMWG, 3) void k_lin_mfma(BaBatch bat) {
     }
     __syncthreads();
     LINM_T(3);
-    // (C) per observation, rows of W~ split over three lanes (lane h * 64 + k:
-    //     rows 3h .. 3h + 2, h < 3): W~_{p,a} rows summed over the run of
+    // (C) per observation, rows i of W~ split over two lanes (lane t: rows
+    //     0..4, lane t + 128: rows 5..8): W~_{p,a} rows summed over the run of
     //     observations of the same (point, camera) (adjacent: obs are sorted by
-    //     point, then camera), Y = W~ V*^-1, into the operand planes; lanes
-    //     192 + k: u_k = Jp_k e_p.
+    //     point, then camera), Y = W~ V*^-1, into the operand planes; u_o.
     {
-      const int h = t >> 6, k0 = t & 63;
-      if (h < 3) {
-        const bool lead = k0 < nobs && (k0 == 0 || L.lpt[k0 - 1] != L.lpt[k0] ||
-                                        L.la[k0 - 1] != L.la[k0]);
-        if (lead) {
-          const int lp = L.lpt[k0], a = L.la[k0];
-          const int ib = 3 * h;
-          double W[3][3];
+      const int h = t >> 7, k0 = t & 127;
+      const bool lead = k0 < nobs && (k0 == 0 || L.lpt[k0 - 1] != L.lpt[k0] ||
+                                      L.la[k0 - 1] != L.la[k0]);
+      if (lead) {
+        const int lp = L.lpt[k0], a = L.la[k0];
+        const int ib = h ? 5 : 0, ie = h ? 9 : 5;
+        double W[5][3];
 #pragma unroll
-          for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 5; ++i)
 #pragma unroll
-            for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
-          for (int k = k0; k < nobs && L.lpt[k] == lp && L.la[k] == a; ++k) {
+          for (int c = 0; c < 3; ++c) W[i][c] = 0.0;
+        for (int k = k0; k < nobs && L.lpt[k] == lp && L.la[k] == a; ++k) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
+          for (int i = 0; i < 5; ++i) {
+            if (ib + i >= ie) break;
 #pragma unroll
-              for (int c = 0; c < 3; ++c)
-                W[i][c] += L.jc[k][ib + i] * L.jp[k][c] + L.jc[k][9 + ib + i] * L.jp[k][3 + c];
-          }
-          const double* vi = L.vi[lp];
-          const double V[3][3] = {{vi[0], vi[1], vi[2]}, {vi[1], vi[3], vi[4]}, {vi[2], vi[4], vi[5]}};
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const int row = 9 * a + ib + i;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              L.wt[lp][c][row] = W[i][c];
-              L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
-            }
+            for (int c = 0; c < 3; ++c)
+              W[i][c] += L.jc[k][ib + i] * L.jp[k][c] + L.jc[k][9 + ib + i] * L.jp[k][3 + c];
           }
         }
-      } else if (k0 < nobs) {
+        const double* vi = L.vi[lp];
+        const double V[3][3] = {{vi[0], vi[1], vi[2]}, {vi[1], vi[3], vi[4]}, {vi[2], vi[4], vi[5]}};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          if (ib + i >= ie) break;
+          const int row = 9 * a + ib + i;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            L.wt[lp][c][row] = W[i][c];
+            L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
+          }
+        }
+      }
+      if (h == 0 && k0 < nobs) {
         const double* e = L.e[L.lpt[k0]];
         L.ru[k0][2] = L.jp[k0][0] * e[0] + L.jp[k0][1] * e[1] + L.jp[k0][2] * e[2];
         L.ru[k0][3] = L.jp[k0][3] * e[0] + L.jp[k0][4] * e[1] + L.jp[k0][5] * e[2];
@@ -857,37 +847,32 @@ __global__ __launch_bounds__(kMWG, 3) void k_lin_mfma(BaBatch bat) {
   //     the partial rows
   __syncthreads();
   LINM_T(5);
+  double* T = &L.yt[0][0][0];
+  double* Z = T + kMRows * kMRows;  // [kMCams][16][16]
 #pragma unroll
   for (int s = 0; s < 3; ++s) {
     if (s >= ntl) break;
-    double* Tt = L.Tt[tslot(tI[s], tJ[s], nt)];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Tt[(mk + 4 * r) * 16 + mi] = acc[s][r];
+    for (int r = 0; r < 4; ++r)
+      T[(16 * tI[s] + mk + 4 * r) * kMRows + 16 * tJ[s] + mi] = acc[s][r];
   }
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     if (s >= nza) break;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) L.Zt[wid + 4 * s][(mk + 4 * r) * 16 + mi] = zacc[s][r];
+    for (int r = 0; r < 4; ++r) Z[(wid + 4 * s) * 256 + (mk + 4 * r) * 16 + mi] = zacc[s][r];
   }
   __syncthreads();
-  // T(row, col) from the upper tiles (T is symmetric)
-  auto Tget = [&](int row, int col) -> double {
-    int I = row >> 4, J = col >> 4;
-    if (I > J) {
-      const int tmp = row; row = col; col = tmp;
-      I = row >> 4; J = col >> 4;
-    }
-    return L.Tt[tslot(I, J, nt)][(row & 15) * 16 + (col & 15)];
-  };
   // camera rows: items (a, 112-wide row entry)
   for (int q = t; q < m * 109; q += kMWG) {
     const int a = q / 109, e = q - 109 * (q / 109);
-    const double* Za = L.Zt[a];
+    const double* Za = Z + a * 256;
     double v;
     if (e < 81) {
       const int i = e / 9, j = e - 9 * (e / 9);
-      v = Za[i * 16 + j] - Tget(9 * a + i, 9 * a + j);
+      const int row = 9 * a + i, col = 9 * a + j;  // T is symmetric; upper tiles were formed
+      const double tv = (row >> 4) <= (col >> 4) ? T[row * kMRows + col] : T[col * kMRows + row];
+      v = Za[i * 16 + j] - tv;
     } else if (e < 90) {
       v = Za[(e - 81) * 16 + 9];   // Jc^T r
     } else if (e < 99) {
@@ -903,7 +888,7 @@ __global__ __launch_bounds__(kMWG, 3) void k_lin_mfma(BaBatch bat) {
     const int pr = q / 81, e = q - 81 * (q / 81);
     const int ab = L.bab[pr], a = ab & 255, b = ab >> 8;
     const int i = e / 9, j = e - 9 * (e / 9);
-    p.bpart[(size_t)L.brow[pr] * 81 + e] = Tget(9 * a + i, 9 * b + j);
+    p.bpart[(size_t)L.brow[pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
   }
   LINM_T(6);
 }

@@ -207,8 +207,8 @@ def plan(n_cams, n_pts, cam_idx, pt_idx, block_list=None):
 # together see at most MF_CAMS cameras, so a supergroup's share of the
 # reduced camera system is one dense (9m x 9m, m <= 7) matrix: the Schur term
 # sum_p Y_p W_p^T on the f64 matrix cores, U on the vector ALUs.
-MF_CHUNK_OBS = 64   # kMObs: observations per chunk (<= k_back_trial's group cap 128)
-MF_CHUNK_PTS = 8    # kMPts: points per chunk
+MF_CHUNK_OBS = 120  # kMObs: observations per chunk (<= k_back_trial's group cap 128)
+MF_CHUNK_PTS = 16   # kMPts: points per chunk
 MF_CAMS = 7         # kMCams: cameras per supergroup (9m <= 63 rows: 4 MFMA tile rows)
 
 

@@ -472,7 +472,7 @@ def _emulate_union_linearisation(pl, C, cams, pts_new, qs_sorted, lam):
         for ch in range(pl["sg_ptr"][sg], pl["sg_ptr"][sg + 1]):
             p0, p1 = pl["grp_ptr"][ch], pl["grp_ptr"][ch + 1]
             o0, o1 = pl["pt_ptr"][p0], pl["pt_ptr"][p1]
-            assert o1 - o0 <= 64 and p1 - p0 <= 8
+            assert o1 - o0 <= 120 and p1 - p0 <= 16
             for q in range(p0, p1):
                 Wp = np.zeros((9 * m, 3))
                 for o in range(pl["pt_ptr"][q], pl["pt_ptr"][q + 1]):
