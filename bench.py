@@ -748,7 +748,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ba-scale", action="store_true",
                     help="tracking: skip the sharded C4 local-BA iterations/s measurement")
-    ap.add_argument("--track-cus", type=int, default=224,
+    ap.add_argument("--track-cus", type=int, default=0,
                     help="restrict the tracking stream to this many CUs (0: all); the rest run "
                          "only local-BA work, whose latency-bound kernels then do not share "
                          "SIMDs and LDS with ORB workgroups")

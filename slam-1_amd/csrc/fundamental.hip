@@ -6,15 +6,17 @@
 // Hartley-normalised Gauss-Jordan null space, cubic roots, float errors,
 // min-median selection, OpenCV's robust sigma for the final inlier mask).
 //
-// One workgroup (8 waves) per frame pair:
+// k_fm_hyp: kSplit workgroups (8 waves) per frame pair, each a contiguous
+// range of the hypotheses:
 //   phase 1: one hypothesis per lane -> up to 3 candidate F in LDS;
-//   phase 2: wave w owns hypotheses h = w mod 8.  Per candidate the wave counts
-//            errors below its best median so far (exact reject: the median
-//            improves iff more than M/2 errors are below it); only improving
-//            candidates pay an exact radix-select median (4 x 8-bit passes,
-//            errors recomputed per pass instead of stored);
-//   phase 3: merge the 8 wave bests (min median, lowest candidate index);
-//   phase 4: inlier mask of the winner.
+//   phase 2: wave w owns hypotheses h = w mod 8 of the range.  Per candidate the
+//            wave counts errors below its best median so far (exact reject: the
+//            median improves iff more than M/2 errors are below it); only
+//            improving candidates pay an exact radix-select median (4 x 8-bit
+//            passes, errors recomputed per pass instead of stored);
+//   phase 3: the workgroup's best (min median, lowest candidate index);
+// k_fm_finish: one workgroup per pair merges the kSplit bests by the same rule,
+//   recomputes the winner and writes the inlier mask.
 #include "common.hpp"
 
 #include <cmath>
@@ -294,38 +296,38 @@ __device__ __forceinline__ float fm_error(const double* F, const double* p1, con
   return isnan(e) ? INFINITY : e;
 }
 
-__global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1all,
-                                                  const double* __restrict__ m2all,
-                                                  const int32_t* __restrict__ count, int cap,
-                                                  uint64_t seed, int item0, int n_hyp,
-                                                  uint8_t* __restrict__ mask,
-                                                  double* __restrict__ Fout,
-                                                  int32_t* __restrict__ ninl) {
-  __shared__ double cand[kMaxHyp / 2][3][9];  // hypotheses processed in rounds of 256
-  __shared__ int ncand[kMaxHyp / 2];
+// Hypotheses of one frame pair are spread over kSplit workgroups (a
+// contiguous hypothesis range each), so a batch of B pairs fills B * kSplit
+// workgroups; each reports its best (median, candidate index) and k_fm_finish
+// merges them (min median, lowest index: the order-independent rule of the
+// single-workgroup form) and computes the mask.  The per-split bests travel in
+// F's own slot (72 B per pair), which k_fm_finish then overwrites.
+constexpr int kSplit = 8;
+constexpr int kRound = 64;  // hypotheses per round (one per lane of wave 0)
+static_assert(kSplit * 8 <= 9 * 8, "per-split bests must fit F[b]");
+
+__global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all,
+                                                const double* __restrict__ m2all,
+                                                const int32_t* __restrict__ count, int cap,
+                                                uint64_t seed, int item0, int n_hyp,
+                                                double* __restrict__ Fout) {
+  __shared__ double cand[kRound][3][9];  // hypotheses processed in rounds of kRound
+  __shared__ int ncand[kRound];
   __shared__ int hist[kWaves][256];
   __shared__ float wbest[kWaves];
   __shared__ int wbidx[kWaves];
-  __shared__ double Fb[9];
-  __shared__ double Fw[3][9];  // the winner's candidates, recomputed
-  __shared__ float best_s;
-  __shared__ int found_s, cnt_s;
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int b = blockIdx.x, sp = blockIdx.y, t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int M = min(max(count[b], 0), cap);
+  if (M < 8) return;  // k_fm_finish writes the empty mask
   const double* m1 = m1all + (size_t)b * cap * 2;
   const double* m2 = m2all + (size_t)b * cap * 2;
-  uint8_t* mk = mask + (size_t)b * cap;
-  if (M < 8) {
-    for (int i = t; i < M; i += kWG) mk[i] = 0;
-    if (t == 0) ninl[b] = -1;
-    return;
-  }
+  const int hb = (int)((long long)n_hyp * sp / kSplit), he = (int)((long long)n_hyp * (sp + 1) / kSplit);
   float my_best = INFINITY;
   int my_idx = 0x7FFFFFFF;
   const int need = M / 2 + 1;  // #errors below a value for the median to be below it
-  for (int h0 = 0; h0 < n_hyp; h0 += kMaxHyp / 2) {
-    const int nh = min(kMaxHyp / 2, n_hyp - h0);
+  for (int h0 = hb; h0 < he; h0 += kRound) {
+    const int nh = min(kRound, he - h0);
     __syncthreads();
     if (t < nh) {
       const int h = h0 + t;
@@ -403,11 +405,51 @@ __global__ __launch_bounds__(kWG) void k_fm_lmeds(const double* __restrict__ m1a
         bm = wbest[i];
         bi = wbidx[i];
       }
+    float* slot = reinterpret_cast<float*>(Fout + 9 * (size_t)b) + 2 * sp;
+    slot[0] = bm;
+    reinterpret_cast<int*>(slot)[1] = bi;
+  }
+}
+
+__global__ __launch_bounds__(kWG) void k_fm_finish(const double* __restrict__ m1all,
+                                                   const double* __restrict__ m2all,
+                                                   const int32_t* __restrict__ count, int cap,
+                                                   uint64_t seed, int item0,
+                                                   uint8_t* __restrict__ mask,
+                                                   double* __restrict__ Fout,
+                                                   int32_t* __restrict__ ninl) {
+  __shared__ double Fb[9];
+  __shared__ double Fw[3][9];  // the winner's candidates, recomputed
+  __shared__ float best_s;
+  __shared__ int found_s, cnt_s;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63;
+  const int M = min(max(count[b], 0), cap);
+  const double* m1 = m1all + (size_t)b * cap * 2;
+  const double* m2 = m2all + (size_t)b * cap * 2;
+  uint8_t* mk = mask + (size_t)b * cap;
+  if (M < 8) {
+    for (int i = t; i < M; i += kWG) mk[i] = 0;
+    if (t == 0) ninl[b] = -1;
+    return;
+  }
+  if (t == 0) {
+    const float* slots = reinterpret_cast<const float*>(Fout + 9 * (size_t)b);
+    float bm = INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int i = 0; i < kSplit; ++i) {
+      const float v = slots[2 * i];
+      const int ix = reinterpret_cast<const int*>(slots)[2 * i + 1];
+      if (v < bm || (v == bm && ix < bi)) {
+        bm = v;
+        bi = ix;
+      }
+    }
     best_s = bm;
     found_s = bi != 0x7FFFFFFF && bm < INFINITY;
     cnt_s = 0;
     if (found_s) {
-      // recompute the winner (its hypothesis round is gone from LDS)
+      // recompute the winner
       const int h = bi / 3, k = bi % 3;
       uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
                    ((uint64_t)h * 0x9FB21C651E98DF25ull);
@@ -487,9 +529,12 @@ extern "C" int slam_fundamental_lmeds(const double* d_m1, const double* d_m2,
   if (batch == 0) return SLAM_OK;
   SLAM_REQUIRE(d_m1 && d_m2 && d_count && d_mask && d_F && d_ninliers,
                "slam_fundamental_lmeds: null pointer");
-  k_fm_lmeds<<<batch, kWG, 0, slam::as_stream(stream)>>>(d_m1, d_m2, d_count, cap, seed, item0,
-                                                         n_hyp, d_mask, d_F, d_ninliers);
-  SLAM_LAUNCHED("k_fm_lmeds");
+  hipStream_t s = slam::as_stream(stream);
+  k_fm_hyp<<<dim3(batch, kSplit), kWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, n_hyp, d_F);
+  SLAM_LAUNCHED("k_fm_hyp");
+  k_fm_finish<<<batch, kWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, d_mask, d_F,
+                                    d_ninliers);
+  SLAM_LAUNCHED("k_fm_finish");
   return SLAM_OK;
 }
 
