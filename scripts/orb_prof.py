@@ -9,23 +9,25 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "slam-1_amd")]
 
+os.environ.setdefault("SLAM355_LIB", os.path.join(ROOT, "slam-1_amd", "prof", "libslam355_orbprof.so"))
 import torch  # noqa: E402
 
 from slam355 import _lib, orb  # noqa: E402
-from slam355.synthetic import stereo_sequence  # noqa: E402
+from slam355.synthetic import corridor_sequence  # noqa: E402
 
 B = 32
-L, R, _, _ = stereo_sequence(B + 1, 1280, 720, seed=1000)
-imgs = torch.from_numpy(np.concatenate([L, R[:B]])).cuda()
+KP = 64
+L, R, _, _ = corridor_sequence(B + 1, 1280, 720, seed=1000, device="cuda", as_numpy=False)
+imgs = torch.cat([L, R[:B]]).contiguous()
 f = _lib.lib.slam_orb_profile_read
 f.argtypes = [ctypes.c_void_p]
 buf = (ctypes.c_ulonglong * 16)()
-orb.orb_batch(imgs, 56)
+orb.orb_batch(imgs, KP)
 f(buf)
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ev0.record()
 for _ in range(5):
-    orb.orb_batch(imgs, 56)
+    orb.orb_batch(imgs, KP)
 ev1.record()
 torch.cuda.synchronize()
 f(buf)

@@ -1100,6 +1100,17 @@ struct BlkLds {
   }
 };
 
+#ifdef SLAM_SOLVE_TRACE
+__device__ unsigned long long g_solve_trace[20][6];
+#define SOLVE_TR(step, i)                                                        \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && (step) < 20)                      \
+      g_solve_trace[step][i] = __builtin_amdgcn_s_memtime();                     \
+  } while (0)
+#else
+#define SOLVE_TR(step, i) (void)0
+#endif
+
 __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
   BA_PROB(bat);
   lm_wave_priority();
@@ -1123,6 +1134,7 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int NT = g.n16 / 16, NL = NT * (NT + 1) / 2;
   SOLVE_PROF_T(0);
+  SOLVE_TR(19, 1);
   const int n2 = (n + 1) & ~1;
   if (t == 0) *fail_p = 0;
   for (int i = t; i < 2 * g.n16 * kWLs; i += kBlkWG) WL[i] = 0.0;  // WL and LL
@@ -1171,7 +1183,9 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
   }
   SOLVE_PROF_T(1);
   bool ok = true;
+  SOLVE_TR(19, 0);
   for (int c0 = 0; c0 < n; c0 += kPanelW) {
+    SOLVE_TR(c0 / kPanelW, 0);
 #ifdef SLAM_SOLVE_PROFILE_STEP
     const uint64_t q0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1189,6 +1203,7 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
       }
     }
     __syncthreads();
+    SOLVE_TR(c0 / kPanelW, 1);
 #ifdef SLAM_SOLVE_PROFILE_STEP
     const uint64_t q1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1272,7 +1287,9 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
 #ifdef SLAM_SOLVE_PROFILE_STEP
     const uint64_t q2 = __builtin_amdgcn_s_memtime();
 #endif
+    SOLVE_TR(c0 / kPanelW, 2);
     __syncthreads();
+    SOLVE_TR(c0 / kPanelW, 3);
 #ifdef SLAM_SOLVE_PROFILE_STEP
     const uint64_t q3 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1304,6 +1321,14 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
         if (live[s])
           acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[s][kk], lb[s][kk], acc[s], 0, 0, 0);
     }
+#ifdef SLAM_SOLVE_TRACE
+    if (threadIdx.x == 0) {
+      double chk = acc[0][0];
+      __asm__ volatile("" : "+v"(chk));
+      acc[0][0] = chk;
+    }
+    SOLVE_TR(c0 / kPanelW, 4);
+#endif
 #ifdef SLAM_SOLVE_PROFILE_STEP
     __builtin_amdgcn_s_waitcnt(0);
     const uint64_t q4 = __builtin_amdgcn_s_memtime();
@@ -1318,6 +1343,7 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
 #endif
   }
   SOLVE_PROF_T(2);
+  SOLVE_TR(18, 0);
   if (ok && wid == 0) {
     // z = D^-1 y, then L^T x = z from the bottom; lane l holds rows l, l + 64.
     // Step k: x_i -= L(k, i) x_k for i < k, x_k broadcast by v_readlane.  Rows
@@ -1372,8 +1398,10 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
   }
   __syncthreads();
   SOLVE_PROF_T(3);
+  SOLVE_TR(18, 1);
   solve_epilogue(p, X, ok, red, EpiSrc{Eb + n2, Eb + 2 * n2, Eb + 3 * n2, Eb + 4 * n2});
   SOLVE_PROF_END();
+  SOLVE_TR(18, 2);
 }
 
 // ---------------------------------------------------------------- tiled solve
@@ -2262,6 +2290,14 @@ extern "C" int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, 
   }
   return SLAM_OK;
 }
+
+#ifdef SLAM_SOLVE_TRACE
+extern "C" int slam_solve_trace(unsigned long long* out) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_trace), 20 * 6 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif
 
 #ifdef SLAM_LINM_PROFILE
 extern "C" int slam_linm_stamps(unsigned long long* out, int n) {
