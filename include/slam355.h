@@ -140,7 +140,10 @@ int slam_triangulate(const double* d_ptl, const double* d_ptr, const int32_t* d_
 int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count, int cap,
                     int batch, const double* d_K, uint64_t seed, int item0, int n_hyp,
                     double reproj_thresh, int hyp_iters, int refine_iters, double* d_rvec,
-                    double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, void* stream);
+                    double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, double* d_ws,
+                    void* stream);
+/* Doubles of slam_pnp_ransac's workspace d_ws (the hypothesis poses). */
+long long slam_pnp_workspace_len(int batch, int n_hyp);
 
 /* Pose chain of main.py:94-98, 120-124 (pose_{b+1} = pose_b @ T_b with
  * T_b = [Rodrigues(-rvec_b) | -tvec_b], transformation.py:15-19; when

@@ -4,14 +4,15 @@
  * CPU restatement of the pose step of the reference's tracking loop:
  *   /root/reference/transformation.py:5-19  cv2.solvePnPRansac(Q, q, K, zeros(5))
  *     (defaults: SOLVEPNP_ITERATIVE, 100 iterations, 8 px, confidence 0.99)
- * OpenCV's RNG sequence and DLT initialisation are not reproducible here
+ * OpenCV's RNG sequence and exact EPnP arithmetic are not reproducible here
  * (OpenCV absent; PARITY UNPINNED vs OpenCV), so the deterministic spec both
  * this oracle and the HIP kernel follow is:
  *   - n_hyp hypotheses; hypothesis h draws 5 distinct indices from a
  *     splitmix64 stream seeded with seed ^ (frame * C1) ^ (h * C2);
- *   - each hypothesis: LM (lambda 1e-3, x0.1 / x10, Marquardt diagonal) from
- *     r = t = 0 on its 5 points, hyp_iters iterations (small inter-frame motion,
- *     the in-repo LM template of visual_odometry.py:135-157);
+ *   - each hypothesis: EPnP on its 5 points (epnp.h: OpenCV's RANSAC kernel
+ *     for SOLVEPNP_ITERATIVE is EPnP on 5-point samples), then LM (lambda
+ *     1e-3, x0.1 / x10, Marquardt diagonal) from that pose on the same points,
+ *     hyp_iters iterations (a degenerate sample starts LM from r = t = 0);
  *   - score = #points with squared reprojection error <= thresh^2; best = max
  *     score, lowest h on ties;
  *   - refinement: the same LM from the best hypothesis over its inlier set,
@@ -23,6 +24,7 @@
 #include <string.h>
 
 #include "pose_util.h"
+#include "epnp.h"
 
 typedef struct { double fx, fy, cx, cy; } camk;
 
@@ -117,6 +119,12 @@ static void lm(const double* Q, const double* q, const int* idx, int n, const ui
   }
 }
 
+/* EPnP on n (4..8) points: p = (rvec, t), X_cam = R(rvec) X + t; returns 1 if finite */
+int oracle_epnp(const double* pw, const double* uv, int n, const double* Kmat, double* p) {
+  if (n < 4 || n > EPNP_MAXN) return 0;
+  return epnp(pw, uv, n, Kmat[0], Kmat[4], Kmat[2], Kmat[5], p);
+}
+
 /* returns #inliers of the chosen hypothesis, -1 if L < 5 */
 int oracle_pnp_ransac(const double* Q, const double* q, int L, const double* Kmat, uint64_t seed,
                       int item, int n_hyp, double thresh, int hyp_iters, int refine_iters,
@@ -143,7 +151,17 @@ int oracle_pnp_ransac(const double* Q, const double* q, int L, const double* Kma
       } while (dup);
       idx[k] = v;
     }
+    /* EPnP seed on the sample (OpenCV's RANSAC kernel for ITERATIVE), then LM
+       on the same 5 points; a degenerate sample starts LM from r = t = 0 */
     double p[6] = {0, 0, 0, 0, 0, 0}, R[9];
+    {
+      double pw[15], uv[10];
+      for (int k = 0; k < 5; ++k) {
+        memcpy(pw + 3 * k, Q + 3 * idx[k], 3 * sizeof(double));
+        memcpy(uv + 2 * k, q + 2 * idx[k], 2 * sizeof(double));
+      }
+      if (!epnp(pw, uv, 5, K.fx, K.fy, K.cx, K.cy, p)) memset(p, 0, sizeof(p));
+    }
     lm(Q, q, idx, 5, NULL, L, &K, hyp_iters, p);
     int c = 0;
     int finite = 1;

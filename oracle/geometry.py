@@ -131,6 +131,18 @@ def pnp_ransac(Q, q, K, seed=0, item=0, n_hyp=100, thresh=8.0, hyp_iters=10, ref
     return out + (hyp, hc) if return_hypotheses else out
 
 
+def epnp(pw, uv, K):
+    """EPnP (oracle/epnp.h) on 4..8 points -> (rvec, t) as one array [6], or None."""
+    pw = np.ascontiguousarray(pw, np.float64).reshape(-1, 3)
+    uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
+    K = np.ascontiguousarray(K, np.float64).reshape(3, 3)
+    f = lib().oracle_epnp
+    f.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    p = np.zeros(6)
+    return p if f(_ptr(pw), _ptr(uv), len(pw), _ptr(K), _ptr(p)) else None
+
+
 _VO = None
 
 

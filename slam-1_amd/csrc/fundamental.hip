@@ -25,7 +25,6 @@ namespace {
 
 constexpr int kWG = 512;
 constexpr int kWaves = kWG / 64;
-constexpr int kMaxHyp = 512;
 constexpr int kS = 7;
 
 __device__ inline uint64_t splitmix64(uint64_t& s) {

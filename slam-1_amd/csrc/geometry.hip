@@ -10,6 +10,7 @@
 // hypothesis) so the CPU oracle draws the same subsets (OpenCV's own RNG
 // sequence is not reproducible here).
 #include "common.hpp"
+#include "epnp.hpp"
 #include "dlt.hpp"
 
 #include <climits>
@@ -275,6 +276,58 @@ __device__ __forceinline__ double wave_allsum(double v) {
   return v;
 }
 
+// PnP-RANSAC hypotheses: kHypLanes per workgroup, one per lane.  Sample h of
+// pair b: 5 distinct indices from splitmix64(seed, item0 + b, h); EPnP on the
+// sample (OpenCV's RANSAC kernel for SOLVEPNP_ITERATIVE), then hyp_iters LM
+// steps on the same 5 points from that pose (a degenerate sample starts LM at
+// r = t = 0).  Poses -> ws [b][h][6].  The 12x12 EPnP matrices sit in LDS.
+constexpr int kHypLanes = 16;
+__global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
+                                                const double* __restrict__ qall,
+                                                const int32_t* __restrict__ count, int cap,
+                                                const double* __restrict__ Kp, uint64_t seed,
+                                                int item0, int n_hyp, int hyp_iters,
+                                                double* __restrict__ ws) {
+  __shared__ double mt[kHypLanes][144];
+  __shared__ double v12[kHypLanes][144];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int h = blockIdx.y * kHypLanes + t;
+  const int L = min(max(count[b], 0), cap);
+  if (L < kMinSample || t >= kHypLanes || h >= n_hyp) return;
+  const double* Q = Qall + (size_t)b * cap * 3;
+  const double* q = qall + (size_t)b * cap * 2;
+  const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
+  uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+               ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+  int idx[kMinSample];
+#pragma unroll
+  for (int k = 0; k < kMinSample; ++k) {
+    int v;
+    bool dup;
+    do {
+      v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
+      dup = false;
+#pragma unroll
+      for (int j = 0; j < k; ++j) dup |= idx[j] == v;
+    } while (dup);
+    idx[k] = v;
+  }
+  double p[6] = {0, 0, 0, 0, 0, 0};
+  {
+    double pw[3 * kMinSample], uv[2 * kMinSample];
+#pragma unroll
+    for (int k = 0; k < kMinSample; ++k) {
+      for (int d = 0; d < 3; ++d) pw[3 * k + d] = Q[3 * idx[k] + d];
+      for (int d = 0; d < 2; ++d) uv[2 * k + d] = q[2 * idx[k] + d];
+    }
+    if (!slam_epnp::epnp(pw, uv, kMinSample, K.fx, K.fy, K.cx, K.cy, p, mt[t], v12[t]))
+      for (int i = 0; i < 6; ++i) p[i] = 0.0;
+  }
+  lm_small(Q, q, idx, kMinSample, K, hyp_iters, p);
+  double* o = ws + ((size_t)b * n_hyp + h) * 6;
+  for (int i = 0; i < 6; ++i) o[i] = p[i];
+}
+
 // One workgroup per frame pair:
 //   hypotheses   one per lane: 5 distinct random points, LM from r = t = 0; the
 //                pose and its rotation matrix go to LDS;
@@ -293,7 +346,8 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
                                                 int hyp_iters, int refine_iters,
                                                 double* __restrict__ rvec, double* __restrict__ tvec,
                                                 int32_t* __restrict__ ninl,
-                                                uint8_t* __restrict__ mask) {
+                                                uint8_t* __restrict__ mask,
+                                                const double* __restrict__ hws) {
   __shared__ double hp[kMaxHyp][6];
   __shared__ double hR[kMaxHyp][9];
   __shared__ int hcnt[kMaxHyp];
@@ -317,25 +371,11 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
 #ifdef SLAM_PNP_PROFILE
   const uint64_t pt0 = __builtin_amdgcn_s_memtime();
 #endif
-  // ---- hypotheses
+  // ---- hypotheses (k_pnp_hyp: EPnP + LM on each sample)
   for (int h = t; h < n_hyp; h += kPnPWG) {
-    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
-    int idx[kMinSample];
-#pragma unroll
-    for (int k = 0; k < kMinSample; ++k) {
-      int v;
-      bool dup;
-      do {
-        v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
-        dup = false;
-#pragma unroll
-        for (int j = 0; j < k; ++j) dup |= idx[j] == v;
-      } while (dup);
-      idx[k] = v;
-    }
-    double p[6] = {0, 0, 0, 0, 0, 0}, R[9];
-    lm_small(Q, q, idx, kMinSample, K, hyp_iters, p);
+    double p[6], R[9];
+    const double* src = hws + ((size_t)b * n_hyp + h) * 6;
+    for (int i = 0; i < 6; ++i) p[i] = src[i];
     const bool finite = isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]) && isfinite(p[3]) &&
                         isfinite(p[4]) && isfinite(p[5]);
     rodrigues(p, R);
@@ -917,22 +957,29 @@ extern "C" int slam_triangulate(const double* d_ptl, const double* d_ptr, const 
   return SLAM_OK;
 }
 
+extern "C" long long slam_pnp_workspace_len(int batch, int n_hyp) {
+  return (long long)batch * n_hyp * 6;
+}
+
 extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count,
                                int cap, int batch, const double* d_K, uint64_t seed, int item0,
                                int n_hyp, double reproj_thresh, int hyp_iters, int refine_iters,
                                double* d_rvec, double* d_tvec, int32_t* d_ninliers,
-                               uint8_t* d_mask, void* stream) {
+                               uint8_t* d_mask, double* d_ws, void* stream) {
   SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_pnp_ransac: bad shape");
   SLAM_REQUIRE(n_hyp >= 1 && n_hyp <= kMaxHyp, "slam_pnp_ransac: n_hyp in [1, %d]", kMaxHyp);
   SLAM_REQUIRE(hyp_iters >= 0 && refine_iters >= 0 && reproj_thresh > 0,
                "slam_pnp_ransac: bad iteration/threshold arguments");
   if (batch == 0) return SLAM_OK;
-  SLAM_REQUIRE(d_Q && d_q && d_count && d_K && d_rvec && d_tvec && d_ninliers && d_mask,
+  SLAM_REQUIRE(d_Q && d_q && d_count && d_K && d_rvec && d_tvec && d_ninliers && d_mask && d_ws,
                "slam_pnp_ransac: null pointer");
-  k_pnp<<<batch, kPnPWG, 0, slam::as_stream(stream)>>>(d_Q, d_q, d_count, cap, d_K, seed, item0,
-                                                      n_hyp, reproj_thresh, hyp_iters,
-                                                      refine_iters, d_rvec, d_tvec, d_ninliers,
-                                                      d_mask);
+  hipStream_t s = slam::as_stream(stream);
+  k_pnp_hyp<<<dim3(batch, (n_hyp + kHypLanes - 1) / kHypLanes), 64, 0, s>>>(
+      d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, hyp_iters, d_ws);
+  SLAM_LAUNCHED("k_pnp_hyp");
+  k_pnp<<<batch, kPnPWG, 0, s>>>(d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, reproj_thresh,
+                                 hyp_iters, refine_iters, d_rvec, d_tvec, d_ninliers, d_mask,
+                                 d_ws);
   SLAM_LAUNCHED("k_pnp");
   return SLAM_OK;
 }

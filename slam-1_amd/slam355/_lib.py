@@ -61,7 +61,8 @@ SIGNATURES = {
                              c_p],
     "slam_triangulate": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "slam_pnp_ransac": [c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int, c_double, c_int,
-                        c_int, c_p, c_p, c_p, c_p, c_p],
+                        c_int, c_p, c_p, c_p, c_p, c_p, c_p],
+    "slam_pnp_workspace_len": [c_int, c_int],
     "slam_pose_chain": [c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_vo_estimate_pose": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int,
                               c_int, c_int, c_p, c_p, c_p, c_p, c_p, c_size_t, c_p],
@@ -113,7 +114,7 @@ SIGNATURES = {
                             c_p, c_p],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
-            "slam_ba_chol_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}
+            "slam_ba_chol_len": ctypes.c_longlong, "slam_pnp_workspace_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}
 
 
 class SlamError(RuntimeError):

@@ -103,11 +103,24 @@ def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, **kw):
         mask = torch.zeros((B, max(cap, 1)), dtype=torch.uint8, device=dev)
     else:
         rvec, tvec, ninl, mask = out
+    ws = _pnp_ws(B, prm["n_hyp"], dev)
     _lib.call("slam_pnp_ransac", ptr(Q), ptr(q), ptr(count), cap, B, ptr(Kt.contiguous()),
               int(seed) & ((1 << 64) - 1), int(item0), prm["n_hyp"], float(prm["reproj_thresh"]),
               prm["hyp_iters"], prm["refine_iters"], ptr(rvec), ptr(tvec), ptr(ninl), ptr(mask),
-              stream_ptr(stream))
+              ptr(ws), stream_ptr(stream))
     return rvec, tvec, ninl, mask
+
+
+_PNP_WS: dict = {}
+
+
+def _pnp_ws(B, n_hyp, dev):
+    """Hypothesis-pose workspace of slam_pnp_ransac (cached per device, grown)."""
+    n = int(_lib.lib.slam_pnp_workspace_len(B, n_hyp))
+    ws = _PNP_WS.get(dev)
+    if ws is None or ws.numel() < n:
+        ws = _PNP_WS[dev] = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    return ws
 
 
 VO_DEFAULTS = dict(max_iter=100, lm_iters=20, early_stop=5)

@@ -14,7 +14,7 @@ import pytest
 from oracle import geometry as og
 
 
-def _scene(seed, n=400, outliers=0.2, noise=0.5):
+def _scene(seed, n=400, outliers=0.2, noise=0.5, large=False):
     from slam355.synthetic import StereoRig
 
     rig = StereoRig(1280, 720)
@@ -22,6 +22,11 @@ def _scene(seed, n=400, outliers=0.2, noise=0.5):
     Q = np.stack([rng.uniform(-10, 10, n), rng.uniform(-3, 3, n), rng.uniform(5, 60, n)], 1)
     r = np.array([0.002, 0.01, -0.003]) * (1 + seed % 3)
     t = np.array([0.02, -0.01, -1.0])
+    if large:  # loop-closure-sized motion (0.5 rad, 5 m) in the camera frame
+        r = np.array([0.1, 0.48, -0.12]) * (1 + 0.1 * (seed % 3))
+        t = np.array([3.0, -1.0, 3.5])
+        Xc = np.stack([rng.uniform(-12, 12, n), rng.uniform(-4, 4, n), rng.uniform(6, 60, n)], 1)
+        Q = (Xc - t) @ og.rodrigues(r)  # R^T (Xc - t): world points seen in front
     Xc = Q @ og.rodrigues(r).T + t
     q = Xc[:, :2] / Xc[:, 2:3] * rig.K[0, 0] + rig.K[:2, 2] + rng.normal(0, noise, (n, 2))
     k = int(outliers * n)
@@ -54,6 +59,31 @@ def test_oracle_pnp_recovers_pose_with_outliers():
     # deterministic
     rv2, tv2, n2, m2 = og.pnp_ransac(Q, q, rig.K, seed=3, item=7)
     assert np.array_equal(rv, rv2) and np.array_equal(tv, tv2) and n == n2
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_oracle_pnp_large_motion_epnp_seed(seed):
+    """0.5 rad / 5 m motion, 20 % outliers: hypotheses seeded by EPnP (the
+    RANSAC kernel OpenCV's solvePnPRansac uses for ITERATIVE) recover the pose."""
+    rig, Q, q, r, t = _scene(seed, n=300, large=True)
+    rv, tv, n, mask = og.pnp_ransac(Q, q, rig.K, seed=5, item=seed)
+    assert n >= 0.75 * len(Q)
+    assert np.allclose(rv, r, atol=2e-3) and np.allclose(tv, t, atol=5e-2)
+    assert mask[int(0.2 * len(Q)):].mean() > 0.95
+
+
+def test_oracle_epnp_exact_points():
+    rng = np.random.default_rng(3)
+    K = np.array([[716.8, 0, 640], [0, 716.8, 360], [0, 0, 1.0]])
+    for _ in range(20):
+        r, t = rng.normal(0, 0.6, 3), rng.normal(0, 4, 3)
+        Xc = np.stack([rng.uniform(-10, 10, 5), rng.uniform(-5, 5, 5), rng.uniform(5, 60, 5)], 1)
+        Xw = (Xc - t) @ og.rodrigues(r)
+        uv = Xc[:, :2] / Xc[:, 2:3] * 716.8 + [640, 360]
+        p = og.epnp(Xw, uv, K)
+        assert p is not None
+        assert np.allclose(og.rodrigues(p[:3]), og.rodrigues(r), atol=1e-9)
+        assert np.allclose(p[3:], t, atol=1e-8 * (1 + np.abs(t).max()))
 
 
 def test_oracle_pnp_guard_and_pose_sign_convention():
@@ -138,6 +168,31 @@ def test_gpu_pnp_matches_oracle():
             continue
         assert np.array_equal(mask[i, :L].astype(bool), emask), i
         assert np.allclose(rv[i], erv, rtol=0, atol=1e-8) and np.allclose(tv[i], etv, atol=1e-8), i
+
+
+@pytest.mark.gpu
+def test_gpu_pnp_large_motion_matches_oracle():
+    """EPnP-seeded hypotheses on the GPU (k_pnp_hyp) equal the oracle's on
+    loop-closure-sized motion with outliers: counts, masks, pose 1e-8."""
+    import torch
+    from slam355 import geometry
+
+    B = 3
+    scenes = [_scene(s, n=250, large=True) for s in range(B)]
+    cap = 250
+    Q = np.stack([s[1] for s in scenes])
+    q = np.stack([s[2] for s in scenes])
+    cnt = np.full(B, cap, np.int32)
+    K = scenes[0][0].K
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    rv, tv, n, mask = geometry.pnp_ransac(T(Q), T(q), T(cnt), K, seed=4, item0=20)
+    rv, tv, n, mask = rv.cpu().numpy(), tv.cpu().numpy(), n.cpu().numpy(), mask.cpu().numpy()
+    for i in range(B):
+        erv, etv, en, emask = og.pnp_ransac(Q[i], q[i], K, seed=4, item=20 + i)
+        assert n[i] == en, i
+        assert np.array_equal(mask[i].astype(bool), emask), i
+        assert np.allclose(rv[i], erv, rtol=0, atol=1e-8) and np.allclose(tv[i], etv, atol=1e-8), i
+        assert np.allclose(tv[i], scenes[i][4], atol=5e-2)
 
 
 @pytest.mark.gpu
