@@ -11,7 +11,7 @@
  *                   eigen-decomposition (cyclic Jacobi) of the scatter matrix;
  *   barycentric     alpha = [c1-c0 c2-c0 c3-c0]^-1 (X - c0) (3x3 cofactors);
  *   M (2n x 12)     the projection rows; the 4 eigenvectors of M^T M with the
- *                   smallest eigenvalues (cyclic Jacobi, 12x12);
+ *                   smallest eigenvalues (Jacobi, round-robin pair ordering);
  *   betas           OpenCV's three approximations (L columns {B11 B12 B13 B14},
  *                   {B11 B12 B22}, {B11 B12 B22 B13 B23}) by normal equations,
  *                   each refined by 5 Gauss-Newton steps (normal equations);
@@ -70,6 +70,76 @@ static inline void ep_jacobi(double* A, int n, double* V) {
           V[k * n + q] = s * vkp + c * vkq;
         }
       }
+  }
+}
+
+/* the 12x12 eigen-decomposition of M^T M: Jacobi with the round-robin
+ * (tournament) ordering -- 11 rounds of 6 disjoint pairs per sweep, the pair
+ * (p, q) of slot i in round r being {a[i], a[11 - i]} with a[0] = 0 and
+ * a[1..11] = 1..11 rotated by r.  In a round, every pair's (c, s) comes from
+ * the matrix at the round start (c = 1, s = 0 when a_pq = 0); then all column
+ * rotations (A J), then all row rotations (J^T (A J)), then V J; sweeps stop
+ * when the off-diagonal mass is below 1e-24 of the diagonal mass.  The rounds
+ * are what a GPU group executes in parallel (csrc/epnp.hpp). */
+static inline void ep_pairs12(int r, int pp[6], int qq[6]) {
+  int a[12];
+  a[0] = 0;
+  for (int i = 1; i < 12; ++i) a[i] = 1 + (i - 1 + r) % 11;
+  for (int i = 0; i < 6; ++i) {
+    const int x = a[i], y = a[11 - i];
+    pp[i] = x < y ? x : y;
+    qq[i] = x < y ? y : x;
+  }
+}
+
+static inline void ep_rot_cs(double app, double aqq, double apq, double* c, double* s) {
+  if (apq == 0.0) {
+    *c = 1.0;
+    *s = 0.0;
+    return;
+  }
+  const double th = (aqq - app) / (2.0 * apq);
+  const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+  *c = 1.0 / sqrt(t * t + 1.0);
+  *s = t * *c;
+}
+
+static inline void ep_jacobi12_par(double* A, double* V) {
+  const int n = 12;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) V[i * n + j] = i == j ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double off = 0.0, dia = 0.0;
+    for (int i = 0; i < n; ++i) {
+      dia += A[i * n + i] * A[i * n + i];
+      for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+    }
+    if (!(off > 1e-24 * dia)) break;
+    for (int r = 0; r < 11; ++r) {
+      int pp[6], qq[6];
+      double c[6], s[6];
+      ep_pairs12(r, pp, qq);
+      for (int i = 0; i < 6; ++i)
+        ep_rot_cs(A[pp[i] * n + pp[i]], A[qq[i] * n + qq[i]], A[pp[i] * n + qq[i]], &c[i], &s[i]);
+      for (int i = 0; i < 6; ++i)
+        for (int k = 0; k < n; ++k) {  /* columns */
+          const double akp = A[k * n + pp[i]], akq = A[k * n + qq[i]];
+          A[k * n + pp[i]] = c[i] * akp - s[i] * akq;
+          A[k * n + qq[i]] = s[i] * akp + c[i] * akq;
+        }
+      for (int i = 0; i < 6; ++i)
+        for (int k = 0; k < n; ++k) {  /* rows */
+          const double apk = A[pp[i] * n + k], aqk = A[qq[i] * n + k];
+          A[pp[i] * n + k] = c[i] * apk - s[i] * aqk;
+          A[qq[i] * n + k] = s[i] * apk + c[i] * aqk;
+        }
+      for (int i = 0; i < 6; ++i)
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + pp[i]], vkq = V[k * n + qq[i]];
+          V[k * n + pp[i]] = c[i] * vkp - s[i] * vkq;
+          V[k * n + qq[i]] = s[i] * vkp + c[i] * vkq;
+        }
+    }
   }
 }
 
@@ -268,7 +338,7 @@ static inline int epnp(const double* pw, const double* uv, int n, double fx, dou
     for (int r = 0; r < 12; ++r)
       for (int c = 0; c < 12; ++c) MtM[12 * r + c] += m1[r] * m1[c] + m2[r] * m2[c];
   }
-  ep_jacobi(MtM, 12, V12);
+  ep_jacobi12_par(MtM, V12);
   /* the 4 eigenvectors of the smallest eigenvalues, ascending: v[0] smallest */
   int o12[12];
   for (int i = 0; i < 12; ++i) o12[i] = i;

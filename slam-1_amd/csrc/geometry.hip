@@ -276,56 +276,87 @@ __device__ __forceinline__ double wave_allsum(double v) {
   return v;
 }
 
-// PnP-RANSAC hypotheses: kHypLanes per workgroup, one per lane.  Sample h of
-// pair b: 5 distinct indices from splitmix64(seed, item0 + b, h); EPnP on the
-// sample (OpenCV's RANSAC kernel for SOLVEPNP_ITERATIVE), then hyp_iters LM
-// steps on the same 5 points from that pose (a degenerate sample starts LM at
-// r = t = 0).  Poses -> ws [b][h][6].  The 12x12 EPnP matrices sit in LDS.
-constexpr int kHypLanes = 16;
+// PnP-RANSAC hypotheses: kHypGroups per one-wave workgroup, a 16-lane group
+// each.  Sample h of pair b: 5 distinct indices from splitmix64(seed,
+// item0 + b, h); EPnP on the sample (OpenCV's RANSAC kernel for
+// SOLVEPNP_ITERATIVE; csrc/epnp.hpp group form: M^T M rows and the 12x12
+// Jacobi on 12 lanes, the three beta approximations on 3 lanes), then
+// hyp_iters LM steps on the same 5 points from that pose (a degenerate sample
+// starts LM at r = t = 0).  Poses -> ws [b][h][6].
+constexpr int kHypGroups = 4;  // hypotheses per one-wave workgroup (16 lanes each)
+#ifdef SLAM_PNPH_TRACE
+__device__ unsigned long long g_pnph[8];
+#define PNPH_T(i) do { if (threadIdx.x == 0 && blockIdx.x == 3 && blockIdx.y == 5) g_pnph[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PNPH_T(i) (void)0
+#endif
 __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
                                                 const double* __restrict__ qall,
                                                 const int32_t* __restrict__ count, int cap,
                                                 const double* __restrict__ Kp, uint64_t seed,
                                                 int item0, int n_hyp, int hyp_iters,
                                                 double* __restrict__ ws) {
-  __shared__ double mt[kHypLanes][144];
-  __shared__ double v12[kHypLanes][144];
+  __shared__ slam_epnp::EpGroup grp[kHypGroups];
+  __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
+  __shared__ int sidx[kHypGroups][kMinSample];
   const int b = blockIdx.x, t = threadIdx.x;
-  const int h = blockIdx.y * kHypLanes + t;
+  const int g = t >> 4, k = t & 15;
+  const int h = blockIdx.y * kHypGroups + g;
   const int L = min(max(count[b], 0), cap);
-  if (L < kMinSample || t >= kHypLanes || h >= n_hyp) return;
+  if (L < kMinSample) return;  // uniform over the workgroup
+  const bool live = h < n_hyp;
   const double* Q = Qall + (size_t)b * cap * 3;
   const double* q = qall + (size_t)b * cap * 2;
   const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
-  uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
-               ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
-  int idx[kMinSample];
-#pragma unroll
-  for (int k = 0; k < kMinSample; ++k) {
-    int v;
-    bool dup;
-    do {
-      v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
-      dup = false;
-#pragma unroll
-      for (int j = 0; j < k; ++j) dup |= idx[j] == v;
-    } while (dup);
-    idx[k] = v;
-  }
-  double p[6] = {0, 0, 0, 0, 0, 0};
-  {
-    double pw[3 * kMinSample], uv[2 * kMinSample];
-#pragma unroll
-    for (int k = 0; k < kMinSample; ++k) {
-      for (int d = 0; d < 3; ++d) pw[3 * k + d] = Q[3 * idx[k] + d];
-      for (int d = 0; d < 2; ++d) uv[2 * k + d] = q[2 * idx[k] + d];
+  slam_epnp::EpGroup& G = grp[g];
+  PNPH_T(0);
+  // sample h: 5 distinct indices from splitmix64(seed, item0 + b, h)
+  if (k == 0 && live) {
+    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
+                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+    int idx[kMinSample];
+    for (int kk = 0; kk < kMinSample; ++kk) {
+      int v;
+      bool dup;
+      do {
+        v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
+        dup = false;
+        for (int j = 0; j < kk; ++j) dup |= idx[j] == v;
+      } while (dup);
+      idx[kk] = v;
+      sidx[g][kk] = v;
+      for (int d = 0; d < 3; ++d) spw[g][3 * kk + d] = Q[3 * v + d];
+      for (int d = 0; d < 2; ++d) suv[g][2 * kk + d] = q[2 * v + d];
     }
-    if (!slam_epnp::epnp(pw, uv, kMinSample, K.fx, K.fy, K.cx, K.cy, p, mt[t], v12[t]))
-      for (int i = 0; i < 6; ++i) p[i] = 0.0;
+    G.flag = slam_epnp::ep_bary<kMinSample>(spw[g], G);
   }
-  lm_small(Q, q, idx, kMinSample, K, hyp_iters, p);
-  double* o = ws + ((size_t)b * n_hyp + h) * 6;
-  for (int i = 0; i < 6; ++i) o[i] = p[i];
+  __syncthreads();
+  PNPH_T(1);
+  bool ok = live && G.flag != 0;
+  if (ok && k < 12) slam_epnp::ep_mtm_row<kMinSample>(k, suv[g], K.fx, K.fy, K.cx, K.cy, G);
+  __syncthreads();
+  PNPH_T(2);
+  slam_epnp::ep_jacobi12_group(G, k, ok);
+  PNPH_T(3);
+#ifdef SLAM_PNPH_TRACE
+  if (threadIdx.x == 0 && blockIdx.x == 3 && blockIdx.y == 5) g_pnph[7] = (unsigned long long)G.offdia[1];
+#endif
+  if (ok && k == 0) slam_epnp::ep_lrho(G);
+  __syncthreads();
+  PNPH_T(4);
+  if (ok && k < 3) slam_epnp::ep_approx<kMinSample>(k, spw[g], suv[g], K.fx, K.fy, K.cx, K.cy, G);
+  __syncthreads();
+  PNPH_T(5);
+  if (k == 0 && live) {
+    double p[6] = {0, 0, 0, 0, 0, 0};
+    if (!(ok && slam_epnp::ep_choose(G, p)))
+      for (int i = 0; i < 6; ++i) p[i] = 0.0;
+    // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0)
+    lm_small(Q, q, sidx[g], kMinSample, K, hyp_iters, p);
+    double* o = ws + ((size_t)b * n_hyp + h) * 6;
+    for (int i = 0; i < 6; ++i) o[i] = p[i];
+  }
+  PNPH_T(6);
 }
 
 // One workgroup per frame pair:
@@ -974,7 +1005,7 @@ extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32
   SLAM_REQUIRE(d_Q && d_q && d_count && d_K && d_rvec && d_tvec && d_ninliers && d_mask && d_ws,
                "slam_pnp_ransac: null pointer");
   hipStream_t s = slam::as_stream(stream);
-  k_pnp_hyp<<<dim3(batch, (n_hyp + kHypLanes - 1) / kHypLanes), 64, 0, s>>>(
+  k_pnp_hyp<<<dim3(batch, (n_hyp + kHypGroups - 1) / kHypGroups), 64, 0, s>>>(
       d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, hyp_iters, d_ws);
   SLAM_LAUNCHED("k_pnp_hyp");
   k_pnp<<<batch, kPnPWG, 0, s>>>(d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, reproj_thresh,
@@ -1053,3 +1084,11 @@ extern "C" int slam_pose_chain(const double* d_rvec, const double* d_tvec,
   SLAM_LAUNCHED("k_pose_chain");
   return SLAM_OK;
 }
+
+#ifdef SLAM_PNPH_TRACE
+extern "C" int slam_pnph_trace(unsigned long long* out) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pnph), 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif
