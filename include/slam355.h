@@ -185,6 +185,12 @@ int slam_vo_residuals(const double* d_dof, const double* d_q1, const double* d_q
                       const double* d_Q1, const double* d_Q2, const int32_t* d_count, int cap,
                       int batch, const double* d_P, double* d_res, void* stream);
 
+/* relative_to_abs3DPoints (Point3D.py:22-30) for a tracking batch:
+ * d_abs[b][i] = (pose_b [X;1])[:3] / (pose_b [X;1])[3] for i < d_count[b];
+ * d_rel, d_abs [batch][cap][3] f64, d_poses [batch][16] f64 row-major. */
+int slam_rel_to_abs(const double* d_rel, const int32_t* d_count, int cap, int batch,
+                    const double* d_poses, double* d_abs, void* stream);
+
 /* ------------------------------------------------------------------------
  * Map association: appendKeyPoints (keypoint.py:101-122).
  *

@@ -124,6 +124,35 @@ extern "C" int slam_map_workspace_bytes(int max_queries, int map_cap, size_t* by
   return SLAM_OK;
 }
 
+namespace {
+
+// relative_to_abs3DPoints (Point3D.py:22-30) for a tracking batch: abs =
+// (pose_b [X; 1])[:3] / (pose_b [X; 1])[3], one thread per point.
+__global__ void k_rel_to_abs(const double* __restrict__ rel, const int32_t* __restrict__ count,
+                             int cap, const double* __restrict__ poses, double* __restrict__ out) {
+  const int b = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= min(max(count[b], 0), cap)) return;
+  const double* P = poses + 16 * (size_t)b;
+  const double* X = rel + ((size_t)b * cap + i) * 3;
+  double a[4];
+  for (int r = 0; r < 4; ++r) a[r] = P[4 * r] * X[0] + P[4 * r + 1] * X[1] + P[4 * r + 2] * X[2] + P[4 * r + 3];
+  double* o = out + ((size_t)b * cap + i) * 3;
+  for (int r = 0; r < 3; ++r) o[r] = a[r] / a[3];
+}
+
+}  // namespace
+
+extern "C" int slam_rel_to_abs(const double* d_rel, const int32_t* d_count, int cap, int batch,
+                               const double* d_poses, double* d_abs, void* stream) {
+  SLAM_REQUIRE(cap >= 0 && batch >= 0, "slam_rel_to_abs: bad shape");
+  if (cap == 0 || batch == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_rel && d_count && d_poses && d_abs, "slam_rel_to_abs: null pointer");
+  k_rel_to_abs<<<dim3((cap + 255) / 256, batch), 256, 0, slam::as_stream(stream)>>>(
+      d_rel, d_count, cap, d_poses, d_abs);
+  SLAM_LAUNCHED("k_rel_to_abs");
+  return SLAM_OK;
+}
+
 extern "C" int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int M_bound,
                                   const double* d_abs, const double* d_rel, const double* d_pts2d,
                                   const int32_t* d_n, int N, double threshold, int frame_index,

@@ -195,3 +195,50 @@ def chain_poses(pose0, rvecs, tvecs, ninl, T_prev=None):
         pose = pose @ T
         poses.append(pose)
     return np.stack(poses), T
+
+
+class LocalMap:
+    """The mapping half of main.py's loop (:120-127) on the device, for
+    tracked batches: each pair's temporally matched 3-D points (Q1, relative to
+    frame i) go to the world frame with the NEW pose (relative_to_abs3DPoints,
+    Point3D.py:22-30: k_rel_to_abs), then appendKeyPoints (keypoint.py:101-122:
+    MapStore, exact nearest landmark + the |rel|-scaled gate) adds the rows
+    [frame i, landmark, u, v] (u, v = the left image coordinates at time i).
+    `problem()` returns the BA problem export_data / read_bal_data would give
+    (XXXport_files.problem_from_map), ready for slam355.ba.BAProblem."""
+
+    def __init__(self, tracker: Tracker, threshold=0.01, capacity=1 << 16):
+        from .mapping import MapStore
+
+        self.trk = tracker
+        self.threshold = float(threshold)
+        B, cap = tracker.B, tracker.cap
+        self.store = MapStore(capacity=capacity, max_queries=cap)
+        d = tracker.dev
+        self.abs = torch.zeros((B, cap, 3), dtype=torch.float64, device=d)
+        self.rows = torch.zeros((B, cap, 4), dtype=torch.float64, device=d)
+        self._rows_host = []
+        self.poses = [np.eye(4)]  # camera_frames (main.py:52-54)
+
+    def add(self, frame0: int):
+        """Map the batch Tracker.track(frame0) just tracked (same stream)."""
+        t = self.trk
+        st = t.stream
+        _lib.call("slam_rel_to_abs", ptr(t.Q1), ptr(t.t_cnt), t.cap, t.B, ptr(t.poses),
+                  ptr(self.abs), stream_ptr(st))
+        for b in range(t.B):
+            self.store.append(self.abs[b], t.Q1[b], t.q1[b], frame0 + b, self.threshold,
+                              count=t.t_cnt[b:b + 1], rows=self.rows[b], stream=st)
+        cnt = t.t_cnt.cpu().numpy()
+        rows = self.rows.cpu().numpy()
+        self._rows_host += [rows[b, :cnt[b]] for b in range(t.B)]
+        self.poses += list(t.poses.cpu().numpy())
+
+    def optimization_matrix(self):
+        return np.vstack(self._rows_host) if self._rows_host else np.empty((0, 4))
+
+    def problem(self, P_left):
+        from .XXXport_files import problem_from_map
+
+        return problem_from_map(self.optimization_matrix(), self.poses,
+                                self.store.points().cpu().numpy(), P_left)

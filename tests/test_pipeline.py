@@ -170,3 +170,65 @@ def test_gpu_tracker_raises_on_orb_overflow(corridor):
     trk.imgs.copy_(torch.from_numpy(np.stack([L[0], L[1], R[0]])))
     trk.track(0)
     trk.check()  # flag was reset; a normal batch passes
+
+
+@pytest.mark.gpu
+def test_gpu_tracked_frames_feed_local_ba(corridor):
+    """tracking and local BA as one pipeline.  3 tracked pairs
+    -> device pose chain -> relative_to_abs3DPoints -> appendKeyPoints on the
+    device map -> the export_data / read_bal_data problem -> BAProblem LM;
+    equals the oracle chain (track_pair, the reference pose rule,
+    oracle.mapping.append_keypoints, oracle Schur LM) step by step."""
+    import torch
+    from oracle import ba as oba
+    from oracle import geometry as og
+    from oracle import mapping as omap
+    from slam355 import XXXport_files as xp
+    from slam355.ba import BAProblem
+    from slam355.pipeline import LocalMap, Tracker
+
+    L, R, poses, rig = corridor
+    B = 3
+    trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=6)
+    lm = LocalMap(trk)
+    trk.imgs.copy_(torch.from_numpy(np.concatenate([L[:B + 1], R[:B]])))
+    trk.track(0)
+    lm.add(0)
+    # oracle chain (main.py:79-127)
+    cache = {}
+    Qs = np.empty((0, 3))
+    om_rows = []
+    pose, T = np.eye(4), np.eye(4)
+    frames = [np.eye(4)]
+    for i in range(B):
+        e = op.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, max_kp=64, seed=6, frame=i,
+                          orb_cache=cache)
+        if e["n_pnp"] >= 0:
+            T, _, _ = og.pose_matrix_from_pnp(e["rvec"], e["tvec"])
+        pose = pose @ T
+        frames.append(pose)
+        absP = og.relative_to_abs3DPoints(e["Q1"], pose)
+        Qs, rows = omap.append_keypoints(Qs, absP, 0.01, e["q1"], i, e["Q1"])
+        om_rows.append(rows)
+    om = np.vstack(om_rows)
+    got = lm.optimization_matrix()
+    assert got.shape == om.shape
+    assert np.array_equal(got[:, [0, 1]], om[:, [0, 1]]) and np.array_equal(got[:, 2:], om[:, 2:])
+    assert np.allclose(np.stack(lm.poses), np.stack(frames), rtol=0, atol=1e-10)
+    gQ = lm.store.points().cpu().numpy()
+    assert gQ.shape == Qs.shape and np.allclose(gQ, Qs, rtol=1e-12, atol=1e-12)
+    cams, pts, ci, pi, qs = lm.problem(rig.P_l)
+    ec, ep_, eci, epi, eqs = xp.problem_from_map(om, frames, Qs, rig.P_l)
+    assert np.allclose(cams, ec, atol=1e-10) and np.array_equal(ci, eci) and np.array_equal(pi, epi)
+    prob = BAProblem(cams, pts, ci, pi, qs)
+    st = oba.LMState(1e-4)
+    oc, opt = ec.copy(), ep_.copy()
+    pairs = oba._obs_pairs(eci, epi)
+    for it in range(3):
+        prob.iterate(1)
+        oc, opt, info = oba.lm_iteration_schur(oc, opt, eci, epi, eqs, st, pairs)
+        s = prob.state()
+        assert bool(s["ACCEPTED"]) == bool(info["accepted"]), it
+        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-8 * abs(info["cost_new"]), it
+        gc, gp = prob.params()
+        assert np.allclose(gc, oc, rtol=1e-6, atol=1e-8), it
