@@ -39,9 +39,10 @@ __device__ __forceinline__ void ep_jacobi(double* A, double* V) {
       for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
     }
     if (!(off > 1e-30 * dia)) break;
-    #pragma unroll (n <= 4 ? 4 : 1)
+    constexpr int kUnroll = n <= 4 ? 4 : 1;
+    #pragma unroll kUnroll
     for (int p = 0; p < n - 1; ++p)
-      #pragma unroll (n <= 4 ? 4 : 1)
+      #pragma unroll kUnroll
       for (int q = p + 1; q < n; ++q) {
         const double apq = A[p * n + q];
         if (apq == 0.0) continue;

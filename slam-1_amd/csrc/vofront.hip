@@ -1455,6 +1455,7 @@ extern "C" int slam_vo_right_qs_3d(const float* d_tp1, const float* d_tp2, const
       d_tp1, d_tp2, d_cnt, cap, d_disp, disp1_stride, disp2_offset, H, W, min_disp, max_disp, d_Pl,
       d_Pr, d_q1l, d_q1r, d_q2l, d_q2r, d_Q1, d_Q2, d_q1l64, d_q2l64, d_Q1_64, d_Q2_64, d_count);
   SLAM_LAUNCHED("k_vo_right_qs_3d");
+  if (cap == 0) return SLAM_OK;  // counts written as 0; nothing to triangulate
   // calc_3d over the kept points: one thread per point (count read on the device)
   const dim3 grid((cap + kBS - 1) / kBS, batch);
   k_triangulate_f32<<<grid, kBS, 0, s>>>(d_q1l, d_q1r, d_count, cap, d_Pl, d_Pr, d_Q1, d_Q1_64);

@@ -77,6 +77,13 @@ def lk_track(prev: LKPyramids, nxt: LKPyramids, pts: torch.Tensor, npts: torch.T
     B, cap, ps = pts.shape
     if prev.der is None:
         raise ValueError("prev pyramids were built without derivatives")
+    for name, pyr, i0 in (("prev", prev, prev0), ("next", nxt, next0)):
+        last = i0 + (B - 1) * pair_stride
+        if B > 0 and not (0 <= i0 < pyr.pyr.shape[0] and 0 <= last < pyr.pyr.shape[0]):
+            raise IndexError(f"lk_track: {name} images {i0}..{last} outside the "
+                             f"{pyr.pyr.shape[0]} pyramids")
+    if (prev.H, prev.W, prev.win, prev.max_level) != (nxt.H, nxt.W, nxt.win, nxt.max_level):
+        raise ValueError("lk_track: prev/next pyramids have different layouts")
     dev = pts.device
     out = torch.empty((B, cap, 2), dtype=torch.float32, device=dev)
     st = torch.empty((B, cap), dtype=torch.uint8, device=dev)
@@ -125,7 +132,12 @@ def right_qs_3d(tp1, tp2, cnt, disp_f32, P_l, P_r, disp1_index=0, disp2_offset=1
     and disp_f32[disp1_index + b + disp2_offset]."""
     B, cap, _ = tp1.shape
     dev = tp1.device
-    _, H, W = disp_f32.shape
+    nd, H, W = disp_f32.shape
+    if B > 0:
+        first, last = disp1_index, disp1_index + B - 1 + disp2_offset
+        if not (0 <= first < nd and 0 <= disp1_index + disp2_offset and last < nd):
+            raise IndexError(f"right_qs_3d: disparity maps {first}..{last} outside the "
+                             f"{nd} maps")
     f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
     d = lambda *s: torch.empty(s, dtype=torch.float64, device=dev) if f64 else None  # noqa: E731
     o = dict(q1_l=f(B, cap, 2), q1_r=f(B, cap, 2), q2_l=f(B, cap, 2), q2_r=f(B, cap, 2),

@@ -124,6 +124,41 @@ def _dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+def test_wrappers_reject_image_indices_outside_the_tensors():
+    """lk_track / right_qs_3d check their image ranges on the host before any
+    launch (the kernels index prev0 + b*pair_stride and disp1_index + b +
+    disp2_offset directly)."""
+    import types
+
+    import torch
+
+    from slam355 import vofront
+
+    B, cap = 3, 8
+    pts = torch.zeros((B, cap, 2))
+    npts = torch.zeros(B, dtype=torch.int32)
+    pyr = types.SimpleNamespace(pyr=torch.zeros((4, 16)), der=torch.zeros((4, 16, 2)), H=8, W=8,
+                                win=5, max_level=1)
+    with pytest.raises(IndexError):  # next images 1..3 exist, 2..4 do not
+        vofront.lk_track(pyr, pyr, pts, npts, prev0=0, next0=2)
+    with pytest.raises(IndexError):
+        vofront.lk_track(pyr, pyr, pts, npts, prev0=0, next0=1, pair_stride=2)
+    with pytest.raises(IndexError):
+        vofront.lk_track(pyr, pyr, pts, npts, prev0=-1, next0=0)
+    other = types.SimpleNamespace(**{**vars(pyr), "W": 16})
+    with pytest.raises(ValueError):
+        vofront.lk_track(pyr, other, pts, npts, prev0=0, next0=1)
+    disp = torch.zeros((4, 8, 8))
+    with pytest.raises(IndexError):  # pairs 0..2 read maps 0..3; offset 2 reads map 4
+        vofront.right_qs_3d(pts, pts, npts, disp, np.eye(3, 4), np.eye(3, 4), disp2_offset=2)
+    with pytest.raises(IndexError):
+        vofront.right_qs_3d(pts, pts, npts, disp, np.eye(3, 4), np.eye(3, 4), disp1_index=1,
+                            disp2_offset=1)
+    with pytest.raises(IndexError):
+        vofront.right_qs_3d(pts, pts, npts, disp, np.eye(3, 4), np.eye(3, 4), disp1_index=1,
+                            disp2_offset=-2)
+
+
 @pytest.mark.gpu
 def test_gpu_fast_tiles_bit_exact():
     import torch
