@@ -39,6 +39,8 @@ _SIGS = {
     "oracle_orb_umax": [_p],
     "oracle_gauss_blur7": [_p, _i, _i, _i, _p, _i],
     "oracle_gauss_kernel7": [_p],
+    "oracle_harris": [_p, _i, _i, _i],
+    "oracle_ic_angle": [_p, _i, _i, _i, _p],
     "oracle_orb_tiles": [_p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i],
     "oracle_orb_tiles_batch": [_p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p],
 }

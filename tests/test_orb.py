@@ -152,6 +152,142 @@ def test_oracle_orb_tiles_structure():
     assert np.array_equal(kp, kp2) and np.array_equal(desc, d2)
 
 
+def test_fast_atan2_known_answers():
+    """cv::fastAtan2 (degrees, [0, 360)): exact on the axes, and the 7th-order
+    polynomial stays within 0.01 deg of atan2 on a 0.25-deg sweep (OpenCV's
+    documented bound is 0.3 deg)."""
+    f = oracle.lib().oracle_fast_atan2
+    assert f(0.0, 1.0) == 0.0 and f(1.0, 0.0) == 90.0
+    assert f(0.0, -1.0) == 180.0 and f(-1.0, 0.0) == 270.0
+    # on the diagonal the polynomial gives (p1 + p3 + p5 + p7) * 180/pi = 44.99046
+    d = (0.9997878412794807 - 0.3258083974640975 + 0.1555786518463281 - 0.04432655554792128)
+    assert abs(f(1.0, 1.0) - d * 180 / np.pi) < 1e-4 and abs(f(1.0, 1.0) - 45.0) < 0.0096
+    assert abs(f(-3.0, -3.0) - (180 + d * 180 / np.pi)) < 1e-4
+    worst = 0.0
+    for deg in np.arange(0, 360, 0.25):
+        y, x = np.float32(np.sin(np.radians(deg)) * 37), np.float32(np.cos(np.radians(deg)) * 37)
+        a = f(float(y), float(x))
+        assert 0.0 <= a < 360.0 or (a == 360.0 and deg > 359)
+        ref = np.degrees(np.arctan2(float(y), float(x))) % 360.0
+        worst = max(worst, min(abs(a - ref), 360 - abs(a - ref)))
+    assert worst < 0.01
+
+
+def test_ic_umax_table():
+    """The circular-patch row extents of ORB's IC angle for HALF_PATCH_SIZE 15
+    (the table every ORB implementation derives: cvRound(sqrt(15^2 - v^2)) with
+    the symmetric fix-up above 15/sqrt(2))."""
+    assert oracle.orb_umax()[:16].tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9,
+                                               8, 6, 3]
+
+
+def _np_ic_angle(img, x, y):
+    um = oracle.orb_umax()
+    m10 = m01 = 0
+    for v in range(-15, 16):
+        d = um[abs(v)]
+        row = img[y + v, x - d:x + d + 1].astype(np.int64)
+        u = np.arange(-d, d + 1)
+        m10 += int((u * row).sum())
+        m01 += int(v * row.sum())
+    return m01, m10
+
+
+@pytest.mark.parametrize("theta", [0, 30, 90, 135, 200, 270, 333])
+def test_ic_angle_known_answers(theta):
+    """Intensity centroid of a linear ramp along theta points along theta; the
+    oracle's moments equal an independent NumPy sum over the same disc."""
+    h = w = 64
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    t = np.radians(theta)
+    img = np.clip(np.rint(128 + 3.0 * ((xx - 32) * np.cos(t) + (yy - 32) * np.sin(t))), 0,
+                  255).astype(np.uint8)
+    a = oracle.lib().oracle_ic_angle(_p(img), w, 32, 32, _p(oracle.orb_umax()))
+    m01, m10 = _np_ic_angle(img, 32, 32)
+    ref = np.degrees(np.arctan2(m01, m10)) % 360.0
+    assert min(abs(a - ref), 360 - abs(a - ref)) < 0.01
+    assert min(abs(a - theta), 360 - abs(a - theta)) < 0.5  # rounding of the ramp
+    if theta % 90 == 0:
+        assert a == float(theta)
+
+
+def _p(a):
+    return np.ascontiguousarray(a).ctypes.data_as(__import__("ctypes").c_void_p)
+
+
+def _np_harris(img, x0, y0):
+    im = img.astype(np.int64)
+    a = b = c = 0
+    for y in range(y0 - 3, y0 + 4):
+        for x in range(x0 - 3, x0 + 4):
+            ix = 2 * (im[y, x + 1] - im[y, x - 1]) + (im[y - 1, x + 1] - im[y - 1, x - 1]) + \
+                (im[y + 1, x + 1] - im[y + 1, x - 1])
+            iy = 2 * (im[y + 1, x] - im[y - 1, x]) + (im[y + 1, x - 1] - im[y - 1, x - 1]) + \
+                (im[y + 1, x + 1] - im[y - 1, x + 1])
+            a, b, c = a + ix * ix, b + iy * iy, c + ix * iy
+    f = np.float32
+    scale = f(1) / (f(4 * 7) * f(255))
+    ssss = scale * scale * scale * scale
+    fa, fb, fc = f(a), f(b), f(c)
+    return (fa * fb - fc * fc - f(0.04) * (fa + fb) * (fa + fb)) * ssss
+
+
+def test_harris_response_known_answers():
+    """cv::ORB HarrisResponses (7x7 block, Sobel 3x3, k = 0.04, scale
+    1/(4*7*255), applied as scale^4): an ideal 255-step edge through the block
+    gives exactly -0.04 (2/7)^2 (a = 14 * 1020^2 = 2/7 of (4*7*255)^2, b = c = 0),
+    a flat block 0, a quadrant corner > 0; contrast x2 gives response x16; and
+    every value equals an independent NumPy restatement bit for bit."""
+    h = oracle.lib().oracle_harris
+    img = np.zeros((32, 32), np.uint8)
+    img[:, 16:] = 255
+    r = h(_p(img), 32, 16, 16)
+    assert abs(r - (-0.04 * (2 / 7) ** 2)) < 1e-7
+    assert np.float32(r) == _np_harris(img, 16, 16)
+    assert h(_p(np.full((32, 32), 77, np.uint8)), 32, 16, 16) == 0.0
+    q = np.zeros((32, 32), np.uint8)
+    q[16:, 16:] = 60
+    r1 = h(_p(q), 32, 16, 16)
+    assert r1 > 0 and np.float32(r1) == _np_harris(q, 16, 16)
+    r2 = h(_p(q * 2), 32, 16, 16)
+    assert abs(r2 / r1 - 16.0) < 1e-5
+    rng = np.random.default_rng(3)
+    n = rng.integers(0, 256, (32, 32), dtype=np.uint8)
+    for (x, y) in ((5, 5), (16, 9), (26, 26)):
+        assert np.float32(h(_p(n), 32, x, y)) == _np_harris(n, x, y)
+
+
+def _dot_grid(H=200, W=200, step=10, values=(255,)):
+    img = np.zeros((H, W), np.uint8)
+    for j, y in enumerate(range(5, H - 5, step)):
+        for i, x in enumerate(range(5, W - 5, step)):
+            img[y, x] = values[(i + j) % len(values)]
+    return img
+
+
+def test_retain_best_keeps_boundary_ties():
+    """KeyPointsFilter::retainBest keeps every keypoint whose response equals
+    the n-th best (nth_element + partition on >=): identical isolated dots all
+    survive both cuts (FAST score to 2n, Harris to n) at octave 0 though the
+    level budget is 4; with two contrasts the cut falls between the groups and
+    every dot of the stronger group survives."""
+    nl = oracle.orb_level_budget(20)
+    assert nl[0] == 4
+    img = _dot_grid()
+    inside = [(x, y) for y in range(5, 195, 10) for x in range(5, 195, 10)
+              if 31 <= x < 169 and 31 <= y < 169]
+    kp, octv, _ = oracle.orb_tiles(img, 20, 1, 0, 0)
+    k0 = kp[octv == 0]
+    assert len(k0) == len(inside) > nl[0]
+    assert len(set(k0[:, 4].tolist())) == 1  # one Harris response shared by all
+    assert sorted(map(tuple, k0[:, :2].astype(int).tolist())) == sorted(inside)
+    img2 = _dot_grid(values=(255, 128))
+    kp, octv, _ = oracle.orb_tiles(img2, 20, 1, 0, 0)
+    k0 = kp[octv == 0]
+    strong = [(x, y) for (x, y) in inside if img2[y, x] == 255]
+    assert sorted(map(tuple, k0[:, :2].astype(int).tolist())) == sorted(strong)
+
+
 # ----------------------------------------------------------------------------- GPU
 def _gpu_vs_oracle(imgs, max_kp, **tiling):
     import torch
@@ -210,6 +346,18 @@ def test_gpu_orb_extraction_detect_single_patch():
     assert len(kps) == len(ek)
     assert np.array_equal(np.array([k.pt for k in kps], np.float32), ek[:, :2])
     assert np.array_equal(des, ed)
+
+
+@pytest.mark.gpu
+def test_gpu_orb_retain_best_ties_match_oracle():
+    from slam355 import orb
+
+    for img in (_dot_grid(), _dot_grid(values=(255, 128))):
+        kps, des = orb.orb_extraction_detect(img, 20)
+        ek, eo, ed = oracle.orb_tiles(img, 20, 1, 0, 0)
+        assert len(kps) == len(ek) > 20
+        assert np.array_equal(np.array([k.pt for k in kps], np.float32), ek[:, :2])
+        assert np.array_equal(des, ed)
 
 
 @pytest.mark.gpu
