@@ -228,12 +228,21 @@ def test_gpu_tracked_frames_feed_local_ba(corridor):
         # every iteration starts the oracle from the device's parameters, so a
         # rounding difference of one (ill-conditioned, real-track) solve does not
         # compound into the next; lambda follows the same accept/reject chain
+        c0 = None
         if it:
             oc, opt = prob.params()
+            c0 = prob.state()["COST"]
         prob.iterate(1)
         oc, opt, info = oba.lm_iteration_schur(oc, opt, eci, epi, eqs, st, pairs)
         s = prob.state()
         assert bool(s["ACCEPTED"]) == bool(info["accepted"]), it
-        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-8 * abs(info["cost_new"]), it
+        if c0 is not None:  # the same parameters: the cost itself agrees to rounding
+            assert abs(c0 - info["cost"]) <= 1e-12 * info["cost"], it
+        # the step: the map holds mismatched far points (cost ~1e8), so the
+        # reduced system is ill-conditioned and the new cost agrees to ~1e-8
+        # of itself; the achieved decrease agrees to 1e-5 of the decrease
+        assert abs(s["COST_NEW"] - info["cost_new"]) <= 1e-7 * abs(info["cost_new"]), it
+        dec = info["cost"] - info["cost_new"]
+        assert abs((info["cost"] - s["COST_NEW"]) - dec) <= 1e-5 * abs(dec), it
         gc, gp = prob.params()
         assert np.allclose(gc, oc, rtol=1e-6, atol=1e-8), it
