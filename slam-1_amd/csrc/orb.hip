@@ -849,7 +849,9 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
   g->lds_s = g->lds_l + al(g->list_cap * (int)sizeof(KP));
   g->lds_m = g->lds_s + al(g->list_cap * 8);
   g->lds_total = g->lds_m + (256 + 16) * 4;
-  g->tcap = max_kp + 64;
+  // slots per tile: the budget plus 64 for retainBest's boundary ties; a single
+  // patch (orb_extraction_detect) gets room for a full tie list on every level
+  g->tcap = g->n_tiles == 1 ? kNLev * g->list_cap : max_kp + 64;
   SLAM_REQUIRE(g->lds_total <= 160 * 1024,
                "slam_orb: patch %dx%d needs %d B of LDS (> 160 KiB)", pw, ph, g->lds_total);
   return SLAM_OK;
