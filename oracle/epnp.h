@@ -109,10 +109,13 @@ static inline void ep_jacobi12_par(double* A, double* V) {
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) V[i * n + j] = i == j ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 40; ++sweep) {
+    /* off-diagonal mass summed row by row (row partials, then the rows in order) */
     double off = 0.0, dia = 0.0;
     for (int i = 0; i < n; ++i) {
       dia += A[i * n + i] * A[i * n + i];
-      for (int j = i + 1; j < n; ++j) off += A[i * n + j] * A[i * n + j];
+      double o = 0.0;
+      for (int j = i + 1; j < n; ++j) o += A[i * n + j] * A[i * n + j];
+      off += o;
     }
     if (!(off > 1e-24 * dia)) break;
     for (int r = 0; r < 11; ++r) {

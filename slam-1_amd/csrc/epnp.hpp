@@ -239,6 +239,7 @@ __device__ inline void ep_rvec(const double R[9], double r[3]) {
 // approximations on lanes 0..2, the rest on lane 0.  Every value is computed
 // with the operations of oracle/epnp.h in the same order.  The caller's
 // workgroup is one wave, so __syncthreads() is a cheap wave-level fence.
+constexpr int kJld = 13;  // row stride of the Jacobi buffers (odd: rows on distinct banks)
 struct EpGroup {         // LDS of one group
   double A[144], V[144]; // M^T M (destroyed: eigenvalues on the diagonal), eigenvectors
   double alph[4 * EPNP_MAXN];
@@ -247,8 +248,15 @@ struct EpGroup {         // LDS of one group
   double cw[4][3];
   double res[3][8];      // per approximation: err, p[6], valid
   double offdia[2];
+  double B[2][12 * kJld];  // Jacobi: A ping-pong (round r reads B[cur], writes B[cur ^ 1])
+  double cs[12];           // Jacobi: the round's (c, s) of the 6 pairs
+  double part[24];         // Jacobi: per-row diagonal / off-diagonal squares
+  double pad[27];
   int flag;              // 0: degenerate, 1: ok; Jacobi: 1 while sweeping
 };
+// consecutive groups 32 banks apart, so lanes 0..15 and 16..31 of a wave
+// (one ds_read_b64 bank group) never collide on the stride-13 rows
+static_assert(sizeof(EpGroup) % 256 == 128, "EpGroup stride must be 128 mod 256 bytes");
 
 // control points and barycentric weights (lane 0); returns 0 when degenerate
 template <int n>
@@ -329,11 +337,15 @@ __device__ __forceinline__ void ep_mtm_row(int r, const double* uv, double fx, d
 }
 
 // The 12x12 Jacobi of M^T M with the round-robin ordering of
-// oracle/epnp.h ep_jacobi12_par: lanes k < 12 of the group own row k of A and
-// V.  Per round: every lane derives the 6 pairs' (c, s) from the round-start
-// matrix, rotates its row's column pairs (A J, V J), then the two lanes of a
-// pair rotate their rows (J^T (A J)).  The wave loops until every group has
-// met its own stopping rule.
+// oracle/epnp.h ep_jacobi12_par: lanes k < 12 of the group own row k of A
+// (in LDS, ping-pong B[cur] -> B[cur ^ 1]) and of V (in registers).  Per
+// round: lanes 0..5 derive pair k's (c, s) from the round-start matrix and
+// publish them; then every lane rotates the column pairs of its own row AND
+// of its partner's row (A J, the same operations the partner performs), and
+// forms its new row from the two (J^T (A J)) -- one exchange through LDS
+// per round, rounds fully unrolled so the pair columns are compile-time
+// register indices.  The wave loops until every group has met its own
+// stopping rule; a finished group keeps copying its rows.
 __device__ __forceinline__ void ep_pairs12(int r, int pp[6], int qq[6]) {
   int a[12];
   a[0] = 0;
@@ -358,22 +370,101 @@ __device__ __forceinline__ void ep_rot_cs(double app, double aqq, double apq, do
   s = z ? 0.0 : t * cc;
 }
 
+template <int r>
+__device__ __forceinline__ void ep_jacobi_round(EpGroup& G, int k, int kr, bool act, int cur,
+                                                double (&vr)[12]) {
+  constexpr int n = 12, ld = kJld;
+  const double* A0 = G.B[cur];
+  double* A1 = G.B[cur ^ 1];
+  int pp[6], qq[6];
+  ep_pairs12(r, pp, qq);
+  if (k < 6) {
+    // pair k of this round (a[k], a[11 - k] of ep_pairs12)
+    const int x = k == 0 ? 0 : 1 + (k - 1 + r) % 11, y = 1 + (10 - k + r) % 11;
+    const int p = x < y ? x : y, q = x < y ? y : x;
+    double c, s;
+    ep_rot_cs(A0[p * ld + p], A0[q * ld + q], A0[p * ld + q], c, s);
+    G.cs[k] = c;
+    G.cs[6 + k] = s;
+  }
+  __syncthreads();
+  double c[6], s[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    c[i] = G.cs[i];
+    s[i] = G.cs[6 + i];
+  }
+  int partner = kr;
+  double ck = 1.0, sk = 0.0;
+  bool isp = true;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    if (pp[i] == kr) { partner = qq[i]; ck = c[i]; sk = s[i]; isp = true; }
+    if (qq[i] == kr) { partner = pp[i]; ck = c[i]; sk = s[i]; isp = false; }
+  }
+  double row[n], prow[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    row[j] = A0[kr * ld + j];
+    prow[j] = A0[partner * ld + j];
+  }
+  // columns (A J, V J): the pairs are disjoint, any order
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int P = pp[i], Q = qq[i];
+    const double akp = row[P], akq = row[Q];
+    row[P] = c[i] * akp - s[i] * akq;
+    row[Q] = s[i] * akp + c[i] * akq;
+    const double bkp = prow[P], bkq = prow[Q];
+    prow[P] = c[i] * bkp - s[i] * bkq;
+    prow[Q] = s[i] * bkp + c[i] * bkq;
+    const double vkp = vr[P], vkq = vr[Q];
+    const double wp = c[i] * vkp - s[i] * vkq, wq = s[i] * vkp + c[i] * vkq;
+    vr[P] = act ? wp : vkp;
+    vr[Q] = act ? wq : vkq;
+  }
+  // rows (J^T (A J)) of the pair holding k; a finished group copies its row
+  if (k < n) {
+#pragma unroll
+    for (int j = 0; j < n; ++j) {
+      const double nv = isp ? ck * row[j] - sk * prow[j] : sk * prow[j] + ck * row[j];
+      A1[k * ld + j] = act ? nv : A0[k * ld + j];
+    }
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ void ep_jacobi12_group(EpGroup& G, int k, bool live) {
-  constexpr int n = 12;
+  constexpr int n = 12, ld = kJld;
   const bool own = k < n;
   const int kr = own ? k : 0;
+  double vr[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) vr[j] = kr == j ? 1.0 : 0.0;
   if (own) {
 #pragma unroll
-    for (int j = 0; j < n; ++j) G.V[k * n + j] = k == j ? 1.0 : 0.0;
+    for (int j = 0; j < n; ++j) G.B[0][k * ld + j] = G.A[k * n + j];
   }
   if (k == 0) G.flag = live ? 1 : 0;
   __syncthreads();
+  int cur = 0;
   for (int sweep = 0; sweep < 40; ++sweep) {
+    // off / dia by rows: row k's squares, then lane 0 sums the rows in order
+    if (own) {
+      const double* Ar = G.B[cur] + k * ld;
+      double o = 0.0;
+#pragma unroll
+      for (int j = 1; j < n; ++j)
+        if (j > k) o += Ar[j] * Ar[j];
+      G.part[k] = Ar[k] * Ar[k];
+      G.part[n + k] = o;
+    }
+    __syncthreads();
     if (k == 0 && G.flag) {
       double off = 0.0, dia = 0.0;
       for (int i = 0; i < n; ++i) {
-        dia += G.A[i * n + i] * G.A[i * n + i];
-        for (int j = i + 1; j < n; ++j) off += G.A[i * n + j] * G.A[i * n + j];
+        dia += G.part[i];
+        off += G.part[n + i];
       }
       if (!(off > 1e-24 * dia)) G.flag = 0;
     }
@@ -383,59 +474,27 @@ __device__ __forceinline__ void ep_jacobi12_group(EpGroup& G, int k, bool live) 
 #ifdef SLAM_PNPH_TRACE
     if (threadIdx.x == 0) G.offdia[1] = sweep + 1;
 #endif
-    for (int r = 0; r < 11; ++r) {
-      int pp[6], qq[6];
-      double c[6], s[6];
-      ep_pairs12(r, pp, qq);
+    ep_jacobi_round<0>(G, k, kr, act, cur, vr);
+    ep_jacobi_round<1>(G, k, kr, act, cur ^ 1, vr);
+    ep_jacobi_round<2>(G, k, kr, act, cur, vr);
+    ep_jacobi_round<3>(G, k, kr, act, cur ^ 1, vr);
+    ep_jacobi_round<4>(G, k, kr, act, cur, vr);
+    ep_jacobi_round<5>(G, k, kr, act, cur ^ 1, vr);
+    ep_jacobi_round<6>(G, k, kr, act, cur, vr);
+    ep_jacobi_round<7>(G, k, kr, act, cur ^ 1, vr);
+    ep_jacobi_round<8>(G, k, kr, act, cur, vr);
+    ep_jacobi_round<9>(G, k, kr, act, cur ^ 1, vr);
+    ep_jacobi_round<10>(G, k, kr, act, cur, vr);
+    cur ^= 1;  // 11 rounds: odd
+  }
+  if (own) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
-        ep_rot_cs(G.A[pp[i] * n + pp[i]], G.A[qq[i] * n + qq[i]], G.A[pp[i] * n + qq[i]], c[i], s[i]);
-      // columns of row k (pairs are disjoint: any order)
-      double np[6], nq[6], wp[6], wq[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double akp = G.A[kr * n + pp[i]], akq = G.A[kr * n + qq[i]];
-        const double vkp = G.V[kr * n + pp[i]], vkq = G.V[kr * n + qq[i]];
-        np[i] = c[i] * akp - s[i] * akq;
-        nq[i] = s[i] * akp + c[i] * akq;
-        wp[i] = c[i] * vkp - s[i] * vkq;
-        wq[i] = s[i] * vkp + c[i] * vkq;
-      }
-      __syncthreads();  // every lane has read the round-start values
-      if (act) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          G.A[k * n + pp[i]] = np[i];
-          G.A[k * n + qq[i]] = nq[i];
-          G.V[k * n + pp[i]] = wp[i];
-          G.V[k * n + qq[i]] = wq[i];
-        }
-      }
-      __syncthreads();
-      // rows: the pair (p, q) holding k, from both column-rotated rows
-      int partner = kr;
-      double ck = 1.0, sk = 0.0;
-      bool isp = true;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        if (pp[i] == kr) { partner = qq[i]; ck = c[i]; sk = s[i]; isp = true; }
-        if (qq[i] == kr) { partner = pp[i]; ck = c[i]; sk = s[i]; isp = false; }
-      }
-      double row[n], prow[n];
-#pragma unroll
-      for (int j = 0; j < n; ++j) {
-        row[j] = G.A[kr * n + j];
-        prow[j] = G.A[partner * n + j];
-      }
-      __syncthreads();
-      if (act) {
-#pragma unroll
-        for (int j = 0; j < n; ++j)
-          G.A[k * n + j] = isp ? ck * row[j] - sk * prow[j] : sk * prow[j] + ck * row[j];
-      }
-      __syncthreads();
+    for (int j = 0; j < n; ++j) {
+      G.A[k * n + j] = G.B[cur][k * ld + j];
+      G.V[k * n + j] = vr[j];
     }
   }
+  __syncthreads();
 }
 
 // eigen ordering, the 4 null vectors, L and rho (lane 0)
