@@ -384,30 +384,38 @@ __device__ __forceinline__ void ep_jacobi_round(EpGroup& G, int k, int kr, bool 
     const int p = x < y ? x : y, q = x < y ? y : x;
     double c, s;
     ep_rot_cs(A0[p * ld + p], A0[q * ld + q], A0[p * ld + q], c, s);
-    G.cs[k] = c;
-    G.cs[6 + k] = s;
+    G.cs[2 * k] = c;
+    G.cs[2 * k + 1] = s;
   }
-  __syncthreads();
-  double c[6], s[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    c[i] = G.cs[i];
-    s[i] = G.cs[6 + i];
-  }
-  int partner = kr;
-  double ck = 1.0, sk = 0.0;
-  bool isp = true;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    if (pp[i] == kr) { partner = qq[i]; ck = c[i]; sk = s[i]; isp = true; }
-    if (qq[i] == kr) { partner = pp[i]; ck = c[i]; sk = s[i]; isp = false; }
-  }
+  // the pair holding row kr (closed form of ep_pairs12: kr sits at position
+  // pos of a[], its partner at 11 - pos) -- no per-pair compare chains
+  const int pos = kr == 0 ? 0 : (kr + 10 - r % 11) % 11 + 1;
+  const int ppos = 11 - pos;
+  const int partner = ppos == 0 ? 0 : 1 + (ppos - 1 + r) % 11;
+  const int pi = pos < ppos ? pos : ppos;
+  const bool isp = kr < partner;
   double row[n], prow[n];
 #pragma unroll
   for (int j = 0; j < n; ++j) {
     row[j] = A0[kr * ld + j];
     prow[j] = A0[partner * ld + j];
   }
+  __syncthreads();
+  double c[6], s[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    c[i] = G.cs[2 * i];
+    s[i] = G.cs[2 * i + 1];
+  }
+  double ck = c[0], sk = s[0];
+#pragma unroll
+  for (int i = 1; i < 6; ++i) {
+    ck = pi == i ? c[i] : ck;
+    sk = pi == i ? s[i] : sk;
+  }
+  double out[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) out[j] = row[j];
   // columns (A J, V J): the pairs are disjoint, any order
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -424,12 +432,14 @@ __device__ __forceinline__ void ep_jacobi_round(EpGroup& G, int k, int kr, bool 
     vr[Q] = act ? wq : vkq;
   }
   // rows (J^T (A J)) of the pair holding k; a finished group copies its row
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    const double nv = isp ? ck * row[j] - sk * prow[j] : sk * prow[j] + ck * row[j];
+    out[j] = act ? nv : out[j];
+  }
   if (k < n) {
 #pragma unroll
-    for (int j = 0; j < n; ++j) {
-      const double nv = isp ? ck * row[j] - sk * prow[j] : sk * prow[j] + ck * row[j];
-      A1[k * ld + j] = act ? nv : A0[k * ld + j];
-    }
+    for (int j = 0; j < n; ++j) A1[k * ld + j] = out[j];
   }
   __syncthreads();
 }

@@ -351,8 +351,10 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
     double p[6] = {0, 0, 0, 0, 0, 0};
     if (!(ok && slam_epnp::ep_choose(G, p)))
       for (int i = 0; i < 6; ++i) p[i] = 0.0;
-    // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0)
-    lm_small(Q, q, sidx[g], kMinSample, K, hyp_iters, p);
+    // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0),
+    // read from the sample's LDS copy (spw / suv hold Q[idx], q[idx] in order)
+    const int seq[kMinSample] = {0, 1, 2, 3, 4};
+    lm_small(spw[g], suv[g], seq, kMinSample, K, hyp_iters, p);
     double* o = ws + ((size_t)b * n_hyp + h) * 6;
     for (int i = 0; i < 6; ++i) o[i] = p[i];
   }
