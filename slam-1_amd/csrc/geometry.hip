@@ -226,40 +226,74 @@ constexpr int kMinSample = 5;
 constexpr int kPnPWG = 256;
 constexpr int kMaxHyp = 256;
 
-// LM on a handful of points entirely in one thread (hypothesis generation).
-__device__ void lm_small(const double* Q, const double* q, const int* idx, int n, const Cam& K,
-                         int iters, double p[6]) {
+// Levenberg-Marquardt on a hypothesis' sample (oracle/geometry.c lm with idx)
+// on a 16-lane group (lane k = lane & 15): lanes s < n evaluate
+// point s (residual, Jacobian) and publish its per-(s, a) terms; lane j < 28
+// sums term j over (s, a) in the oracle's order (H, g, cost), every lane then
+// reads the 28 sums and runs the identical 6x6 solve and decision, so p and
+// lam stay replicated.  Bitwise the operations of oracle lm.
+// t: LDS [2 * kMinSample][28], sums: LDS [28 + kMinSample].  Every lane of the
+// group's wave must call it (wave-level __syncthreads inside).
+__device__ void lm_group(const double* Q, const double* q, int n, const Cam& K, int iters,
+                         double p[6], int k, double (*t)[28], double* sums) {
   double lam = 1e-3;
-  double R[9];
   for (int it = 0; it < iters; ++it) {
+    double R[9];
     rodrigues(p, R);
-    double H[21] = {0}, g[6] = {0}, cost = 0.0;
-    for (int s = 0; s < n; ++s) {
+    if (k < n) {
       double r[2], J[2][6];
-      pnp_residual<true>(p, R, Q + 3 * idx[s], q + 2 * idx[s], K, r, J);
+      pnp_residual<true>(p, R, Q + 3 * k, q + 2 * k, K, r, J);
+#pragma unroll
       for (int a = 0; a < 2; ++a) {
-        int k = 0;
-        for (int i = 0; i < 6; ++i) {
-          for (int j = 0; j <= i; ++j) H[k++] += J[a][i] * J[a][j];
-          g[i] += J[a][i] * r[a];
+        double* o = t[2 * k + a];
+        int m = 0;
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+#pragma unroll
+          for (int v = 0; v <= u; ++v) o[m++] = J[a][u] * J[a][v];
+          o[21 + u] = J[a][u] * r[a];
         }
-        cost += r[a] * r[a];
+        o[27] = r[a] * r[a];
       }
     }
+    __syncthreads();
+    // lane k sums terms k and k + 16 (< 28)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int j = k + 16 * e;
+      if (j < 28) {
+        double acc = 0.0;
+        for (int sa = 0; sa < 2 * n; ++sa) acc += t[sa][j];
+        sums[j] = acc;
+      }
+    }
+    __syncthreads();
+    double H[21], g[6];
+#pragma unroll
+    for (int i = 0; i < 21; ++i) H[i] = sums[i];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) g[i] = sums[21 + i];
+    const double cost = sums[27];
     double d[6], pn[6];
-    if (!solve6(H, g, lam, d)) {
+    const bool ok = solve6(H, g, lam, d);
+    if (!ok) {
       lam = fmin(lam * 10.0, 1e12);
+      __syncthreads();  // sums are rewritten next iteration
       continue;
     }
     for (int i = 0; i < 6; ++i) pn[i] = p[i] + d[i];
     double Rn[9];
     rodrigues(pn, Rn);
-    double cn = 0.0;
-    for (int s = 0; s < n; ++s) {
+    __syncthreads();  // every lane has read sums
+    if (k < n) {
       double r[2], J[2][6];
-      pnp_residual<false>(pn, Rn, Q + 3 * idx[s], q + 2 * idx[s], K, r, J);
-      cn += r[0] * r[0] + r[1] * r[1];
+      pnp_residual<false>(pn, Rn, Q + 3 * k, q + 2 * k, K, r, J);
+      sums[k] = r[0] * r[0] + r[1] * r[1];
     }
+    __syncthreads();
+    double cn = 0.0;
+    for (int s2 = 0; s2 < n; ++s2) cn += sums[s2];
+    __syncthreads();
     if (cn < cost) {
       for (int i = 0; i < 6; ++i) p[i] = pn[i];
       lam = fmax(lam * 0.1, 1e-12);
@@ -299,6 +333,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
   __shared__ slam_epnp::EpGroup grp[kHypGroups];
   __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
   __shared__ int sidx[kHypGroups][kMinSample];
+  __shared__ double lmt[kHypGroups][2 * kMinSample][28], lms[kHypGroups][28 + kMinSample];
   const int b = blockIdx.x, t = threadIdx.x;
   const int g = t >> 4, k = t & 15;
   const int h = blockIdx.y * kHypGroups + g;
@@ -347,14 +382,20 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
   if (ok && k < 3) slam_epnp::ep_approx<kMinSample>(k, spw[g], suv[g], K.fx, K.fy, K.cx, K.cy, G);
   __syncthreads();
   PNPH_T(5);
-  if (k == 0 && live) {
+  if (k == 0) {
     double p[6] = {0, 0, 0, 0, 0, 0};
     if (!(ok && slam_epnp::ep_choose(G, p)))
       for (int i = 0; i < 6; ++i) p[i] = 0.0;
-    // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0),
-    // read from the sample's LDS copy (spw / suv hold Q[idx], q[idx] in order)
-    const int seq[kMinSample] = {0, 1, 2, 3, 4};
-    lm_small(spw[g], suv[g], seq, kMinSample, K, hyp_iters, p);
+    for (int i = 0; i < 6; ++i) G.res[0][i] = p[i];  // the EPnP pose to the group
+  }
+  __syncthreads();
+  // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0),
+  // read from the sample's LDS copy (spw / suv hold Q[idx], q[idx] in order);
+  // a dead group (h >= n_hyp) runs along on its zeros and writes nothing
+  double p[6];
+  for (int i = 0; i < 6; ++i) p[i] = G.res[0][i];
+  lm_group(spw[g], suv[g], kMinSample, K, hyp_iters, p, k, lmt[g], lms[g]);
+  if (k == 0 && live) {
     double* o = ws + ((size_t)b * n_hyp + h) * 6;
     for (int i = 0; i < 6; ++i) o[i] = p[i];
   }
