@@ -224,6 +224,9 @@ def run_tracking(args, world, rank):
     L_np, R_np = L[:3].cpu().numpy(), R[:2].cpu().numpy()
     del L, R
     trk_stream = masked_stream(args.track_cus) if args.track_cus else None
+    if trk_stream is None and args.priority == "track":
+        trk_stream = torch.cuda.Stream(priority=-1)
+        trk_stream.destroy = lambda: None
     trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
                   stream=trk_stream)
     rng = np.random.default_rng(2000 + rank)
@@ -237,9 +240,11 @@ def run_tracking(args, world, rank):
     stream = torch.cuda.current_stream()
     # local mapping (BA) on its own HIP stream, concurrent with tracking, unless --ba-serial
     # (high priority: its short latency-bound kernels go ahead of queued ORB tiles)
-    ba_stream = stream if args.ba_serial else torch.cuda.Stream(priority=-1)
+    ba_stream = (stream if args.ba_serial else
+                 torch.cuda.Stream(priority=-1 if args.priority == "ba" else 0))
     with torch.cuda.stream(ba_stream):
-        ba = BABatch([BAProblem(*w, stream=ba_stream) for w in windows], stream=ba_stream)
+        ba = BABatch([BAProblem(*w, stream=ba_stream, chunks_per_wg=args.chunks_per_wg)
+                      for w in windows], stream=ba_stream)
     torch.cuda.synchronize()
     tstream = trk_stream if trk_stream is not None else stream
     all_poses = {}
@@ -250,6 +255,8 @@ def run_tracking(args, world, rank):
         ev.record(s)
         return ev
 
+    ba_done = [None]
+
     def step(marks):
         with torch.cuda.stream(tstream):
             tracked_step(marks)
@@ -259,10 +266,14 @@ def run_tracking(args, world, rank):
         imgs, win = feed.next(tstream)
         if win == 0:  # a new pass over the sequence starts at frame 0
             trk.reset_chain()
+        if args.ba_overlap == "after-orb" and ba_done[0] is not None:
+            tstream.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
         trk.track(win * B, imgs=imgs, marks=tmarks)
         feed.release(tstream)
         if marks is None and args.keep_poses:
             all_poses[win] = trk.poses.clone()
+        if args.ba_overlap == "after-orb":
+            ba_stream.wait_event(trk.orb_event)
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
         with torch.cuda.stream(ba_stream):
             # the step's local-BA windows, all advanced together (one launch set
@@ -272,6 +283,8 @@ def run_tracking(args, world, rank):
                 ba.iterate(args.ba_iters)
             else:
                 ba.iterate_graphed(args.ba_iters, with_restore=True)
+        if args.ba_overlap == "after-orb":
+            ba_done[0] = ev_on(ba_stream)
         if marks is not None:
             bmarks.append(("local_ba", ev_on(ba_stream)))
             marks["track"], marks["ba"] = tmarks, bmarks
@@ -340,6 +353,8 @@ def run_tracking(args, world, rank):
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
                    "h2d_upload": "in timed region (pinned, copy stream, double-buffered)",
                    "local_ba_stream": "serial" if args.ba_serial else "concurrent",
+                   "high_priority_stream": args.priority,
+                   "ba_overlap": args.ba_overlap,
                    "tracking_cus": args.track_cus or "all"},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
@@ -743,6 +758,11 @@ def main():
                     help="--workload ba: C5 loop-closure global BA (500 KF x 200k pts)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the LM iterations eagerly instead of replaying a HIP graph")
+    ap.add_argument("--ba-overlap", default="full", choices=["full", "after-orb"],
+                    help="tracking workload: local BA overlaps all of tracking (full), or "
+                         "starts after the batch's ORB and holds the next batch's ORB back")
+    ap.add_argument("--priority", default="ba", choices=["ba", "track", "equal"],
+                    help="which stream gets the high HIP stream priority (tracking workload)")
     ap.add_argument("--ba-serial", action="store_true",
                     help="run local BA on the tracking stream (no overlap)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -344,6 +344,13 @@ typedef struct slam_ba_problem {
                                    chunk (= pt_ptr[grp_ptr]); required in both modes */
   const int32_t* chk_cptr;      /* [n_grps][8] start of each camera's run in chk_cobs */
   const int32_t* bslot_ab;      /* [n_bslots] camera pair a | b << 8 (a < b) of a block slot */
+  /* Optional level schedule of the tiled solve (9C > 120), built by
+   * slam355/ba.py tl_schedule: tiles renumbered by nested dissection, columns
+   * grouped by elimination-tree level.  Null: one panel step per tile column.
+   * tl_sched is the device copy, tl_sched_host the same array in host memory
+   * (the launcher reads the level counts from it); both or neither. */
+  const int32_t* tl_sched;
+  const int32_t* tl_sched_host;
 } slam_ba_problem;
 
 /* Problems per batched launch (slam_ba_iterate_batch splits larger batches). */

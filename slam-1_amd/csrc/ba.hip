@@ -1901,6 +1901,260 @@ __global__ __launch_bounds__(1024) void k_tl_epilogue(slam_ba_problem p) {
                  EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
 }
 
+// ---------------------------------------------------------------- level-scheduled tiled solve
+// The same tile factor with the columns grouped by elimination-tree level
+// (slam355/ba.py tl_schedule: tiles renumbered by nested dissection of the
+// tile graph, symbolic structure on the host).  Per level: k_tl2_panel (WG per
+// (k, I) of every column k of the level: the diagonal WG stores L_kk^-1 and
+// y_k = L_kk^-1 b_k, the others L_Ik = A_Ik L_kk^-T), then k_tl2_update (WG
+// per target tile (I, J) of the level: A_IJ -= sum_k L_Ik L_Jk^T on the f64
+// matrix cores, and for I = J also b_I -= sum_k L_Ik y_k -- the sums over the
+// level's columns inside one WG, no atomics).  k_tl2_back walks the levels in
+// reverse: x_k = L_kk^-T (y_k - sum_I L_Ik^T x_I) over the ancestors I; then
+// k_tl2_unperm moves x back to the camera order (into the y region, which the
+// epilogue reads).  A banded window of T tiles runs ~log2 T levels instead of
+// T panel steps (C4: 4 levels for 9 tiles; C5: 8 for 71).
+__device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) {
+  return sched[sched[2] + (r >> 6)] * kTB + (r & 63);
+}
+
+// Zero the lower tiles (identity on the padded rows' diagonal), b in the new order.
+__global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p) {
+  lm_wave_priority();
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const int32_t* S = p.tl_sched;
+  const int idx = blockIdx.x;
+  int I = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
+  while ((I + 1) * (I + 2) / 2 <= idx) ++I;
+  while (I * (I + 1) / 2 > idx) --I;
+  const int J = idx - I * (I + 1) / 2;
+  double* A = p.chol + L.a;
+  const int oldI = S[S[3] + I];  // padded rows live in the old last tile
+  for (int e = threadIdx.x; e < kTB * kTB; e += kTlWG) {
+    const int i = I * kTB + (e >> 6), j = J * kTB + (e & 63);
+    A[(size_t)i * L.N + j] = (i == j && oldI * kTB + (e >> 6) >= n) ? 1.0 : 0.0;
+  }
+  if (I == J && threadIdx.x < kTB) {
+    const int r = oldI * kTB + threadIdx.x;  // old row landing at new row I*64 + t
+    p.chol[L.b + I * kTB + threadIdx.x] =
+        r < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
+  }
+  if (idx == 0 && threadIdx.x == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 0;
+}
+
+// One WG per packed block: its values at their renumbered positions (lower
+// tiles, full symmetric inside diagonal tiles), camera damping on the diagonal.
+__global__ __launch_bounds__(128) void k_tl2_scatter(slam_ba_problem p) {
+  lm_wave_priority();
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const int32_t* S = p.tl_sched;
+  const int blk = blockIdx.x, t = threadIdx.x;
+  if (t >= 81) return;
+  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
+  const double* vec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
+  const int i = t / 9, j = t - 9 * (t / 9);
+  const int r = 9 * c1 + i, c = 9 * c2 + j;  // element (r, c) of S
+  double v = p.sys[(size_t)blk * 81 + t];
+  if (r == c) v += p.state[SLAM_BA_ST_LAMBDA] * clampd(vec[2 * n + r]);
+  double* A = p.chol + L.a;
+  const int rn = tl_new_row(S, r), cn = tl_new_row(S, c);
+  const int tr = rn / kTB, tc = cn / kTB;
+  if (tr >= tc) A[(size_t)rn * L.N + cn] = v;
+  if (c1 != c2 && tc >= tr) A[(size_t)cn * L.N + rn] = v;
+}
+
+__global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_tl2_panel(slam_ba_problem p, int eoff) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int32_t* S = p.tl_sched;
+  const int k = S[eoff + 2 * blockIdx.x], I = S[eoff + 2 * blockIdx.x + 1];
+  __shared__ double VX[2 * kTB * kTB];
+  double* Vf = VX;                        // L_kk^-1, fragment order
+  __shared__ double Xf[kTB * kTB];        // A_Ik, fragment order
+  __shared__ int okf;
+  double* A = p.chol + L.a;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double* Akk = A + (size_t)k * kTB * L.N + k * kTB;
+  double* AIk = A + (size_t)I * kTB * L.N + k * kTB;
+  if (I > k && w >= 2) tile_to_frag(AIk, L.N, Xf, w - 2, 2);
+  double x[kTB];
+  double* Mb = VX;
+  double* Xb = VX + kTB * kMS;
+  double* Tb = Xb + 10 * 16 * kBS17;
+  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf);
+  if (w == 1) {
+    const int cb16 = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < kTB; ++m)
+      x[m] = (m >> 4) >= cb16 ? Xb[blk_id(m >> 4, cb16) * 16 * kBS17 + (m & 15) * kBS17 + (lane & 15)]
+                              : 0.0;
+  }
+  __syncthreads();  // VX is reused below
+  if (w == 1) {
+    if (I == k) {
+      const double bc = p.chol[L.b + k * kTB + lane];
+      double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) Vkk[m * kTB + lane] = x[m];
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) Vf[m * kTB + lane] = x[m] * bc;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      double y = 0.0;
+      for (int c = 0; c < kTB; ++c) y += Vf[lane * kTB + ((c + lane) & 63)];
+      p.chol[L.y + k * kTB + lane] = y;
+      if (!ok && lane == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 1;
+    } else {
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) Vf[frag_idx(m, lane)] = x[m];
+    }
+  }
+  if (I == k || !ok) return;
+  __syncthreads();
+  d4 acc[4];
+  gemm_xyT(Xf, Vf, acc);  // L_Ik = A_Ik (L_kk^-1)^T
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+      AIk[(size_t)row * L.N + col] = acc[s2][r];
+    }
+}
+
+__global__ __launch_bounds__(kTlWG) void k_tl2_update(slam_ba_problem p, int eoff) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int32_t* S = p.tl_sched;
+  const int32_t* e = S + eoff + 4 * blockIdx.x;
+  const int I = e[0], J = e[1], ko = e[2], kc = e[3];
+  __shared__ double Xf[kTB * kTB], Yf[kTB * kTB];
+  __shared__ double part[4][kTB];
+  double* A = p.chol + L.a;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  d4 acc[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+  double bs = 0.0;  // thread (w, lane): sum over k of row lane's part [16w, 16w + 16) of L_Ik y_k
+  for (int q = 0; q < kc; ++q) {
+    const int k = S[ko + q];
+    const double* LIk = A + (size_t)I * kTB * L.N + k * kTB;
+    tile_to_frag(LIk, L.N, Xf);
+    if (I != J) tile_to_frag(A + (size_t)J * kTB * L.N + k * kTB, L.N, Yf);
+    if (I == J) {
+      const double* yk = p.chol + L.y + k * kTB;
+      for (int m = 16 * w; m < 16 * w + 16; ++m)
+        bs = __builtin_fma(LIk[(size_t)lane * L.N + m], yk[m], bs);
+    }
+    __syncthreads();
+    const double* Y = I == J ? Xf : Yf;
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+      const double a = Xf[((w * 16 + kk) << 6) + lane];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+        acc[s2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Y[((s2 * 16 + kk) << 6) + lane], acc[s2],
+                                                       0, 0, 0);
+    }
+    __syncthreads();  // Xf / Yf reloaded next k
+  }
+  double* AIJ = A + (size_t)I * kTB * L.N + J * kTB;
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+      AIJ[(size_t)row * L.N + col] -= acc[s2][r];
+    }
+  if (I == J) {
+    part[w][lane] = bs;
+    __syncthreads();
+    if (t < kTB)
+      p.chol[L.b + I * kTB + t] -= ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+  }
+}
+
+// x_k = L_kk^-T (y_k - sum_I L_Ik^T x_I), I over the column's structure (ancestors).
+__global__ __launch_bounds__(kTlWG) void k_tl2_back(slam_ba_problem p, int eoff) {
+  lm_wave_priority();
+  const TlLayout L(9 * p.n_cams);
+  if (tl_failed(p, L)) return;
+  const int32_t* S = p.tl_sched;
+  const int32_t* e = S + eoff + 3 * blockIdx.x;
+  const int k = e[0], so = e[1], sc = e[2];
+  __shared__ double r[kTB];
+  __shared__ double part[4][kTB];
+  const double* A = p.chol + L.a;
+  const int t = threadIdx.x, c = t & 63, q = t >> 6;
+  // thread (q, c): rows m in [16q, 16q + 16) of every L_Ik^T x_I, column c
+  double s2 = 0.0;
+  for (int u = 0; u < sc; ++u) {
+    const int I = S[so + u];
+    const double* LIk = A + (size_t)I * kTB * L.N + k * kTB;
+    const double* xI = p.chol + L.x + I * kTB;
+    for (int m = 16 * q; m < 16 * q + 16; ++m) s2 = __builtin_fma(LIk[(size_t)m * L.N + c], xI[m], s2);
+  }
+  part[q][c] = s2;
+  __syncthreads();
+  if (t < kTB) r[t] = p.chol[L.y + k * kTB + t] - (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
+  __syncthreads();
+  const double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;  // L_kk^-1
+  double s3 = 0.0;
+  for (int m = 16 * q; m < 16 * q + 16; ++m) s3 = __builtin_fma(Vkk[m * kTB + c], r[m], s3);
+  part[q][c] = s3;
+  __syncthreads();
+  if (t < kTB) p.chol[L.x + k * kTB + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+}
+
+// x (new tile order, L.x) -> camera order in the y region (read by the epilogue)
+__global__ __launch_bounds__(kTB) void k_tl2_unperm(slam_ba_problem p) {
+  const TlLayout L(9 * p.n_cams);
+  const int I = blockIdx.x;  // new tile
+  const int oldI = p.tl_sched[p.tl_sched[3] + I];
+  p.chol[L.y + oldI * kTB + threadIdx.x] = p.chol[L.x + I * kTB + threadIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
+  lm_wave_priority();
+  __shared__ double red[32];
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const bool ok = !tl_failed(p, L);
+  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
+  const double* gvec = bvec + n;
+  solve_epilogue(p, p.chol + L.y, ok, red,
+                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+}
+
+static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
+  const TlLayout L(9 * p.n_cams);
+  const int32_t* h = p.tl_sched_host;
+  const int nlev = h[0], T = h[1];
+  SLAM_REQUIRE(T == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d", T, L.T);
+  const int32_t* tab = h + h[4];
+  k_tl2_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p);
+  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
+  for (int lv = 0; lv < nlev; ++lv) {
+    const int32_t* e = tab + 6 * lv;
+    if (e[1] > 0) k_tl2_panel<<<e[1], kTlWG, 0, s>>>(p, e[0]);
+    if (e[3] > 0) k_tl2_update<<<e[3], kTlWG, 0, s>>>(p, e[2]);
+  }
+  for (int lv = nlev - 1; lv >= 0; --lv) {
+    const int32_t* e = tab + 6 * lv;
+    if (e[5] > 0) k_tl2_back<<<e[5], kTlWG, 0, s>>>(p, e[4]);
+  }
+  k_tl2_unperm<<<T, kTB, 0, s>>>(p);
+  k_tl2_epilogue<<<1, 1024, 0, s>>>(p);
+  SLAM_LAUNCHED("k_tl2_*");
+  return SLAM_OK;
+}
+
 static void tl_solve(const slam_ba_problem& p, hipStream_t s) {
   const TlLayout L(9 * p.n_cams);
   const int T = L.T;
@@ -2103,6 +2357,8 @@ int check_problem(const slam_ba_problem* p) {
                                      : p->n_blocks == p->n_cams * (p->n_cams + 1) / 2,
                "slam_ba: n_blocks must list all C(C+1)/2 upper blocks (9C <= %d) or the "
                "diagonal and every block with common points (packed)", kDenseMaxN);
+  SLAM_REQUIRE(!p->tl_sched == !p->tl_sched_host,
+               "slam_ba: tl_sched and tl_sched_host come together");
   SLAM_REQUIRE(!sys_packed(p->n_cams) || p->chol != nullptr,
                "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
                kLdsMaxN);
@@ -2212,8 +2468,12 @@ static int launch_solve(const Launch& L, bool fuse_decide, hipStream_t s) {
     k_solve_blk<<<dim3(1, L.n), kBlkWG, L.solve_lds, s>>>(L.b);
     SLAM_LAUNCHED("k_solve_blk");
   } else {
-    tl_solve(L.b.p[0], s);
-    SLAM_LAUNCHED("k_tl_*");
+    if (L.b.p[0].tl_sched != nullptr) {
+      if (int rc = tl_solve_levels(L.b.p[0], s)) return rc;
+    } else {
+      tl_solve(L.b.p[0], s);
+      SLAM_LAUNCHED("k_tl_*");
+    }
   }
   if (fuse_decide)
     k_back_trial<true><<<dim3(L.max_grps, L.n), kGrp, 0, s>>>(L.b);

@@ -91,6 +91,167 @@ def upper_blocks(n_cams, cam_idx, pt_idx):
     return np.unique(np.concatenate([block_index(diag, diag, n_cams), block_index(c1, c2, n_cams)]))
 
 
+TB = 64  # tile edge of the tiled solver (csrc/ba.hip kTB)
+
+
+def _nd_order(adj, nodes):
+    """Nested-dissection order of `nodes` in the tile graph `adj` (list of
+    sets): each connected component separately; a component whose BFS level
+    structure (from a pseudo-peripheral node) has >= 3 levels is split by its
+    middle level, the separator numbered last."""
+    nodes = set(nodes)
+    out = []
+    while nodes:  # components, lowest node first
+        root = min(nodes)
+        comp, stack = {root}, [root]
+        while stack:
+            u = stack.pop()
+            for v in adj[u]:
+                if v in nodes and v not in comp:
+                    comp.add(v)
+                    stack.append(v)
+        nodes -= comp
+        out += _nd_component(adj, comp)
+    return out
+
+
+def _bfs_levels(adj, comp, root):
+    levels, seen = [[root]], {root}
+    while True:
+        nxt = sorted({v for u in levels[-1] for v in adj[u] if v in comp and v not in seen})
+        if not nxt:
+            return levels
+        seen.update(nxt)
+        levels.append(nxt)
+
+
+def _nd_component(adj, comp):
+    if len(comp) <= 2:
+        return sorted(comp)
+    levels = _bfs_levels(adj, comp, min(comp))
+    for _ in range(2):  # pseudo-peripheral: restart from the far end
+        far = min(levels[-1])
+        lv2 = _bfs_levels(adj, comp, far)
+        if len(lv2) <= len(levels):
+            break
+        levels = lv2
+    if len(levels) < 3:
+        return sorted(comp)
+    sep = set(levels[len(levels) // 2])
+    return _nd_order(adj, comp - sep) + sorted(sep)
+
+
+def tl_schedule(n_cams, blocks):
+    """Level schedule of the tiled camera solve (csrc/ba.hip tl_solve_levels).
+
+    The 64-row tiles of the 9C-row camera system are renumbered by nested
+    dissection of their adjacency graph (tiles sharing a camera block), the
+    tile-level Cholesky structure and elimination tree are computed
+    symbolically, and the columns are grouped by their height in the tree:
+    the columns of one level are mutually independent, so each level is one
+    panel launch (factor + L_Ik for every column of the level) and one update
+    launch (A_IJ -= sum_k L_Ik L_Jk^T, b_I -= sum_k L_Ik y_k per target tile),
+    and the back substitution walks the levels in reverse.  A banded window of
+    T tiles needs ~log2(T) levels instead of T sequential panel steps.
+
+    Returns the int32 schedule (device and host copies are the same array):
+      [0] nlev, [1] T, [2] tperm offset, [3] itperm offset, [4] level table offset
+      level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
+      panel entries (k, I)         -- I == k: the diagonal tile
+      update entries (I, J, koff, kcnt), I >= J, k list in `koff`
+      back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)
+    tperm[old tile] = new tile, itperm its inverse."""
+    blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
+    n = 9 * int(n_cams)
+    T = (n + TB - 1) // TB
+    adj = [set() for _ in range(T)]
+    for c1, c2 in blocks:
+        t1 = range((9 * c1) // TB, (9 * c1 + 8) // TB + 1)
+        t2 = range((9 * c2) // TB, (9 * c2 + 8) // TB + 1)
+        for a in t1:
+            for b in t2:
+                if a != b:
+                    adj[a].add(b)
+                    adj[b].add(a)
+    order = _nd_order(adj, range(T))
+    tperm = np.empty(T, np.int64)
+    tperm[np.asarray(order, np.int64)] = np.arange(T)
+    itperm = np.asarray(order, np.int64)
+    # symbolic tile Cholesky in the new numbering
+    struct = [set() for _ in range(T)]
+    for a in range(T):
+        for b in adj[a]:
+            A, B = tperm[a], tperm[b]
+            if A > B:
+                struct[B].add(int(A))
+    parent = [-1] * T
+    level = [0] * T
+    for k in range(T):
+        if struct[k]:
+            pk = min(struct[k])
+            parent[k] = pk
+            struct[pk] |= struct[k] - {pk}
+    for k in range(T):
+        if parent[k] >= 0:
+            level[parent[k]] = max(level[parent[k]], level[k] + 1)
+    nlev = max(level) + 1 if T else 0
+    cols = [[k for k in range(T) if level[k] == lv] for lv in range(nlev)]
+    head = [nlev, T, 0, 0, 0]
+    table, body = [], []
+    lists = []  # (k lists / struct lists) appended after the entries
+
+    def list_off(vals):
+        lists.append(list(vals))
+        return len(lists) - 1  # patched below
+
+    pan, upd, bk = [], [], []
+    for lv in range(nlev):
+        p_e = []
+        for k in cols[lv]:
+            p_e.append((k, k))
+            p_e += [(k, I) for I in sorted(struct[k])]
+        tgt = {}
+        for k in cols[lv]:
+            sk = sorted(struct[k])
+            for i, I in enumerate(sk):
+                for J in sk[:i + 1]:
+                    tgt.setdefault((I, J), []).append(k)
+        u_e = [(I, J, list_off(ks)) for (I, J), ks in sorted(tgt.items())]
+        b_e = [(k, list_off(sorted(struct[k]))) for k in cols[lv]]
+        pan.append(p_e)
+        upd.append(u_e)
+        bk.append(b_e)
+    # layout: header | tperm | itperm | level table | entries | lists
+    off = len(head)
+    head[2] = off
+    off += T
+    head[3] = off
+    off += T
+    head[4] = off
+    off += 6 * nlev
+    ent_start = off
+    n_ent = sum(2 * len(a) + 4 * len(b) + 3 * len(c) for a, b, c in zip(pan, upd, bk))
+    list_base = ent_start + n_ent
+    list_offs, o = [], list_base
+    for li in lists:
+        list_offs.append(o)
+        o += len(li)
+    ents = []
+    for lv in range(nlev):
+        po = ent_start + len(ents)
+        for k, I in pan[lv]:
+            ents += [k, I]
+        uo = ent_start + len(ents)
+        for I, J, li in upd[lv]:
+            ents += [I, J, list_offs[li], len(lists[li])]
+        bo = ent_start + len(ents)
+        for k, li in bk[lv]:
+            ents += [k, list_offs[li], len(lists[li])]
+        table += [po, len(pan[lv]), uo, len(upd[lv]), bo, len(bk[lv])]
+    flat = head + tperm.tolist() + itperm.tolist() + table + ents + [v for li in lists for v in li]
+    return np.asarray(flat, np.int32)
+
+
 def _pairs_by_point(cam_idx, pt_idx):
     """Observation pairs (o1 < o2 in (point, camera) order) of the same point."""
     order = np.lexsort((cam_idx, pt_idx))
@@ -439,11 +600,13 @@ class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
-                 block_list=None, lin_mode="auto", chunks_per_wg=None):
+                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_levels=True):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
-        every point is seen by <= MF_CAMS cameras)."""
+        every point is seen by <= MF_CAMS cameras).  tl_levels: the tiled
+        camera solve (9C > 120) runs the nested-dissection level schedule
+        (tl_schedule); False keeps one panel step per tile column."""
         dev = require_gpu()
         cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
@@ -485,6 +648,10 @@ class BAProblem:
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
+        self.tl_levels = tl_levels and C9 > LDS_MAX_N
+        if self.tl_levels:  # level schedule of the tiled solve (host + device copies)
+            self._sched_host = tl_schedule(C, pl["blocks"])
+            t["tl_sched"] = T(self._sched_host)
         t["delta_c"] = z(C9)
         G = pl["n_grps"]
         t["red_part"] = z(_lib.lib.slam_ba_red_slots(G))
@@ -503,6 +670,9 @@ class BAProblem:
                                   "red_part", "small", "state", "ticket") + \
                 (_MFMA_TABLES if pl["mode"] == 1 else ()):
             setattr(s, k, t[k].data_ptr())
+        if self.tl_levels:
+            s.tl_sched = t["tl_sched"].data_ptr()
+            s.tl_sched_host = self._sched_host.ctypes.data
         self._s = s
         self.reset(lam0)
 

@@ -84,6 +84,7 @@ class Tracker:
         # workspace (OpenCV keeps every tie); such a frame must not silently
         # degrade into "no matches" + a stale pose
         self.orb_min = torch.full((1,), 1 << 30, **i32)
+        self.orb_event = torch.cuda.Event()
 
     # ------------------------------------------------------------------ device step
     def track(self, frame0: int, imgs: torch.Tensor | None = None, marks=None, chain=True):
@@ -107,6 +108,8 @@ class Tracker:
         kp, octv, desc, cnt = self.ows.run(im, st)
         with torch.cuda.stream(st if st is not None else torch.cuda.current_stream()):
             torch.minimum(self.orb_min, cnt.amin(), out=self.orb_min)
+        # ORB of this batch done: a caller may hold other work back until here
+        self.orb_event.record(st if st is not None else torch.cuda.current_stream())
         mark("orb")
         kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]

@@ -558,6 +558,79 @@ def test_union_plan_assembles_the_reduced_system(case):
     assert np.abs(b - br).max() <= 1e-9 * max(1.0, np.abs(br).max())
 
 
+def _emulate_tl_levels(S, b, sched):
+    """The level-scheduled tiled solve (csrc/ba.hip k_tl2_*) restated in NumPy,
+    launch by launch: tiles renumbered by the schedule's tperm, each level's
+    panels (diagonal factor + inverse, y_k; L_Ik = A_Ik L_kk^-T), then its
+    updates (A_IJ -= sum_k L_Ik L_Jk^T, b_I -= sum_k L_Ik y_k), then the back
+    substitution by levels in reverse, x un-permuted."""
+    nlev, T = int(sched[0]), int(sched[1])
+    tperm = sched[sched[2]:sched[2] + T]
+    tab = sched[sched[4]:sched[4] + 6 * nlev].reshape(-1, 6)
+    n, TB = len(b), 64
+    N = T * TB
+    new = lambda r: tperm[r // TB] * TB + r % TB  # noqa: E731
+    rn = new(np.arange(N))
+    A = np.zeros((N, N))
+    A[np.ix_(rn[:n], rn[:n])] = S
+    A[rn[n:], rn[n:]] = 1.0
+    bb = np.zeros(N)
+    bb[rn[:n]] = b
+    t = lambda I: slice(I * TB, (I + 1) * TB)  # noqa: E731
+    dinv, y, x = {}, np.zeros(N), np.zeros(N)
+    for lv in range(nlev):
+        po, pc, uo, uc, bo, bc = tab[lv]
+        ent = sched[po:po + 2 * pc].reshape(-1, 2)
+        for k in ent[ent[:, 0] == ent[:, 1], 0]:
+            Lkk = np.linalg.cholesky(A[t(k), t(k)])
+            dinv[k] = np.linalg.inv(Lkk)
+            y[t(k)] = dinv[k] @ bb[t(k)]
+        for k, I in ent[ent[:, 0] != ent[:, 1]]:
+            A[t(I), t(k)] = A[t(I), t(k)] @ dinv[k].T
+        for I, J, ko, kc in sched[uo:uo + 4 * uc].reshape(-1, 4):
+            ks = sched[ko:ko + kc]
+            A[t(I), t(J)] -= sum(A[t(I), t(k)] @ A[t(J), t(k)].T for k in ks)
+            if I == J:
+                bb[t(I)] -= sum(A[t(I), t(k)] @ y[t(k)] for k in ks)
+    for lv in reversed(range(nlev)):
+        po, pc, uo, uc, bo, bc = tab[lv]
+        for k, so, sc in sched[bo:bo + 3 * bc].reshape(-1, 3):
+            r = y[t(k)].copy()
+            for I in sched[so:so + sc]:
+                r -= A[t(I), t(k)].T @ x[t(I)]
+            x[t(k)] = dinv[k].T @ r
+    return x[rn[:n]]
+
+
+@pytest.mark.parametrize("C,loop", [(30, False), (64, False), (120, True)])
+def test_tl_level_schedule_solves_the_camera_system(C, loop):
+    """Nested-dissection level schedule of the tiled solver: every level's
+    columns are independent (no L between them), a banded window needs
+    ~log2(T) levels, and executing the schedule tile by tile solves S x = b."""
+    from slam355.ba import tl_schedule, upper_blocks
+    from slam355.synthetic import ba_problem, ba_problem_loop
+
+    rng = np.random.default_rng(C)
+    cams, pts, ci, pi, qs = (ba_problem_loop if loop else ba_problem)(rng, C, 40 * C, 5)
+    ub = upper_blocks(C, ci, pi)
+    iu, ju = np.triu_indices(C)
+    blocks = np.stack([iu[ub], ju[ub]], 1)
+    sched = tl_schedule(C, blocks)
+    nlev, T = int(sched[0]), int(sched[1])
+    assert T == -(-9 * C // 64) and nlev <= 2 + 2 * int(np.ceil(np.log2(T)))
+    tperm = sched[sched[2]:sched[2] + T]
+    assert sorted(tperm.tolist()) == list(range(T))
+    # S: random SPD with exactly the camera-block pattern
+    n = 9 * C
+    M = np.zeros((n, n))
+    for c1, c2 in blocks:
+        M[9 * c1:9 * c1 + 9, 9 * c2:9 * c2 + 9] = rng.normal(size=(9, 9))
+    S = M + M.T + np.diag(np.abs(M).sum(1) + np.abs(M).sum(0) + 1.0)
+    b = rng.normal(size=n)
+    x = _emulate_tl_levels(S, b, sched)
+    assert np.allclose(x, np.linalg.solve(S, b), rtol=0, atol=1e-10 * np.abs(x).max())
+
+
 def test_union_plan_falls_back_for_wide_tracks():
     """A point seen by more than MF_CAMS cameras: no camera-union plan (the
     slot linearisation takes such problems)."""
