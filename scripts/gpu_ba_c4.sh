@@ -11,5 +11,7 @@ timeout -k 10 300 python bench.py --workload ba --c5 --steps 20 --warmup 3 > "$O
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c4_$TAG" -o run \
   -- python3 "$ROOT/bench.py" --workload ba --c4 --steps 20 --warmup 3 > "$OUT/ba_c4_prof_$TAG.log" 2>&1 || exit 1
-find "$OUT/prof_c4_$TAG" -name "*kernel_trace.csv" -delete
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_c5_$TAG" -o run \
+  -- python3 "$ROOT/bench.py" --workload ba --c5 --steps 5 --warmup 2 > "$OUT/ba_c5_prof_$TAG.log" 2>&1 || exit 1
+find "$OUT/prof_c4_$TAG" "$OUT/prof_c5_$TAG" -name "*kernel_trace.csv" -delete
 echo done
