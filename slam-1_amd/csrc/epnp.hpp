@@ -124,6 +124,60 @@ __device__ __forceinline__ int ep_lsq6(const double* A, const double* b, double*
   return 1;
 }
 
+// ep_lsq6<k> on a 6 x 5 system whose columns >= k are dead (decoupled: unit
+// diagonal in the normal equations, zero right-hand side, x = 0): the live
+// part performs exactly the operations of ep_lsq6<k>
+__device__ __forceinline__ int ep_lsq6_live(const double* A, const double* b, int k, double* x) {
+  double N[5][5], r[5];
+  #pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    #pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      double s = 0.0;
+      #pragma unroll
+      for (int m = 0; m < 6; ++m) s += A[m * 5 + i] * A[m * 5 + j];
+      N[i][j] = i < k ? s : (i == j ? 1.0 : 0.0);
+    }
+    double s = 0.0;
+    #pragma unroll
+    for (int m = 0; m < 6; ++m) s += A[m * 5 + i] * b[m];
+    r[i] = i < k ? s : 0.0;
+  }
+  bool ok = true;
+  #pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    double s = N[j][j];
+    #pragma unroll
+    for (int p = 0; p < j; ++p) s -= N[j][p] * N[j][p];
+    ok = ok && s > 0.0;
+    N[j][j] = sqrt(s);
+    #pragma unroll
+    for (int i = j + 1; i < 5; ++i) {
+      double t = N[i][j];
+      #pragma unroll
+      for (int p = 0; p < j; ++p) t -= N[i][p] * N[j][p];
+      N[i][j] = t / N[j][j];
+    }
+  }
+  if (!ok) return 0;
+  double y[5];
+  #pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    double t = r[i];
+    #pragma unroll
+    for (int p = 0; p < i; ++p) t -= N[i][p] * y[p];
+    y[i] = t / N[i][i];
+  }
+  #pragma unroll
+  for (int i = 4; i >= 0; --i) {
+    double t = y[i];
+    #pragma unroll
+    for (int p = i + 1; p < 5; ++p) t -= N[p][i] * x[p];
+    x[i] = t / N[i][i];
+  }
+  return 1;
+}
+
 /* pose from the 4 camera-frame control points ccs (betas applied): R, t and
  * the mean reprojection error over the n points */
 template <int n>
@@ -551,16 +605,22 @@ __device__ __forceinline__ void ep_approx(int approx, const double* pw, const do
                                           double fy, double cx, double cy, EpGroup& G) {
   double* res = G.res[approx];
   res[7] = 0.0;
-  const int cols[3][5] = {{0, 1, 3, 6, 0}, {0, 1, 2, 0, 0}, {0, 1, 2, 3, 4}};
-  const int nk[3] = {4, 3, 5};
-  const int k = nk[approx];
+  // columns of L per approximation: {B11 B12 B13 B14}, {B11 B12 B22},
+  // {B11 B12 B22 B13 B23}; a fixed 6 x 5 system whose unused columns are
+  // decoupled (unit diagonal, zero right-hand side) -- the live k x k part
+  // rounds exactly as ep_lsq6<k>, and no register array is indexed by lane
+  const int k = approx == 0 ? 4 : approx == 1 ? 3 : 5;
   double As[30], xb[5], rho[6];
+#pragma unroll
   for (int j = 0; j < 6; ++j) rho[j] = G.rho[j];
+#pragma unroll
   for (int j = 0; j < 6; ++j)
-    for (int c = 0; c < k; ++c) As[j * k + c] = G.L[10 * j + cols[approx][c]];
-  const int okls = approx == 0 ? ep_lsq6<4>(As, rho, xb)
-                   : approx == 1 ? ep_lsq6<3>(As, rho, xb) : ep_lsq6<5>(As, rho, xb);
-  if (!okls) return;
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const int col = c < 2 ? c : approx == 0 ? (c == 2 ? 3 : 6) : c;
+      As[j * 5 + c] = c < k ? G.L[10 * j + col] : 0.0;
+    }
+  if (!ep_lsq6_live(As, rho, k, xb)) return;
   double be[4] = {0, 0, 0, 0};
   if (approx == 0) {
     if (xb[0] < 0.0) {
