@@ -136,10 +136,11 @@ def pmc_bytes(pmc, kernels):
     return float(sum(pmc["kernels"][k]["hbm_bytes"] for k in kernels))
 
 
-def masked_stream(n_cus):
-    """A HIP stream whose kernels may use only CUs [0, n_cus) (hipExtStreamCreateWithCUMask),
-    wrapped as a torch stream: `--track-cus` keeps the rest of the CUs free of
-    tracking work for the local-BA stream."""
+def masked_stream(n_cus, first=0):
+    """A HIP stream whose kernels may use only CUs [first, first + n_cus)
+    (hipExtStreamCreateWithCUMask), wrapped as a torch stream: `--track-cus`
+    keeps the rest of the CUs free of tracking work for the local-BA stream;
+    `--ba-cus` gives the two streams disjoint CU sets."""
     import ctypes
 
     hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"),
@@ -147,7 +148,7 @@ def masked_stream(n_cus):
     n_total = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     words = (n_total + 31) // 32
     mask = (ctypes.c_uint32 * words)()
-    for i in range(min(n_cus, n_total)):
+    for i in range(first, min(first + n_cus, n_total)):
         mask[i // 32] |= 1 << (i % 32)
     h = ctypes.c_void_p()
     rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), words, mask)
@@ -223,6 +224,9 @@ def run_tracking(args, world, rank):
     feed = FrameFeed(L, R, B, n_win)
     L_np, R_np = L[:3].cpu().numpy(), R[:2].cpu().numpy()
     del L, R
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    if args.ba_cus:  # disjoint CU sets: tracking on [0, n - ba_cus), local BA on the rest
+        args.track_cus = n_cu - args.ba_cus
     trk_stream = masked_stream(args.track_cus) if args.track_cus else None
     if trk_stream is None and args.priority == "track":
         trk_stream = torch.cuda.Stream(priority=-1)
@@ -240,8 +244,11 @@ def run_tracking(args, world, rank):
     stream = torch.cuda.current_stream()
     # local mapping (BA) on its own HIP stream, concurrent with tracking, unless --ba-serial
     # (high priority: its short latency-bound kernels go ahead of queued ORB tiles)
-    ba_stream = (stream if args.ba_serial else
-                 torch.cuda.Stream(priority=-1 if args.priority == "ba" else 0))
+    if args.ba_cus and not args.ba_serial:
+        ba_stream = masked_stream(args.ba_cus, first=n_cu - args.ba_cus)
+    else:
+        ba_stream = (stream if args.ba_serial else
+                     torch.cuda.Stream(priority=-1 if args.priority == "ba" else 0))
     with torch.cuda.stream(ba_stream):
         ba = BABatch([BAProblem(*w, stream=ba_stream, chunks_per_wg=args.chunks_per_wg)
                       for w in windows], stream=ba_stream)
@@ -318,12 +325,12 @@ def run_tracking(args, world, rank):
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_solves} C3 windows: k_linearize + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_solves} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile", "k_orb_compact"))
-    roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_linearize", "k_assemble", "k_solve_blk",
+    roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_assemble", "k_solve_blk",
                                                   "k_back_trial<true>"))
     for r in roof.values():
         r["frac"] = r["achieved"] / r["peak"]
@@ -355,7 +362,8 @@ def run_tracking(args, world, rank):
                    "local_ba_stream": "serial" if args.ba_serial else "concurrent",
                    "high_priority_stream": args.priority,
                    "ba_overlap": args.ba_overlap,
-                   "tracking_cus": args.track_cus or "all"},
+                   "tracking_cus": args.track_cus or "all",
+                   "local_ba_cus": args.ba_cus or "all"},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
         "stage_ms_per_step": per_step,
@@ -370,15 +378,62 @@ def run_tracking(args, world, rank):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, windows[0])
-    del trk, ba  # their kernels' buffers, then the masked stream itself
+    if not args.no_tracked_ba:
+        rec["tracked_window_ba"] = tracked_window_ba(feed, B, rig, args)
+    del trk, ba  # their kernels' buffers, then the masked streams themselves
     if trk_stream is not None:
         trk_stream.destroy()
+    if hasattr(ba_stream, "destroy"):
+        ba_stream.destroy()
     if not args.no_ba_scale:
         # the metric's second half: local-BA LM iterations/s of ONE C4 window
         # sharded over all ranks (landmarks by anchor keyframe, RCCL all-reduce
         # of the reduced camera system per iteration) -- strong scaling in N
         rec["local_ba_sharded"] = c4_sharded_iters(world, rank, steps=20, warmup=3)
     return rec
+
+
+def tracked_window_ba(feed, B, rig, args, n_pairs=8):
+    """Local BA on a window built from tracked frames (main.py:120-127 ->
+    XXXport_files.export_data -> BundleAdjustment): n_pairs frame pairs of the
+    streamed sequence tracked on the device, their temporally matched points
+    mapped by LocalMap (device rel_to_abs + appendKeyPoints on the device map),
+    the BA problem formed from the map (problem_from_map) and solved with
+    `ba_iters` LM iterations (one HIP graph).  Reported beside `value`: the
+    host-side problem build and the device LM time."""
+    from slam355.ba import BAProblem
+    from slam355.pipeline import LocalMap, Tracker
+
+    pack = feed.packs[0]
+    imgs = torch.cat([pack[:n_pairs + 1], pack[B + 1:B + 1 + n_pairs]]).cuda()
+    trk = Tracker(n_pairs, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=0)
+    lm = LocalMap(trk)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    trk.track(0, imgs=imgs)
+    lm.add(0)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    cams, pts, ci, pi, qs = lm.problem(rig.P_l)
+    prob = BAProblem(cams, pts, ci, pi, qs)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    cost0 = prob.state()["COST"]
+    prob.iterate_graphed(args.ba_iters)  # capture + warm
+    prob.restore()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    prob.iterate_graphed(args.ba_iters)
+    e1.record()
+    torch.cuda.synchronize()
+    st = prob.state()
+    return {"frames": n_pairs + 1, "n_cams": int(len(cams)), "n_pts": int(len(pts)),
+            "n_obs": int(len(ci)), "track_and_map_ms": (t1 - t0) * 1e3,
+            "host_problem_build_ms": (t2 - t1) * 1e3,
+            "lm_ms_per_iter": e0.elapsed_time(e1) / args.ba_iters, "lm_iters": args.ba_iters,
+            "cost_first": cost0, "cost_final": st["COST"], "accepted": int(st["NACCEPT"]),
+            "lin_mode": prob.lin_mode}
 
 
 def _backend_name():
@@ -772,6 +827,10 @@ def main():
                     help="restrict the tracking stream to this many CUs (0: all); the rest run "
                          "only local-BA work, whose latency-bound kernels then do not share "
                          "SIMDs and LDS with ORB workgroups")
+    ap.add_argument("--no-tracked-ba", action="store_true",
+                    help="tracking: skip the local BA of a window built from tracked frames")
+    ap.add_argument("--ba-cus", type=int, default=0,
+                    help="disjoint CU partition: local BA on the last N CUs, tracking on the rest")
     args = ap.parse_args()
     world, rank = dist_init()
     run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher,

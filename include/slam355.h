@@ -297,7 +297,10 @@ typedef struct slam_ba_problem {
                             groups); 1: camera-union linearisation
                             (k_lin_mfma; grp_* = chunks, slots per supergroup) */
   int32_t n_sgrps;       /* lin_mode 1: supergroups (>= 1)                    */
-  int32_t reserved;
+  int32_t tl_mode;       /* tiled solve with tl_sched: 0 dataflow (k_tl3_flow,
+                            one persistent workgroup per tile column, when the
+                            schedule has <= SLAM_TL_FLOW_MAX_T columns), 1 one
+                            launch pair per elimination-tree level           */
   double* cams[2];              /* [C][9]  double-buffered, state[CUR] is live */
   double* pts[2];               /* [P][3]                                      */
   double* camrec[2];            /* [C][32] per-camera projection records of cams[] */
@@ -352,6 +355,10 @@ typedef struct slam_ba_problem {
   const int32_t* tl_sched;
   const int32_t* tl_sched_host;
 } slam_ba_problem;
+
+/* Largest tile count (9C / 64, rounded up) the dataflow tiled solve takes:
+ * one persistent workgroup per tile column, all resident at once (<= 1 per CU). */
+#define SLAM_TL_FLOW_MAX_T 128
 
 /* Problems per batched launch (slam_ba_iterate_batch splits larger batches). */
 #define SLAM_BA_MAX_BATCH 8

@@ -1,0 +1,52 @@
+"""Per-column phase timeline of the dataflow tiled solve (k_tl3_flow) at C4 / C5.
+Run with SLAM355_LIB=slam-1_amd/prof/libslam355_flowprof.so (scripts/build_flow_prof.sh)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "slam-1_amd")]
+
+from slam355 import _lib  # noqa: E402
+from slam355.ba import BAProblem  # noqa: E402
+from slam355.synthetic import ba_problem, ba_problem_loop, perturb  # noqa: E402
+
+PH = ["diag_upd", "factor", "rows", "y", "x_wait", "x", "end"]
+for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_problem_loop)):
+    rng = np.random.default_rng(7)
+    cams, pts, ci, pi, qs = gen(rng, C, P, 6)
+    c0, p0 = perturb(rng, cams, pts)
+    prob = BAProblem(c0, p0, ci, pi, qs)
+    T = int(prob._sched_host[1])
+    fn = _lib.lib.slam_flow_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    runs = []
+    for _ in range(5):
+        prob.iterate(1)
+        buf = (ctypes.c_ulonglong * (8 * T))()
+        fn(ctypes.cast(buf, ctypes.c_void_p), T)
+        runs.append(np.array(buf[:], np.int64).reshape(T, 8))
+    st = runs[-1]
+    t0 = st[:, 0].min()
+    rel = (st - t0) * 10 / 1000.0  # us
+    print(f"{name}: T={T} span {rel[:, 6].max():.1f} us (to last x), epilogue end {rel[:, 7].max():.1f}")
+    sched = prob._sched_host
+    rec = sched[sched[5]:sched[5] + 5 * T].reshape(-1, 5)
+    for J in range(T):
+        d = np.diff(rel[J, :7])
+        print(f"  col {J:3d} rows {rec[J,1]} rs {rec[J,3]}: start {rel[J,0]:7.1f} " +
+              " ".join(f"{PH[i]} {d[i]:6.1f}" for i in range(6)) + f" | x at {rel[J,6]:7.1f}")
+        if J > 24:
+            break
+    ff = getattr(_lib.lib, "slam_flow_fac_stamps", None)
+    if ff is not None:
+        fb = (ctypes.c_ulonglong * 16)()
+        ff.argtypes = [ctypes.c_void_p]
+        ff(ctypes.cast(fb, ctypes.c_void_p))
+        v = np.array(fb[:14], np.int64) * 10 / 1000.0
+        d = np.diff(v)
+        print("  factor of column 0 (us): " + " ".join(
+            f"p{p}: w0 {d[3 * p]:.2f} panel {d[3 * p + 1]:.2f} trail {d[3 * p + 2]:.2f}" for p in range(4))
+            + f" | inverse assembly {d[12]:.2f} | total {v[13] - v[0]:.2f}")

@@ -1429,7 +1429,7 @@ constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a til
 
 struct TlLayout {  // doubles inside p.chol
   int T, N;
-  long long a, dinv, b, y, x, nz, fail, total;
+  long long a, dinv, b, y, x, nz, fail, xo, fc, flow, total;
   __host__ __device__ explicit TlLayout(int n) {
     T = (n + kTB - 1) / kTB;
     N = T * kTB;
@@ -1440,7 +1440,10 @@ struct TlLayout {  // doubles inside p.chol
     x = y + N;
     nz = x + N;                          // T*T bytes
     fail = nz + ((long long)T * T + 7) / 8;
-    total = fail + 8;                    // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
+    xo = fail + 8;                       // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
+    fc = xo + N;                         // k_tl3_flow: x in camera order; [T][T][64] L_Ik y_k
+    flow = fc + (long long)T * T * kTB;  // (forward-substitution terms), then int flags:
+    total = flow + ((long long)T * T + 2 * T + 8 + 1) / 2;  // tile[T][T], y[T], x[T], ticket, epoch
   }
 };
 
@@ -1599,12 +1602,23 @@ __device__ unsigned long long g_tl_stamp[8];
 #else
 #define TL_STAMP(i) (void)0
 #endif
+// Akk == nullptr: the tile is already in M (written before the call; the
+// first barrier below publishes it).
+#ifdef SLAM_FLOW_PROFILE
+__device__ unsigned long long g_flow_fac[16];
+#define FAC_T(i)                                                    \
+  do {                                                              \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_flow_fac[i] = wall_clock64(); \
+  } while (0)
+#else
+#define FAC_T(i) (void)0
+#endif
 __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk, int ld,
                                                   double* M, double* Xb, double* Tb, int* okp,
                                                   bool tl_prof_on = false) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   TL_STAMP(0);
-  {
+  if (Akk != nullptr) {
     // all 16 loads of a lane in flight before the LDS stores
     double tmp[kTB * kTB / kTlWG];
 #pragma unroll
@@ -1621,6 +1635,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   bool ok = true;
   __syncthreads();
   TL_STAMP(1);
+  FAC_T(0);
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
@@ -1651,14 +1666,18 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
         for (int m = j + 1; m < 16; ++m) v[m] = __builtin_fma(-lij, Lt[j * kBS17 + m], v[m]);
       }
       // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
+      // (column-oriented: once x_k is known, every later row's sum takes its
+      // term -- the same k order per sum as the row form, a 16-step chain
+      // instead of 120 dependent FMAs)
       const int c = l & 15;
-      double x[16];
+      double x[16], sacc[16];
 #pragma unroll
-      for (int ii = 0; ii < 16; ++ii) {
-        double sacc = 0.0;
+      for (int ii = 0; ii < 16; ++ii) sacc[ii] = 0.0;
 #pragma unroll
-        for (int k = 0; k < ii; ++k) sacc = __builtin_fma(Lt[k * kBS17 + ii], x[k], sacc);
-        x[ii] = ii < c ? 0.0 : (ii == c ? rj[ii] : -sacc * rj[ii]);
+      for (int k = 0; k < 16; ++k) {
+        x[k] = k < c ? 0.0 : (k == c ? rj[k] : -sacc[k] * rj[k]);
+#pragma unroll
+        for (int ii = k + 1; ii < 16; ++ii) sacc[ii] = __builtin_fma(Lt[k * kBS17 + ii], x[k], sacc[ii]);
       }
       if (l < 16) {
         double* X = Xb + blk_id(p, p) * 16 * kBS17;
@@ -1667,6 +1686,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
       }
     }
     __syncthreads();
+    FAC_T(1 + 3 * p);
     // panel: L_ip = A_ip X_pp^T (one block per wave)
     const int ip = p + 1 + w;
     if (ip < 4) {
@@ -1676,6 +1696,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
       st16(Aip, kMS, acc);
     }
     __syncthreads();
+    FAC_T(2 + 3 * p);
     // trailing: A_ij -= L_ip L_jp^T for p < j <= i <= 3
     const int nt = (3 - p) * (4 - p) / 2;
     for (int q = w; q < nt; q += 4) {
@@ -1691,6 +1712,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
       st16(Aij, kMS, acc);
     }
     __syncthreads();
+    FAC_T(3 + 3 * p);
   }
   TL_STAMP(2);
   // L^-1 by levels d = i - p: T = sum_k L_ik X_kp, then X_ip = -X_ii T
@@ -1716,6 +1738,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   if (w == 0 && l == 0) *okp = ok ? 1 : 0;
   __syncthreads();
   TL_STAMP(3);
+  FAC_T(13);
   return *okp != 0;
 }
 
@@ -1940,7 +1963,13 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p) {
     p.chol[L.b + I * kTB + threadIdx.x] =
         r < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
   }
-  if (idx == 0 && threadIdx.x == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 0;
+  if (idx == 0 && threadIdx.x == 0) {
+    *reinterpret_cast<int*>(p.chol + L.fail) = 0;
+    // k_tl3_flow: a new solve epoch (its flags compare against it), ticket re-armed
+    int* fl = reinterpret_cast<int*>(p.chol + L.flow) + L.T * L.T + 2 * L.T;
+    fl[0] = 0;
+    fl[1] = fl[1] + 1;
+  }
 }
 
 // One WG per packed block: its values at their renumbered positions (lower
@@ -2130,6 +2159,419 @@ __global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
   const double* gvec = bvec + n;
   solve_epilogue(p, p.chol + L.y, ok, red,
                  EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+}
+
+// ---------------------------------------------------------------- dataflow tiled solve
+// The same factor as a dataflow graph in ONE launch: workgroup J owns tile
+// column J (new numbering) for the whole solve and, from the schedule's column
+// table (slam355/ba.py tl_schedule),
+//   (1) A_JJ -= sum_{k in rs(J)} L_Jk L_Jk^T  (waits for each L_Jk's flag),
+//       factor + inverse of the diagonal tile (tile_chol_inv_blk, from LDS);
+//   (2) per row tile I in rows(J), parent first: A_IJ -= sum_k L_Ik L_Jk^T,
+//       L_IJ = A_IJ L_JJ^-T, published (tile flag);
+//   (3) y_J = L_JJ^-1 (b_J - sum_{k in rs(J)} L_Jk y_k)  (waits for y_k);
+//   (4) x_J = L_JJ^-T (y_J - sum_{I in rows(J)} L_IJ^T x_I)  (waits for x_I),
+//       stored in the new order and in camera order;
+//   (5) the last column to finish (ticket) runs the solve epilogue.
+// Launch boundaries become device flags: a column starts as soon as the tiles
+// it needs exist, so the factor advances along the elimination tree with no
+// per-level launch gaps.  Data crossing workgroups (L tiles, y, x) is written
+// with sc1 (write-through) stores and read with sc1 loads; a flag is raised
+// after the writer's stores have drained (s_waitcnt + barrier) and equals the
+// solve's epoch (bumped by k_tl2_load), so flags never need clearing.  Steps
+// (1)-(3) wait only on earlier columns; (4) waits on later ones, which is safe
+// because all T <= SLAM_TL_FLOW_MAX_T workgroups are resident together (one per
+// CU; the host checks T against the CU count).  Every wait gives up when the
+// solve failed (non-SPD tile) or after kFlowSpinMax polls (then it marks the
+// solve failed), so every workgroup reaches the ticket and exits.
+constexpr int kFlowSpinMax = 1 << 22;  // ~0.2 s of 128-cycle polls
+
+#ifdef SLAM_FLOW_PROFILE
+// per column: wall clock (100 MHz) at start, diagonal updates done, factor done,
+// row tiles published, y published, x inputs in, x published, end
+__device__ unsigned long long g_flow_stamp[SLAM_TL_FLOW_MAX_T][8];
+#define FLOW_T(i)                                                   \
+  do {                                                              \
+    if (threadIdx.x == 0) g_flow_stamp[blockIdx.x][i] = wall_clock64(); \
+  } while (0)
+#else
+#define FLOW_T(i) (void)0
+#endif
+
+struct FlowPtrs {
+  int *tile, *yf, *xf, *ticket, *epoch;
+  __device__ FlowPtrs(const slam_ba_problem& p, const TlLayout& L) {
+    int* base = reinterpret_cast<int*>(p.chol + L.flow);
+    tile = base;
+    yf = base + L.T * L.T;
+    xf = yf + L.T;
+    ticket = xf + L.T;
+    epoch = ticket + 1;
+  }
+};
+
+__device__ __forceinline__ int ld_flag(const int* f) {
+  return __hip_atomic_load(const_cast<int*>(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_flag(int* f, int v) {
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 polls until *flag == epoch; false (uniform) when the solve failed or
+// the wait timed out (which marks it failed).
+__device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh) {
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    for (int spins = 0; ld_flag(flag) != epoch; ++spins) {
+      if (ld_flag(fail) != 0) {
+        ok = 0;
+        break;
+      }
+      if (spins > kFlowSpinMax) {
+        st_flag(fail, 2);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    *sh = ok;
+  }
+  __syncthreads();
+  const bool ok = *sh != 0;
+  __syncthreads();
+  return ok;
+}
+
+// Wave 0 polls base[idx[i]] == epoch for all i < cnt together (lane i, chunks
+// of 64), so flags that are already up cost one round trip, not cnt.
+__device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int epoch, int* fail,
+                               int* sh) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    int ok = 1;
+    for (int c0 = 0; c0 < cnt && ok; c0 += 64) {
+      const int* f = c0 + lane < cnt ? base + idx[c0 + lane] : nullptr;
+      for (int spins = 0;; ++spins) {
+        const bool up = f == nullptr || ld_flag(f) == epoch;
+        if (__all(up)) break;
+        if (ld_flag(fail) != 0) {
+          ok = 0;
+          break;
+        }
+        if (spins > kFlowSpinMax) {
+          if (lane == 0) st_flag(fail, 2);
+          ok = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    if (lane == 0) *sh = ok;
+  }
+  __syncthreads();
+  const bool ok = *sh != 0;
+  __syncthreads();
+  return ok;
+}
+
+// every thread's (sc1) stores drained, then thread 0 raises the flag
+__device__ __forceinline__ void flow_publish(int* flag, int epoch) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) st_flag(flag, epoch);
+}
+
+// tile_to_frag through sc1 loads (the tile was written by another workgroup)
+__device__ __forceinline__ void tile_to_frag_sc1(const double* __restrict__ g, int ld, double* f) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, c = lane >> 4;
+  double tmp[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int fi = w + 4 * q;
+    tmp[q] = ld_sc1(g + (size_t)(16 * (fi >> 4) + r) * ld + 4 * (fi & 15) + c);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f[((w + 4 * q) << 6) + lane] = tmp[q];
+}
+
+// acc[s] += (rows 16w.., cols 16s.. of X Y^T), X and Y in fragment order
+__device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf, d4 acc[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int kk = 0; kk < 16; ++kk) {
+    const double a = Xf[((w * 16 + kk) << 6) + lane];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + lane], acc[s], 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_tl3_flow(slam_ba_problem p) {
+  lm_wave_priority();
+  const int n = 9 * p.n_cams;
+  const TlLayout L(n);
+  const int32_t* S = p.tl_sched;
+  const int T = L.T, J = blockIdx.x;
+  const int32_t* rec = S + S[5] + 5 * J;
+  const int ro = rec[0], rc = rec[1], so = rec[2], sc = rec[3], uo = rec[4];
+  const FlowPtrs F(p, L);
+  int* fail = reinterpret_cast<int*>(p.chol + L.fail);
+  const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
+  __shared__ double VX[2 * kTB * kTB];  // factor scratch; then L_JJ^-1 (fragments) | operand Y
+  __shared__ double Xf[kTB * kTB];      // operand X
+  __shared__ double part[4][kTB];
+  __shared__ double yv[kTB];
+  __shared__ double rv[kTB];
+  __shared__ int shf, okf;
+  double* A = p.chol + L.a;
+  double* Vf = VX;
+  double* Yf = VX + kTB * kTB;
+  const double* Vkk = p.chol + L.dinv + (size_t)J * kTB * kTB;  // L_JJ^-1, this column's own
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  bool ok = true;
+  FLOW_T(0);
+  // A_JJ (scattered by the previous launch) in registers before any wait
+  double ajj[16];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+      ajj[4 * s2 + r] = A[(size_t)(J * kTB + row) * L.N + J * kTB + col];
+    }
+  // ... and the first two row tiles' A_IJ
+  double air[2][16];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int I = q < rc ? S[ro + q] : J;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+        air[q][4 * s2 + r] = A[(size_t)(I * kTB + row) * L.N + J * kTB + col];
+      }
+  }
+  // (1) diagonal tile: L_Jk operands double-buffered (Xf / VX[4096:]) so the
+  // next tile's loads are in flight while the current one's MFMAs run
+  d4 acc[4];
+#pragma unroll
+  for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+  if (sc > 0) {
+    ok = flow_wait(F.tile + J * T + S[so], epoch, fail, &shf);
+    if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so] * kTB, L.N, Xf);
+  }
+  for (int q = 0; q < sc && ok; ++q) {
+    double* cur = (q & 1) ? Yf : Xf;
+    double* nxt = (q & 1) ? Xf : Yf;
+    __syncthreads();  // cur filled; the previous MFMAs' reads of nxt done
+    if (q + 1 < sc) {
+      ok = flow_wait(F.tile + J * T + S[so + q + 1], epoch, fail, &shf);
+      if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
+    }
+    gemm_xyT_acc(cur, cur, acc);
+  }
+  __syncthreads();
+  FLOW_T(1);
+  if (ok) {
+    double* M = VX;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+        M[row * kMS + col] = ajj[4 * s2 + r] - acc[s2][r];
+      }
+    double* Xb = VX + kTB * kMS;
+    ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf);
+    double x[kTB];
+    if (ok && w == 1) {
+      const int cb16 = lane >> 4;
+#pragma unroll
+      for (int m = 0; m < kTB; ++m)
+        x[m] = (m >> 4) >= cb16 ? Xb[blk_id(m >> 4, cb16) * 16 * kBS17 + (m & 15) * kBS17 + (lane & 15)]
+                                : 0.0;
+    }
+    __syncthreads();  // VX is reused below
+    if (!ok) {
+      if (t == 0) st_flag(fail, 1);
+    } else if (w == 1) {
+      double* V = p.chol + L.dinv + (size_t)J * kTB * kTB;
+#pragma unroll
+      for (int m = 0; m < kTB; ++m) {
+        V[m * kTB + lane] = x[m];
+        Vf[frag_idx(m, lane)] = x[m];
+      }
+    }
+    __syncthreads();
+  }
+  FLOW_T(2);
+  // (2) row tiles, parent first
+  for (int q = 0; q < rc && ok; ++q) {
+    const int I = S[ro + q];
+    const int ko = S[uo + 2 * q], kc = S[uo + 2 * q + 1];
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int u = 0; u < kc && ok; ++u) {
+      const int k = S[ko + u];
+      ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);  // (J, k) was waited for in (1)
+      if (!ok) break;
+      tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, Xf);
+      tile_to_frag_sc1(A + (size_t)J * kTB * L.N + k * kTB, L.N, Yf);
+      __syncthreads();
+      gemm_xyT_acc(Xf, Yf, acc);
+      __syncthreads();
+    }
+    if (!ok) break;
+    double* AIJ = A + (size_t)I * kTB * L.N + J * kTB;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+        const double a = q == 0 ? air[0][4 * s2 + r] : q == 1 ? air[1][4 * s2 + r]
+                                                             : AIJ[(size_t)row * L.N + col];
+        Xf[frag_idx(row, col)] = a - acc[s2][r];
+      }
+    __syncthreads();
+    d4 lacc[4];
+    gemm_xyT(Xf, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
+        st_sc1(AIJ + (size_t)row * L.N + col, lacc[s2][r]);
+      }
+    flow_publish(F.tile + I * T + J, epoch);
+  }
+  FLOW_T(3);
+  // (3) forward substitution: r = b_J - sum_{k in rs(J)} L_Jk y_k, the terms
+  // pushed by the children (fc[J][k]); y_J = L_JJ^-1 r; then this column's
+  // own terms L_IJ y_J for its rows I (fc[I][J]), published with the y flag
+  if (ok) ok = flow_wait_many(F.yf, S + so, sc, epoch, fail, &shf);
+  if (ok) {
+    if (t < kTB) {
+      double r = p.chol[L.b + J * kTB + t];
+      for (int q0 = 0; q0 < sc; q0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          v[u] = q0 + u < sc ? ld_sc1(p.chol + L.fc + ((size_t)J * T + S[so + q0 + u]) * kTB + t) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (q0 + u < sc) r -= v[u];
+      }
+      rv[t] = r;
+    }
+    __syncthreads();
+    // y_J[m] = sum_c L_JJ^-1[m][c] r[c]: thread (w, m) sums c in [16w, 16w + 16)
+    double s3 = 0.0;
+    for (int c = 16 * w; c < 16 * w + 16; ++c) s3 = __builtin_fma(Vkk[lane * kTB + c], rv[c], s3);
+    part[w][lane] = s3;
+    __syncthreads();
+    if (t < kTB) yv[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+    __syncthreads();
+    for (int q = 0; q < rc; ++q) {
+      const int I = S[ro + q];
+      const double* LIJ = A + (size_t)(I * kTB + lane) * L.N + J * kTB + 16 * w;
+      double la[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) la[c] = ld_sc1(LIJ + c);
+      double s4 = 0.0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) s4 = __builtin_fma(la[c], yv[16 * w + c], s4);
+      part[w][lane] = s4;
+      __syncthreads();
+      if (t < kTB)
+        st_sc1(p.chol + L.fc + ((size_t)I * T + J) * kTB + t,
+               ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
+      __syncthreads();
+    }
+    flow_publish(F.yf + J, epoch);
+  }
+  FLOW_T(4);
+  // (4) back substitution: thread (w, c = lane) sums rows [16w, 16w + 16)
+  if (ok) {
+    double s2 = 0.0;
+    for (int q = 0; q < rc && ok; ++q) {
+      const int I = S[ro + q];
+      ok = flow_wait(F.xf + I, epoch, fail, &shf);
+      if (!ok) break;
+      const double* LIJ = A + (size_t)(I * kTB + 16 * w) * L.N + J * kTB + lane;
+      const double* xI = p.chol + L.x + I * kTB + 16 * w;
+      double la[16], xa[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        la[m] = ld_sc1(LIJ + (size_t)m * L.N);
+        xa[m] = ld_sc1(xI + m);
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s2 = __builtin_fma(la[m], xa[m], s2);
+    }
+    FLOW_T(5);
+    if (ok) {
+      part[w][lane] = s2;
+      __syncthreads();
+      if (t < kTB) rv[t] = yv[t] - (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
+      __syncthreads();
+      double s3 = 0.0;  // x_J[c] = sum_m L_JJ^-1[m][c] r[m]
+      for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(Vkk[m * kTB + lane], rv[m], s3);
+      part[w][lane] = s3;
+      __syncthreads();
+      if (t < kTB) {
+        const double xv = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+        st_sc1(p.chol + L.x + J * kTB + t, xv);
+        const int orow = S[S[3] + J] * kTB + t;  // camera order (padded rows dropped)
+        if (orow < n) st_sc1(p.chol + L.xo + orow, xv);
+      }
+      flow_publish(F.xf + J, epoch);
+    }
+  }
+  FLOW_T(6);
+  // (5) ticket: the last column runs the epilogue
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) okf = ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1);
+  __syncthreads();
+  if (!okf) return;
+  const bool good = ld_flag(fail) == 0;
+  double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
+  for (int i = t; i < n; i += kTlWG) xs[i] = good ? ld_sc1(p.chol + L.xo + i) : 0.0;
+  __syncthreads();
+  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
+  const double* gvec = bvec + n;
+  solve_epilogue(p, xs, good, &part[0][0],
+                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+  FLOW_T(7);
+}
+
+static int g_cu_count = 0;
+
+static bool tl_flow_ok(const slam_ba_problem& p) {
+  if (p.tl_mode != 0 || p.tl_sched_host == nullptr || p.tl_sched_host[5] <= 0) return false;
+  if (g_cu_count == 0) {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = -1;
+    g_cu_count = cu;
+  }
+  const TlLayout L(9 * p.n_cams);
+  return L.T <= SLAM_TL_FLOW_MAX_T && L.T <= g_cu_count && 9 * p.n_cams <= 2 * kTB * kTB;
+}
+
+static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
+  const TlLayout L(9 * p.n_cams);
+  SLAM_REQUIRE(p.tl_sched_host[1] == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d",
+               p.tl_sched_host[1], L.T);
+  k_tl2_load<<<L.T * (L.T + 1) / 2, kTlWG, 0, s>>>(p);
+  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
+  k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p);
+  SLAM_LAUNCHED("k_tl3_flow");
+  return SLAM_OK;
 }
 
 static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
@@ -2359,6 +2801,7 @@ int check_problem(const slam_ba_problem* p) {
                "diagonal and every block with common points (packed)", kDenseMaxN);
   SLAM_REQUIRE(!p->tl_sched == !p->tl_sched_host,
                "slam_ba: tl_sched and tl_sched_host come together");
+  SLAM_REQUIRE(p->tl_mode == 0 || p->tl_mode == 1, "slam_ba: tl_mode must be 0 or 1");
   SLAM_REQUIRE(!sys_packed(p->n_cams) || p->chol != nullptr,
                "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
                kLdsMaxN);
@@ -2468,7 +2911,9 @@ static int launch_solve(const Launch& L, bool fuse_decide, hipStream_t s) {
     k_solve_blk<<<dim3(1, L.n), kBlkWG, L.solve_lds, s>>>(L.b);
     SLAM_LAUNCHED("k_solve_blk");
   } else {
-    if (L.b.p[0].tl_sched != nullptr) {
+    if (tl_flow_ok(L.b.p[0])) {
+      if (int rc = tl_solve_flow(L.b.p[0], s)) return rc;
+    } else if (L.b.p[0].tl_sched != nullptr) {
       if (int rc = tl_solve_levels(L.b.p[0], s)) return rc;
     } else {
       tl_solve(L.b.p[0], s);
@@ -2563,6 +3008,19 @@ extern "C" int slam_solve_trace(unsigned long long* out) {
 extern "C" int slam_linm_stamps(unsigned long long* out, int n) {
   SLAM_HIP(hipDeviceSynchronize());
   SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_linm_stamp), (size_t)n * 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif
+
+#ifdef SLAM_FLOW_PROFILE
+extern "C" int slam_flow_fac_stamps(unsigned long long* out16) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_flow_fac), 16 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+extern "C" int slam_flow_stamps(unsigned long long* out, int n_cols) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_flow_stamp), (size_t)n_cols * 8 * sizeof(unsigned long long)));
   return SLAM_OK;
 }
 #endif

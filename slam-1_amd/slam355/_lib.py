@@ -28,7 +28,7 @@ class BAProblemStruct(ctypes.Structure):
     _fields_ = [
         ("n_cams", c_i32), ("n_pts", c_i32), ("n_obs", c_i32), ("n_grps", c_i32),
         ("n_blocks", c_i32), ("n_cslots", c_i32), ("n_bslots", c_i32), ("lin_mode", c_i32),
-        ("n_sgrps", c_i32), ("reserved", c_i32),
+        ("n_sgrps", c_i32), ("tl_mode", c_i32),
         ("cams", c_p * 2), ("pts", c_p * 2), ("camrec", c_p * 2),
         ("obs_cam", c_p), ("obs_pt", c_p), ("obs_q", c_p), ("pt_ptr", c_p), ("grp_ptr", c_p),
         ("grp_cslot", c_p), ("cslot_cam", c_p), ("cslot_obs_ptr", c_p), ("cslot_obs", c_p),

@@ -154,8 +154,19 @@ def tl_schedule(n_cams, blocks):
     and the back substitution walks the levels in reverse.  A banded window of
     T tiles needs ~log2(T) levels instead of T sequential panel steps.
 
+    The same symbolic structure also drives the dataflow form of the solve
+    (csrc/ba.hip k_tl3_flow: one persistent workgroup per tile column, columns
+    wait for the tiles they need through device flags instead of launch
+    boundaries), whose per-column table is appended.
+
     Returns the int32 schedule (device and host copies are the same array):
-      [0] nlev, [1] T, [2] tperm offset, [3] itperm offset, [4] level table offset
+      [0] nlev, [1] T, [2] tperm offset, [3] itperm offset, [4] level table offset,
+      [5] column table offset
+      column table: per column J (rows_off, rows_cnt, rs_off, rs_cnt, upd_off)
+        rows: I > J with L_IJ != 0 (ascending); rs: k < J with L_Jk != 0
+        (ascending: the updates of the diagonal tile and the forward
+        substitution); upd: per row I, (koff, kcnt) -- the k < J with L_Ik and
+        L_Jk both nonzero
       level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
@@ -196,7 +207,7 @@ def tl_schedule(n_cams, blocks):
             level[parent[k]] = max(level[parent[k]], level[k] + 1)
     nlev = max(level) + 1 if T else 0
     cols = [[k for k in range(T) if level[k] == lv] for lv in range(nlev)]
-    head = [nlev, T, 0, 0, 0]
+    head = [nlev, T, 0, 0, 0, 0]
     table, body = [], []
     lists = []  # (k lists / struct lists) appended after the entries
 
@@ -249,7 +260,29 @@ def tl_schedule(n_cams, blocks):
             ents += [k, list_offs[li], len(lists[li])]
         table += [po, len(pan[lv]), uo, len(upd[lv]), bo, len(bk[lv])]
     flat = head + tperm.tolist() + itperm.tolist() + table + ents + [v for li in lists for v in li]
-    return np.asarray(flat, np.int32)
+    # column table of the dataflow solve
+    rs = [[k for k in range(J) if J in struct[k]] for J in range(T)]
+    flow_off = len(flat)
+    flat[5] = flow_off
+    recs = [0] * (5 * T)
+    tail = []
+    base = flow_off + 5 * T
+
+    def put(vals):
+        tail.extend(vals)
+        return base + len(tail) - len(vals)
+
+    for J in range(T):
+        rows = sorted(struct[J])
+        r_off = put(rows)
+        s_off = put(rs[J])
+        pairs = []
+        for I in rows:
+            ks = [k for k in rs[J] if I in struct[k]]
+            pairs.append((put(ks), len(ks)))
+        u_off = put([v for pr in pairs for v in pr])
+        recs[5 * J:5 * J + 5] = [r_off, len(rows), s_off, len(rs[J]), u_off]
+    return np.asarray(flat + recs + tail, np.int32)
 
 
 def _pairs_by_point(cam_idx, pt_idx):
@@ -600,13 +633,19 @@ class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
-                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_levels=True):
+                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_levels=True,
+                 tl_mode="flow"):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
         every point is seen by <= MF_CAMS cameras).  tl_levels: the tiled
         camera solve (9C > 120) runs the nested-dissection level schedule
-        (tl_schedule); False keeps one panel step per tile column."""
+        (tl_schedule); False keeps one panel step per tile column.  tl_mode
+        (with the schedule): "flow" runs it as one dataflow launch (k_tl3_flow;
+        the library falls back to levels when the tile count exceeds the CU
+        count), "levels" one launch pair per elimination-tree level."""
+        if tl_mode not in ("flow", "levels"):
+            raise ValueError(f"tl_mode must be 'flow' or 'levels', not {tl_mode!r}")
         dev = require_gpu()
         cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
         pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
@@ -663,6 +702,7 @@ class BAProblem:
         s.n_blocks = len(pl["blocks"])
         s.n_cslots, s.n_bslots = n_cs, n_bs
         s.lin_mode, s.n_sgrps = pl["mode"], pl["n_sgrps"]
+        s.tl_mode = 0 if tl_mode == "flow" else 1
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()

@@ -277,8 +277,9 @@ def test_gpu_local_ba_config3_converges(C, P, k):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["flow", "levels"])
 @pytest.mark.parametrize("C,P,k", [(14, 400, 4), (40, 1500, 5), (130, 3000, 6)])
-def test_gpu_tiled_solver_iterates_match_oracle(C, P, k):
+def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
     """9C > 120: the reduced camera system goes through the tiled Cholesky
     (k_tl_*; 2, 6 and 19 tiles of 64).  The 130-camera trajectory window is
     block-banded (points seen by 6 consecutive keyframes), so most tiles stay
@@ -291,7 +292,7 @@ def test_gpu_tiled_solver_iterates_match_oracle(C, P, k):
     cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
     cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
     pts0 = pts + rng.normal(0, 0.05, pts.shape)
-    prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs, tl_mode=mode)
     st = oba.LMState(1e-4)
     oc, op = cams0.copy(), pts0.copy()
     pairs = oba._obs_pairs(ci, pi)
@@ -628,6 +629,76 @@ def test_tl_level_schedule_solves_the_camera_system(C, loop):
     S = M + M.T + np.diag(np.abs(M).sum(1) + np.abs(M).sum(0) + 1.0)
     b = rng.normal(size=n)
     x = _emulate_tl_levels(S, b, sched)
+    assert np.allclose(x, np.linalg.solve(S, b), rtol=0, atol=1e-10 * np.abs(x).max())
+
+
+def _emulate_tl_flow(S, b, sched):
+    """The dataflow tiled solve (csrc/ba.hip k_tl3_flow) restated in NumPy,
+    column by column from the schedule's column table: the diagonal tile's
+    updates over rs(J), its factor and inverse, y_J; each row tile's updates
+    over its k list and L_IJ = A_IJ L_JJ^-T; then x_J from the rows' x_I."""
+    T = int(sched[1])
+    tperm = sched[sched[2]:sched[2] + T]
+    fo = int(sched[5])
+    rec = sched[fo:fo + 5 * T].reshape(-1, 5)
+    n, TB = len(b), 64
+    N = T * TB
+    rn = tperm[np.arange(N) // TB] * TB + np.arange(N) % TB
+    A = np.zeros((N, N))
+    A[np.ix_(rn[:n], rn[:n])] = S
+    A[rn[n:], rn[n:]] = 1.0
+    bb = np.zeros(N)
+    bb[rn[:n]] = b
+    t = lambda I: slice(I * TB, (I + 1) * TB)  # noqa: E731
+    dinv, y, x = {}, np.zeros(N), np.zeros(N)
+    for J in range(T):
+        ro, rc, so, sc, uo = rec[J]
+        rs = sched[so:so + sc]
+        for k in rs:
+            A[t(J), t(J)] -= A[t(J), t(k)] @ A[t(J), t(k)].T
+        dinv[J] = np.linalg.inv(np.linalg.cholesky(A[t(J), t(J)]))
+        r = bb[t(J)] - sum((A[t(J), t(k)] @ y[t(k)] for k in rs), np.zeros(TB))
+        y[t(J)] = dinv[J] @ r
+        for q, I in enumerate(sched[ro:ro + rc]):
+            ko, kc = sched[uo + 2 * q], sched[uo + 2 * q + 1]
+            for k in sched[ko:ko + kc]:
+                A[t(I), t(J)] -= A[t(I), t(k)] @ A[t(J), t(k)].T
+            A[t(I), t(J)] = A[t(I), t(J)] @ dinv[J].T
+    for J in reversed(range(T)):
+        ro, rc = rec[J][:2]
+        r = y[t(J)].copy()
+        for I in sched[ro:ro + rc]:
+            assert I > J
+            r -= A[t(I), t(J)].T @ x[t(I)]
+        x[t(J)] = dinv[J].T @ r
+    return x[rn[:n]]
+
+
+@pytest.mark.parametrize("C,loop", [(30, False), (64, False), (120, True), (500, True)])
+def test_tl_flow_table_solves_the_camera_system(C, loop):
+    """Column table of the dataflow tiled solve: every dependency of column J
+    is an earlier column (no waits on later workgroups before the back
+    substitution), and executing it column by column solves S x = b."""
+    from slam355.ba import tl_schedule, upper_blocks
+    from slam355.synthetic import ba_problem, ba_problem_loop
+
+    rng = np.random.default_rng(C + 1)
+    cams, pts, ci, pi, qs = (ba_problem_loop if loop else ba_problem)(rng, C, 20 * C, 5)
+    ub = upper_blocks(C, ci, pi)
+    iu, ju = np.triu_indices(C)
+    blocks = np.stack([iu[ub], ju[ub]], 1)
+    sched = tl_schedule(C, blocks)
+    T = int(sched[1])
+    rec = sched[sched[5]:sched[5] + 5 * T].reshape(-1, 5)
+    for J, (ro, rc, so, sc, uo) in enumerate(rec):
+        assert all(I > J for I in sched[ro:ro + rc]) and all(k < J for k in sched[so:so + sc])
+    n = 9 * C
+    M = np.zeros((n, n))
+    for c1, c2 in blocks:
+        M[9 * c1:9 * c1 + 9, 9 * c2:9 * c2 + 9] = rng.normal(size=(9, 9))
+    S = M + M.T + np.diag(np.abs(M).sum(1) + np.abs(M).sum(0) + 1.0)
+    b = rng.normal(size=n)
+    x = _emulate_tl_flow(S, b, sched)
     assert np.allclose(x, np.linalg.solve(S, b), rtol=0, atol=1e-10 * np.abs(x).max())
 
 
