@@ -418,7 +418,8 @@ def tracked_window_ba(feed, B, rig, args, n_pairs=8):
     prob = BAProblem(cams, pts, ci, pi, qs)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    cost0 = prob.state()["COST"]
+    prob.iterate(1)
+    cost0 = prob.state()["COST"]  # at the initial parameters
     prob.iterate_graphed(args.ba_iters)  # capture + warm
     prob.restore()
     torch.cuda.synchronize()
@@ -538,7 +539,7 @@ def run_ba(args, world, rank):
                          block_list=upper_blocks(C, ci, pi))
         step_fn = prob.step_distributed
     else:
-        prob = BAProblem(c0, p0, ci, pi, qs)
+        prob = BAProblem(c0, p0, ci, pi, qs, chunks_per_wg=args.chunks_per_wg)
         if args.no_graph:
             step_fn = lambda: prob.iterate(1)  # noqa: E731
         else:  # one LM iteration = one HIP-graph replay (3T + 5 launches for the tiled solver)

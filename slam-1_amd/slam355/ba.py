@@ -463,7 +463,9 @@ def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=Non
     cntn = np.diff(pt_ptr).tolist()
     n_chunks_est = max(1, -(-O // MF_CHUNK_OBS))
     if chunks_per_wg is None:  # enough workgroups to cover the chip, fewer partial rows
-        chunks_per_wg = int(min(8, max(1, n_chunks_est // 512)))
+        # (a C3 window, ~310 chunks, is batched with others: 3 chunks per
+        # workgroup measured best -- 1/3 of the partial-row traffic, r2 sweep)
+        chunks_per_wg = int(min(8, max(3 if n_chunks_est >= 256 else 1, n_chunks_est // 512)))
     S = max(1, int(chunks_per_wg))
     grp = [0]
     sg = [0]
@@ -765,19 +767,47 @@ class BAProblem:
                                torch.cuda.current_stream()):
             graphs[n].replay()
 
-    def step_distributed(self, group=None):
+    def _phase_graph(self, name, fn):
+        """A captured HIP graph of one launch phase (captured on first use)."""
+        graphs = self.__dict__.setdefault("_phase_graphs", {})
+        if name not in graphs:
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            saved = self.stream
+            self.stream = s
+            try:
+                with torch.cuda.graph(g, stream=s):
+                    fn()
+            finally:
+                self.stream = saved
+            torch.cuda.current_stream().wait_stream(s)
+            graphs[name] = g
+        return graphs[name]
+
+    def step_distributed(self, group=None, graphed=True):
         """One LM iteration with RCCL all-reduce of the camera system (multi-rank).
 
         The kernels and the collectives are ordered on one stream: the body runs
         with self.stream current (torch.distributed orders its work against the
-        current stream)."""
+        current stream).  graphed: the linearisation (k_lin_mfma + k_assemble)
+        and the solve (tiled factor + k_back_trial) are each one HIP-graph
+        replay, so an iteration is 2 graph launches + k_decide + 2 collectives
+        instead of ~8 kernel launches."""
         import torch.distributed as dist
 
         with torch.cuda.stream(self.stream if self.stream is not None
                                else torch.cuda.current_stream()):
-            self.build_system()
-            dist.all_reduce(self.t["sys"], group=group)
-            self.solve_step()
+            if graphed:
+                build = self._phase_graph("build", self.build_system)
+                solve = self._phase_graph("solve", self.solve_step)
+                build.replay()
+                dist.all_reduce(self.t["sys"], group=group)
+                solve.replay()
+            else:
+                self.build_system()
+                dist.all_reduce(self.t["sys"], group=group)
+                self.solve_step()
             dist.all_reduce(self.t["small"], group=group)
             self.decide()
 
