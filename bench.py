@@ -231,8 +231,23 @@ def run_tracking(args, world, rank):
     if trk_stream is None and args.priority == "track":
         trk_stream = torch.cuda.Stream(priority=-1)
         trk_stream.destroy = lambda: None
+    orb_stream = None
+    if args.orb_pipeline and trk_stream is None:
+        # tracking on an explicit stream: a CU-masked stream is a blocking stream,
+        # which would serialise with work on the legacy null stream
+        trk_stream = torch.cuda.Stream()
+        trk_stream.destroy = lambda: None
+    if args.orb_pipeline:  # ORB of batch k+1 overlaps the matching / PnP tail of batch k
+        if args.orb_cus:  # ORB kept off the last CUs (left to the latency-bound BA kernels)
+            orb_stream = masked_stream(args.orb_cus)
+        else:
+            orb_stream = torch.cuda.Stream(priority=-1 if args.priority == "track" else 0)
+    if args.solve_lds_floor:
+        from slam355 import _lib as slib
+
+        slib.call("slam_ba_set_solve_lds_floor", int(args.solve_lds_floor))
     trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
-                  stream=trk_stream)
+                  stream=trk_stream, orb_stream=orb_stream)
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
     n_solves = max(1, B // args.ba_every)
@@ -270,13 +285,16 @@ def run_tracking(args, world, rank):
 
     def tracked_step(marks):
         tmarks = [] if marks is not None else None
-        imgs, win = feed.next(tstream)
+        ist = orb_stream if orb_stream is not None else tstream  # the stream that reads imgs
+        imgs, win = feed.next(ist)
         if win == 0:  # a new pass over the sequence starts at frame 0
             trk.reset_chain()
         if args.ba_overlap == "after-orb" and ba_done[0] is not None:
-            tstream.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
+            ist.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
         trk.track(win * B, imgs=imgs, marks=tmarks)
-        feed.release(tstream)
+        feed.release(ist)
+        if tmarks is not None and orb_stream is not None:
+            marks["orb"] = trk.orb_marks  # ORB's own stream: start -> done there
         if marks is None and args.keep_poses:
             all_poses[win] = trk.poses.clone()
         if args.ba_overlap == "after-orb":
@@ -363,6 +381,8 @@ def run_tracking(args, world, rank):
                    "high_priority_stream": args.priority,
                    "ba_overlap": args.ba_overlap,
                    "tracking_cus": args.track_cus or "all",
+                   "orb_stream": (f"pipelined, CUs 0..{args.orb_cus - 1}" if args.orb_cus else
+                                  "pipelined, all CUs") if args.orb_pipeline else "tracking stream",
                    "local_ba_cus": args.ba_cus or "all"},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
@@ -385,6 +405,8 @@ def run_tracking(args, world, rank):
         trk_stream.destroy()
     if hasattr(ba_stream, "destroy"):
         ba_stream.destroy()
+    if hasattr(orb_stream, "destroy"):
+        orb_stream.destroy()
     if not args.no_ba_scale:
         # the metric's second half: local-BA LM iterations/s of ONE C4 window
         # sharded over all ranks (landmarks by anchor keyframe, RCCL all-reduce
@@ -828,6 +850,17 @@ def main():
                     help="restrict the tracking stream to this many CUs (0: all); the rest run "
                          "only local-BA work, whose latency-bound kernels then do not share "
                          "SIMDs and LDS with ORB workgroups")
+    ap.add_argument("--no-orb-pipeline", dest="orb_pipeline", action="store_false",
+                    help="tracking: ORB on the tracking stream (default: ORB on its own stream "
+                         "into double-buffered outputs, so the next batch's ORB overlaps this "
+                         "batch's matching / PnP tail)")
+    ap.add_argument("--orb-cus", type=int, default=216,
+                    help="ORB pipeline: ORB's stream may use only the first N CUs (0: all); the "
+                         "rest are left to the latency-bound local-BA and tracking-tail kernels "
+                         "(r2 sweep: 224 -> 10.6k, 208 -> 10.7k, 192 -> 10.5k, all -> 10.0k frames/s)")
+    ap.add_argument("--solve-lds-floor", type=int, default=0,
+                    help="LDS bytes the one-workgroup camera solve requests at least "
+                         "(slam_ba_set_solve_lds_floor)")
     ap.add_argument("--no-tracked-ba", action="store_true",
                     help="tracking: skip the local BA of a window built from tracked frames")
     ap.add_argument("--ba-cus", type=int, default=0,

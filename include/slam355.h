@@ -393,6 +393,13 @@ int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream);
  * are the ones slam_ba_iterate gives it alone.  Batched problems must use the
  * one-workgroup solver (9C <= 120); a packed problem iterates on its own. */
 int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, int n_iter, void* stream);
+
+/* Minimum dynamic LDS (bytes, <= 160 KiB) the one-workgroup camera solve
+ * (9C <= 120) requests; 0 (default) = what it needs.  A floor above what
+ * co-resident workgroups of other streams leave (e.g. > 80 KiB beside an ORB
+ * workgroup) keeps its latency-bound pivot chain on CUs of its own.  Process-wide;
+ * takes effect at the next launch (and is baked into graphs captured after). */
+int slam_ba_set_solve_lds_floor(int bytes);
 int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0, void* stream);
 
 /* ------------------------------------------------------------------ pose chain

@@ -2859,6 +2859,11 @@ struct Launch {
   bool dense;
 };
 
+// LDS floor of the one-workgroup camera solve (slam_ba_set_solve_lds_floor): a
+// floor above what a co-resident ORB workgroup leaves keeps the latency-bound
+// pivot chain off CUs whose SIMDs are busy with ORB waves.
+static size_t g_solve_lds_floor = 0;
+
 static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
   SLAM_REQUIRE(n >= 1 && n <= kBaMaxBatch, "slam_ba: batch of %d problems (1..%d)", n, kBaMaxBatch);
   SLAM_REQUIRE(probs != nullptr, "slam_ba: null problem array");
@@ -2879,6 +2884,7 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
     L->max_sgrps = max(L->max_sgrps, probs[i].n_sgrps);
     L->max_blocks = max(L->max_blocks, probs[i].n_blocks);
     L->solve_lds = std::max(L->solve_lds, sizeof(double) * BlkLds(9 * probs[i].n_cams).total);
+    L->solve_lds = std::max(L->solve_lds, g_solve_lds_floor);
     L->dense = L->dense && !sys_packed(probs[i].n_cams);
   }
   SLAM_REQUIRE(n == 1 || L->dense,
@@ -2929,6 +2935,12 @@ static int launch_solve(const Launch& L, bool fuse_decide, hipStream_t s) {
 }
 
 }  // namespace
+
+extern "C" int slam_ba_set_solve_lds_floor(int bytes) {
+  SLAM_REQUIRE(bytes >= 0 && bytes <= 160 * 1024, "slam_ba_set_solve_lds_floor: %d B", bytes);
+  g_solve_lds_floor = (size_t)bytes;
+  return SLAM_OK;
+}
 
 extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* stream) {
   return slam_ba_reset_batch(prob, 1, lambda0, stream);

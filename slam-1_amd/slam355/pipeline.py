@@ -25,7 +25,10 @@ class Tracker:
     """Device buffers for batches of B frame pairs of H x W images."""
 
     def __init__(self, B, H, W, P_l, P_r, max_kp_per_tile=56, seed=0, max_distance=500.0,
-                 stream=None):
+                 stream=None, orb_stream=None):
+        """orb_stream: run ORB on that stream into two alternating workspaces, so
+        the ORB of the next batch overlaps the matching / PnP tail of this one
+        (the tail kernels are latency-bound and leave most CUs idle)."""
         self.dev = require_gpu()
         self.B, self.H, self.W = B, H, W
         self.max_kp = max_kp_per_tile
@@ -41,6 +44,12 @@ class Tracker:
         self.tK = torch.as_tensor(self.K, device=d).contiguous()
         # ORB on 2B+1 images: left_0..left_B then right_0..right_{B-1}
         self.ows = orb.OrbWorkspace(2 * B + 1, H, W, max_kp_per_tile)
+        self.orb_stream = orb_stream
+        if orb_stream is not None:  # double-buffered ORB outputs
+            self.ows_pair = [self.ows, orb.OrbWorkspace(2 * B + 1, H, W, max_kp_per_tile)]
+            self.orb_done = [torch.cuda.Event() for _ in range(2)]
+            self.slot_free = [torch.cuda.Event() for _ in range(2)]
+            self._k = 0
         cap = self.cap = self.ows.kp_cap
         i32 = dict(dtype=torch.int32, device=d)
         f64 = dict(dtype=torch.float64, device=d)
@@ -104,13 +113,37 @@ class Tracker:
                 ev.record(st if st is not None else torch.cuda.current_stream())
                 marks.append((name, ev))
 
-        mark("start")
-        kp, octv, desc, cnt = self.ows.run(im, st)
-        with torch.cuda.stream(st if st is not None else torch.cuda.current_stream()):
-            torch.minimum(self.orb_min, cnt.amin(), out=self.orb_min)
-        # ORB of this batch done: a caller may hold other work back until here
-        self.orb_event.record(st if st is not None else torch.cuda.current_stream())
-        mark("orb")
+        main = st if st is not None else torch.cuda.current_stream()
+        ost = self.orb_stream
+        if ost is None:
+            mark("start")
+            kp, octv, desc, cnt = self.ows.run(im, st)
+            with torch.cuda.stream(main):
+                torch.minimum(self.orb_min, cnt.amin(), out=self.orb_min)
+            # ORB of this batch done: a caller may hold other work back until here
+            self.orb_event.record(main)
+            mark("orb")
+        else:
+            slot = self._k % 2
+            self._k += 1
+            self.ows = ows = self.ows_pair[slot]
+            ost.wait_event(self.slot_free[slot])  # the tail that read this slot is done
+            if imgs is None:  # self.imgs was filled on `main`; a caller passing `imgs`
+                ost.wait_stream(main)  # orders their upload against `orb_stream` itself
+            if marks is not None:  # ORB's own lane: start (past the waits) -> done
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(ost)
+            kp, octv, desc, cnt = ows.run(im, ost)
+            with torch.cuda.stream(ost):
+                torch.minimum(self.orb_min, cnt.amin(), out=self.orb_min)
+            if marks is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(ost)
+                self.orb_marks = [("start", e0), ("orb", e1)]
+            self.orb_event.record(ost)
+            self.orb_done[slot].record(ost)
+            main.wait_event(self.orb_done[slot])
+            mark("orb_wait")
         kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
         nL, nR = cnt[0:B], cnt[B + 1:2 * B + 1]
@@ -141,6 +174,8 @@ class Tracker:
                                 gate=self.max_distance, out=(self.t_pairs, self.t_cnt), stream=st)
         geometry.gather_temporal(self.X, self.f_ptl, kpL1, self.t_pairs, self.t_cnt,
                                  out=(self.Q1, self.q2, self.q1), stream=st)
+        if ost is not None:  # the last read of this slot's ORB outputs
+            self.slot_free[slot].record(main)
         mark("triangulate_temporal")
         # PnP-RANSAC (transformation.py:11-13)
         geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,

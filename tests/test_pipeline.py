@@ -276,3 +276,38 @@ def test_gpu_tracked_frames_feed_local_ba(request, B):
         assert abs((info["cost"] - s["COST_NEW"]) - dec) <= 1e-5 * abs(dec), it
         gc, gp = prob.params()
         assert np.allclose(gc, oc, rtol=1e-6, atol=1e-8), it
+
+
+@pytest.mark.gpu
+def test_gpu_orb_pipelined_tracker_equals_serial():
+    """Tracker(orb_stream=...): ORB of batch k+1 on its own stream into the other
+    of two workspaces while batch k's matching / PnP runs -- the same poses,
+    counts and chained trajectory as the one-stream tracker, batch by batch."""
+    import torch
+    from slam355.pipeline import Tracker
+    from slam355.synthetic import corridor_sequence
+
+    B, nb = 4, 3
+    L, R, poses, rig = corridor_sequence(B * nb + 1, 1280, 720, seed=33)
+    packs = [torch.from_numpy(np.concatenate([L[k * B:k * B + B + 1], R[k * B:k * B + B]])).cuda()
+             for k in range(nb)]
+    ref = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=2)
+    pip = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=2,
+                  stream=torch.cuda.Stream(), orb_stream=torch.cuda.Stream())
+    got, exp = [], []
+    for k in range(nb):
+        ref.track(k * B, imgs=packs[k])
+        exp.append((ref.rvec.clone(), ref.tvec.clone(), ref.p_ninl.clone(), ref.poses.clone(),
+                    ref.t_cnt.clone()))
+    torch.cuda.synchronize()
+    for k in range(nb):  # enqueued back to back: batch k+1's ORB overlaps batch k
+        with torch.cuda.stream(pip.stream):
+            pip.track(k * B, imgs=packs[k])
+            got.append((pip.rvec.clone(), pip.tvec.clone(), pip.p_ninl.clone(),
+                        pip.poses.clone(), pip.t_cnt.clone()))
+    torch.cuda.synchronize()
+    for k in range(nb):
+        for a, b in zip(got[k], exp[k]):
+            assert torch.equal(a, b), k
+    ref.check()
+    pip.check()
