@@ -3,12 +3,14 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload tracking|ba|matcher]
 
 Default workload ("tracking", BASELINE.json metric "frames/sec tracking+local-BA
-@1280x720"): one step = B synthetic 1280x720 stereo frame pairs through the
-whole tracking hot path (ORB on 2B+1 images with 56 kp/tile = 2016 kp/frame,
-stereo kNN-2 + ratio, F-LMedS, triangulation, temporal kNN-2 + gate, PnP-RANSAC,
-host pose chain) plus the local bundle adjustment it schedules: every
-`ba_every` frames one LM solve of `ba_iters` iterations over a C3-shaped window
-(10 keyframes x 5k points x 30k observations).  N > 1: one process per GPU,
+@1280x720"): one step = B synthetic 1280x720 stereo frame pairs, streamed from
+pinned host memory inside the timed region, through the whole tracking hot
+path (ORB on 2B+1 images with 64 kp/tile ~ 2075 kp/frame, on its own CU-masked
+stream pipelined against the previous batch's tail; stereo kNN-2 + ratio,
+F-LMedS, triangulation, temporal kNN-2 + gate, PnP-RANSAC, device pose chain)
+plus the local bundle adjustment it schedules: every `ba_every` frames one LM
+solve of `ba_iters` iterations over a C3-shaped window (10 keyframes x 5k
+points x 30k observations), the step's windows batched.  N > 1: one process per GPU,
 each with its own frame shard and its own BA windows (weak scaling; no
 collective on this path).  `--workload ba` measures local-BA LM iterations/s:
 C3 on one GPU, or C4 (64 KF x 50k points) sharded by landmark over the ranks

@@ -16,12 +16,13 @@ from slam355.ba import BABatch, BAProblem  # noqa: E402
 from slam355.synthetic import ba_problem, perturb  # noqa: E402
 
 nb = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+cpw = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # phases are per chunk: 1 chunk per WG
 rng = np.random.default_rng(0)
 probs = []
 for _ in range(nb):
     cams, pts, ci, pi, qs = ba_problem(rng, 10, 5000, 6)
     c0, p0 = perturb(rng, cams, pts)
-    probs.append(BAProblem(c0, p0, ci, pi, qs))
+    probs.append(BAProblem(c0, p0, ci, pi, qs, chunks_per_wg=cpw))
 bat = BABatch(probs)
 fn = _lib.lib.slam_linm_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]

@@ -537,10 +537,15 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
 constexpr int kSgMeta = 24;  // sg_meta record: ch0 ch1 cs0 m bs0 nb p0 p1 o0 o1 cams[8] pad
+constexpr int kMObsS = kMObs + 1;  // odd stride: element-major arrays read across lanes without conflicts
 struct MLds {
-  double jc[kMObs][18];          // Jc rows (2 x 9)
-  double jp[kMObs][6];           // Jp rows (2 x 3)
-  double ru[kMObs][4];           // r0 r1 u0 u1
+  // per-observation values stored element-major ([value][obs], stride 121):
+  // lanes taking consecutive observations touch consecutive doubles, and the
+  // 16 lanes of an MFMA operand group (one observation, 16 values) stride by
+  // an odd number of doubles (was [obs][18]: 3 LDS conflict cycles per access)
+  double jc[18][kMObsS];         // Jc rows (2 x 9)
+  double jp[6][kMObsS];          // Jp rows (2 x 3)
+  double ru[4][kMObsS];          // r0 r1 u0 u1
   double vi[kMPts][6];           // V*^-1 (i00 i01 i02 i11 i12 i22)
   double e[kMPts][3];
   double yt[kMPts][3][kMRows];   // Y_p, [point][k][row]: the MFMA A operand
@@ -628,47 +633,67 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   for (int s = 0; s < 2; ++s) zacc[s] = d4{0.0, 0.0, 0.0, 0.0};
   const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
 
-  // chunk extents: the first from the record, the next loaded one chunk ahead
+  // chunk extents: the first from the record, the next loaded one chunk ahead;
+  // a chunk's inputs are loaded one chunk ahead too (issued after the current
+  // chunk is staged, in flight across its phases: barriers wait on LDS only)
+  struct ChunkIn {
+    double q0, q1, xv;
+    int meta, pp, cp;
+  };
+  auto load_in = [&](int ch, int p0, int p1, int o0, int o1) {
+    ChunkIn in{0.0, 0.0, 0.0, 0, 0, 0};
+    const int nobs = o1 - o0, npts = p1 - p0;
+    if (t < nobs) {
+      in.q0 = p.obs_q[2 * (o0 + t)];
+      in.q1 = p.obs_q[2 * (o0 + t) + 1];
+      in.meta = p.obs_meta[o0 + t];
+    }
+    if (t < 3 * npts) in.xv = p.pts[cur][3 * p0 + t];
+    if (t >= 128 && t - 128 <= npts) in.pp = p.pt_ptr[p0 + t - 128] - o0;
+    if (t < 8) in.cp = p.chk_cptr[8 * ch + t];
+    return in;
+  };
   int p0 = sm[6], p1 = sm[7], o0 = sm[8], o1 = sm[9];
+  int np0 = 0, np1 = 0, no0 = 0, no1 = 0;
+  if (ch0 + 1 < ch1) {
+    np0 = p.grp_ptr[ch0 + 1];
+    np1 = p.grp_ptr[ch0 + 2];
+    no0 = p.chk_optr[ch0 + 1];
+    no1 = p.chk_optr[ch0 + 2];
+  }
+  ChunkIn in = load_in(ch0, p0, p1, o0, o1);
   for (int ch = ch0; ch < ch1; ++ch) {
     const int nobs = o1 - o0, npts = p1 - p0;
-    int np0 = 0, np1 = 0, no0 = 0, no1 = 0;
-    if (ch + 1 < ch1) {
-      np0 = p.grp_ptr[ch + 1];
-      np1 = p.grp_ptr[ch + 2];
-      no0 = p.chk_optr[ch + 1];
-      no1 = p.chk_optr[ch + 2];
-    }
-    // this chunk's inputs, all issued before any is used
-    double q0 = 0.0, q1 = 0.0;
-    int meta = 0;
-    if (t < nobs) {
-      q0 = p.obs_q[2 * (o0 + t)];
-      q1 = p.obs_q[2 * (o0 + t) + 1];
-      meta = p.obs_meta[o0 + t];
-    }
-    double xv = 0.0;
-    if (t < 3 * npts) xv = p.pts[cur][3 * p0 + t];
-    int pp = 0;
-    if (t >= 128 && t - 128 <= npts) pp = p.pt_ptr[p0 + t - 128] - o0;
-    const int cp = t < 8 ? p.chk_cptr[8 * ch + t] : 0;
+    const double q0 = in.q0, q1 = in.q1;
     __syncthreads();  // the previous chunk's readers are done with L
     if (t < nobs) {
-      L.lpt[t] = meta & 255;
-      L.la[t] = (meta >> 8) & 255;
-      L.cobs[t] = meta >> 16;
+      L.lpt[t] = in.meta & 255;
+      L.la[t] = (in.meta >> 8) & 255;
+      L.cobs[t] = in.meta >> 16;
     }
-    if (t < 3 * npts) (&L.X[0][0])[t] = xv;
-    if (t >= 128 && t - 128 <= npts) L.optr[t - 128] = pp;
-    if (t < 8) L.cptr[t] = cp;
+    if (t < 3 * npts) (&L.X[0][0])[t] = in.xv;
+    if (t >= 128 && t - 128 <= npts) L.optr[t - 128] = in.pp;
+    if (t < 8) L.cptr[t] = in.cp;
     // Y/W operand planes of the chunk's points start at zero (rows of cameras
     // a point is not seen by, rows >= 9m)
     for (int i = t; i < npts * 3 * 16 * nt; i += kMWG) {
       const int row = i % (16 * nt), pk = i / (16 * nt);
-      (&L.yt[0][0][0])[pk * kMRows + row] = 0.0;
-      (&L.wt[0][0][0])[pk * kMRows + row] = 0.0;
+      const int pos = (row + 16 * (pk % 3)) & (kMRows - 1);  // plane rotation, see (D)
+      (&L.yt[0][0][0])[pk * kMRows + pos] = 0.0;
+      (&L.wt[0][0][0])[pk * kMRows + pos] = 0.0;
     }
     __syncthreads();
+    // prefetch: the next chunk's inputs and the extents of the one after
+    int nnp0 = 0, nnp1 = 0, nno0 = 0, nno1 = 0;
+    if (ch + 1 < ch1) {
+      in = load_in(ch + 1, np0, np1, no0, no1);
+      if (ch + 2 < ch1) {
+        nnp0 = p.grp_ptr[ch + 2];
+        nnp1 = p.grp_ptr[ch + 3];
+        nno0 = p.chk_optr[ch + 2];
+        nno1 = p.chk_optr[ch + 3];
+      }
+    }
     LINM_T(1);
     // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350)
     if (t < nobs) {
@@ -679,10 +704,10 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) L.jc[t][9 * a + i] = J[a][i];
+        for (int i = 0; i < 9; ++i) L.jc[9 * a + i][t] = J[a][i];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) L.jp[t][3 * a + c] = J[a][9 + c];
-        L.ru[t][a] = r[a];
+        for (int c = 0; c < 3; ++c) L.jp[3 * a + c][t] = J[a][9 + c];
+        L.ru[a][t] = r[a];
       }
     }
     __syncthreads();
@@ -694,8 +719,8 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       for (int k = L.optr[t]; k < L.optr[t + 1]; ++k) {
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
-          const double j0 = L.jp[k][3 * a], j1 = L.jp[k][3 * a + 1], j2 = L.jp[k][3 * a + 2];
-          const double rr = L.ru[k][a];
+          const double j0 = L.jp[3 * a][k], j1 = L.jp[3 * a + 1][k], j2 = L.jp[3 * a + 2][k];
+          const double rr = L.ru[a][k];
           V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
           V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
           g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
@@ -751,7 +776,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
             if (ib + i >= ie) break;
 #pragma unroll
             for (int c = 0; c < 3; ++c)
-              W[i][c] += L.jc[k][ib + i] * L.jp[k][c] + L.jc[k][9 + ib + i] * L.jp[k][3 + c];
+              W[i][c] += L.jc[ib + i][k] * L.jp[c][k] + L.jc[9 + ib + i][k] * L.jp[3 + c][k];
           }
         }
         const double* vi = L.vi[lp];
@@ -762,20 +787,24 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
           const int row = 9 * a + ib + i;
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            L.wt[lp][c][row] = W[i][c];
-            L.yt[lp][c][row] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
+            const int pos = (row + 16 * c) & (kMRows - 1);
+            L.wt[lp][c][pos] = W[i][c];
+            L.yt[lp][c][pos] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
           }
         }
       }
       if (h == 0 && k0 < nobs) {
         const double* e = L.e[L.lpt[k0]];
-        L.ru[k0][2] = L.jp[k0][0] * e[0] + L.jp[k0][1] * e[1] + L.jp[k0][2] * e[2];
-        L.ru[k0][3] = L.jp[k0][3] * e[0] + L.jp[k0][4] * e[1] + L.jp[k0][5] * e[2];
+        L.ru[2][k0] = L.jp[0][k0] * e[0] + L.jp[1][k0] * e[1] + L.jp[2][k0] * e[2];
+        L.ru[3][k0] = L.jp[3][k0] * e[0] + L.jp[4][k0] * e[1] + L.jp[5][k0] * e[2];
       }
     }
     __syncthreads();
     LINM_T(4);
-    // (D) T += Y_p W_p^T, one MFMA per point and tile:
+    // (D) T += Y_p W_p^T, one MFMA per point and tile (operand plane k stores
+    //     row r at (r + 16k) mod 64, so the 16-lane groups k = 0, 1 of an
+    //     operand read fall on different LDS banks -- a 64-double k stride
+    //     would put them on the same ones):
     //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0.
     //     Every wave issues 3 tile MFMAs per point (a wave with 2 tiles feeds
     //     its third accumulator zeros), so the accumulators stay in their own
@@ -788,8 +817,8 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
         const int lp = min(lp0 + u, kMPts - 1);
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
-          av[u][s] = L.yt[lp][mkc][tRow[s]];
-          bv[u][s] = L.wt[lp][mkc][tCol[s]];
+          av[u][s] = L.yt[lp][mkc][(tRow[s] + 16 * mkc) & (kMRows - 1)];
+          bv[u][s] = L.wt[lp][mkc][(tCol[s] + 16 * mkc) & (kMRows - 1)];
         }
       }
 #pragma unroll
@@ -828,8 +857,8 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
             const int qq = qb[s] + q + 2 * u + (mk >> 1);
             ok[s][u] = qq < qe[s];
             const int k = L.cobs[ok[s][u] ? qq : 0];
-            const double* src = mi < 9 ? &L.jc[k][9 * row + mi]
-                                : mi < 11 ? &L.ru[k][row + 2 * (mi - 9)] : &L.zero;
+            const double* src = mi < 9 ? &L.jc[9 * row + mi][k]
+                                : mi < 11 ? &L.ru[row + 2 * (mi - 9)][k] : &L.zero;
             z[s][u] = *src;
           }
 #pragma unroll
@@ -842,6 +871,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       }
     }
     p0 = np0; p1 = np1; o0 = no0; o1 = no1;
+    np0 = nnp0; np1 = nnp1; no0 = nno0; no1 = nno1;
   }
   // (E) T and the Z_a tiles -> LDS staging (aliases the operand planes), then
   //     the partial rows
