@@ -267,9 +267,17 @@ def run_tracking(args, world, rank):
     else:
         ba_stream = (stream if args.ba_serial else
                      torch.cuda.Stream(priority=-1 if args.priority == "ba" else 0))
-    with torch.cuda.stream(ba_stream):
-        ba = BABatch([BAProblem(*w, stream=ba_stream, chunks_per_wg=args.chunks_per_wg)
-                      for w in windows], stream=ba_stream)
+    # --ba-streams S: the step's windows split into S batches on S streams (one
+    # batch's latency-bound camera solve overlaps another's linearisation)
+    ns = max(1, min(args.ba_streams, len(windows)))
+    ba_subs = [ba_stream] if ns == 1 else [torch.cuda.Stream(priority=-1 if args.priority == "ba" else 0)
+                                            for _ in range(ns)]
+    bas = []
+    for i, s in enumerate(ba_subs):
+        with torch.cuda.stream(s):
+            bas.append(BABatch([BAProblem(*w, stream=s, chunks_per_wg=args.chunks_per_wg)
+                                for w in windows[i::ns]], stream=s))
+    ba = bas[0]
     torch.cuda.synchronize()
     tstream = trk_stream if trk_stream is not None else stream
     all_poses = {}
@@ -303,14 +311,20 @@ def run_tracking(args, world, rank):
         if args.ba_overlap == "after-orb":
             ba_stream.wait_event(trk.orb_event)
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
-        with torch.cuda.stream(ba_stream):
-            # the step's local-BA windows, all advanced together (one launch set
-            # per LM iteration; windows restored to their initial state first)
-            if args.no_graph:
-                ba.restore()
-                ba.iterate(args.ba_iters)
-            else:
-                ba.iterate_graphed(args.ba_iters, with_restore=True)
+        for bt, s in zip(bas, ba_subs):
+            if s is not ba_stream:
+                s.wait_stream(ba_stream)
+            with torch.cuda.stream(s):
+                # the step's local-BA windows, all advanced together (one launch set
+                # per LM iteration; windows restored to their initial state first)
+                if args.no_graph:
+                    bt.restore()
+                    bt.iterate(args.ba_iters)
+                else:
+                    bt.iterate_graphed(args.ba_iters, with_restore=True)
+        for s in ba_subs:
+            if s is not ba_stream:
+                ba_stream.wait_stream(s)
         if args.ba_overlap == "after-orb":
             ba_done[0] = ev_on(ba_stream)
         if marks is not None:
@@ -404,7 +418,7 @@ def run_tracking(args, world, rank):
                                                     pairs=CPU_PAIRS, lm_iters=CPU_PAIRS)
     if not args.no_tracked_ba:
         rec["tracked_window_ba"] = tracked_window_ba(feed, B, rig, args)
-    del trk, ba  # their kernels' buffers, then the masked streams themselves
+    del trk, ba, bas  # their kernels' buffers, then the masked streams themselves
     if trk_stream is not None:
         trk_stream.destroy()
     if hasattr(ba_stream, "destroy"):
@@ -837,7 +851,8 @@ def main():
     ap.add_argument("--chunks-per-wg", type=int, default=None,
                     help="camera-union linearisation: chunks per workgroup (default: auto)")
     ap.add_argument("--ba-streams", type=int, default=1,
-                    help="--workload ba --ba-batch N: split the windows over this many streams")
+                    help="split the local-BA windows over this many streams (tracking, and "
+                         "--workload ba --ba-batch N)")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")

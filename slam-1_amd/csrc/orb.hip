@@ -342,10 +342,12 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int n_l = g.nl[l];
     if (W <= 2 * kEdge || H <= 2 * kEdge || n_l == 0) continue;  // uniform
 
-    // ---- FAST score map over [29, W-30] x [29, H-30]
+    // ---- FAST score map over [29, W-30] x [29, H-30], rows padded to a
+    // multiple of 4 bytes (SW4) so the NMS below reads it a dword at a time
     const int SWd = W - 2 * kNMS0, SHd = H - 2 * kNMS0;
+    const int SW4 = (SWd + 3) & ~3;
     uint8_t* Smap = U;
-    const uint32_t mS = div_magic(SWd);
+    const uint32_t mS = div_magic(SWd), mS4 = div_magic(SW4);
     // Four pixels per pass: the 20 quick-reject reads of the group are all
     // issued before any Smap store.  Survivors (~8% of pixels, but present
     // in ~30% of waves) are queued in a wave-private LDS list (the tail of
@@ -354,12 +356,13 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int SN = SWd * SHd;
     uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * 4 * 64;
     for (int i0 = t; i0 < SN; i0 += 4 * kOrbWG) {
-      int v[4], p0[4], p4[4], p8[4], p12[4];
+      int v[4], p0[4], p4[4], p8[4], p12[4], si[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int i = min(i0 + q * kOrbWG, SN - 1);
         const int y = fdiv(i, mS), x = i - y * SWd;
         const uint8_t* c = I + (y + kNMS0) * W + x + kNMS0;
+        si[q] = y * SW4 + x;
         v[q] = c[0];
         p0[q] = c[3 * W];
         p4[q] = c[3];
@@ -371,17 +374,17 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       for (int q = 0; q < 4; ++q) {
         const int i = i0 + q * kOrbWG;
         const bool ok = i < SN && fast_maybe(v[q], p0[q], p4[q], p8[q], p12[q]);
-        if (i < SN && !ok) Smap[i] = 0;
+        if (i < SN && !ok) Smap[si[q]] = 0;
         const uint64_t m = __ballot(ok);
         if (ok)
           fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-              (uint32_t)i;
+              (uint32_t)si[q];
         nq += __popcll(m);
       }
       for (int j = lane; j < nq; j += 64) {
-        const int i = (int)fq[j];
-        const int y = fdiv(i, mS), x = i - y * SWd;
+        const int i = (int)fq[j];  // padded-map index: y * SW4 + x
+        const int y = fdiv(i, mS4), x = i - y * SW4;
         Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * W + x + kNMS0, W);
       }
     }
@@ -389,21 +392,50 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (t < 8) ctr[t] = 0;
     __syncthreads();
     ORB_T(2);
-    // ---- strict 3x3 NMS + border [31, W-32] -> candidates
+    // ---- strict 3x3 NMS + border [31, W-32] -> candidates: one dword of
+    // the score map (4 pixels) per lane; the scored pixels (FAST corners,
+    // ~8 %) are queued in the wave-private list and take the 8-neighbour test
+    // packed 64 per pass.  The loop trip count is wave-uniform (every lane
+    // stays in it), so a pass drains the whole queue.  The candidate order is
+    // immaterial: the list is ranked by (response, y, x) below and the
+    // histogram is order-free.
     {
-      const int CW = W - 2 * kEdge, CH = H - 2 * kEdge;
-      const uint32_t mC = div_magic(CW);
-      for (int i = t; i < CW * CH; i += kOrbWG) {
-        const int yy = fdiv(i, mC), xx = i - yy * CW;
-        const int x = xx + kEdge, y = yy + kEdge;
-        const uint8_t* sp = Smap + (y - kNMS0) * SWd + (x - kNMS0);
-        const int s = sp[0];
-        if (s == 0) continue;
-        if (s > sp[-1] && s > sp[1] && s > sp[-SWd - 1] && s > sp[-SWd] && s > sp[-SWd + 1] &&
-            s > sp[SWd - 1] && s > sp[SWd] && s > sp[SWd + 1]) {
-          const int k = atomicAdd(&ctr[0], 1);
-          if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 23) | ((uint32_t)y << 12) | (uint32_t)x;
-          atomicAdd(&hist[s], 1);
+      const int CH = H - 2 * kEdge;
+      const int NG = SW4 >> 2, NT = CH * NG;
+      const uint32_t mG = div_magic(NG);
+      for (int base = wid * 64; base < NT; base += kOrbWG) {
+        const int i = base + lane;
+        uint32_t w4 = 0u;
+        int y = 0, g4 = 0;
+        if (i < NT) {
+          const int yy = fdiv(i, mG);
+          g4 = i - yy * NG;
+          y = yy + kEdge;
+          w4 = *reinterpret_cast<const uint32_t*>(Smap + (y - kNMS0) * SW4 + 4 * g4);
+        }
+        int nq = 0;  // wave-uniform
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+          const int x = kNMS0 + 4 * g4 + bb;
+          const bool ok = ((w4 >> (8 * bb)) & 255u) != 0u && x >= kEdge && x <= W - 1 - kEdge;
+          const uint64_t m = __ballot(ok);
+          if (ok)
+            fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                ((uint32_t)y << 12) | (uint32_t)x;
+          nq += __popcll(m);
+        }
+        for (int j = lane; j < nq; j += 64) {
+          const uint32_t yx = fq[j];
+          const int yq = (int)(yx >> 12), xq = (int)(yx & 4095u);
+          const uint8_t* sp = Smap + (yq - kNMS0) * SW4 + (xq - kNMS0);
+          const int s = sp[0];
+          if (s > sp[-1] && s > sp[1] && s > sp[-SW4 - 1] && s > sp[-SW4] && s > sp[-SW4 + 1] &&
+              s > sp[SW4 - 1] && s > sp[SW4] && s > sp[SW4 + 1]) {
+            const int k = atomicAdd(&ctr[0], 1);
+            if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 23) | yx;
+            atomicAdd(&hist[s], 1);
+          }
         }
       }
     }
@@ -799,7 +831,7 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
         const int W0 = w, H0 = h;
         if (W0 > 2 * kEdge && H0 > 2 * kEdge) {
           const int cand = ((W0 - 2 * kEdge + 1) / 2) * ((H0 - 2 * kEdge + 1) / 2);
-          const int smap = (((W0 - 2 * kNMS0) * (H0 - 2 * kNMS0)) + 15) & ~15;
+          const int smap = (((((W0 - 2 * kNMS0) + 3) & ~3) * (H0 - 2 * kNMS0)) + 15) & ~15;
           const int bl = (W0 - 2 * kBl0) * (H0 - 2 * kBl0);
           max_cand = max(max_cand, cand);
           max_smap = max(max_smap, smap);
