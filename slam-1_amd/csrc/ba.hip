@@ -1246,31 +1246,41 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
     // u_j is the partially eliminated entry A^{(j)}(r, c0+j), L(r, j) = u_j/d_j.
     // (Was: every lane factored the whole 9x9 block redundantly, ~3x the
     // VALU work of this form.)
+    // Every 16-lane DPP row of a participating wave holds a copy of the 9 pivot
+    // rows (lanes 0..8 of the row) and 7 rows below the panel (lanes 9..15), so
+    // the pivot entries reach the other lanes as DPP row_newbcast operands
+    // (no v_readlane -> SGPR hop in the pivot chain).  28 rows below per wave:
+    // 4 waves cover 9C + 1 - 9 <= 112 rows.
+    constexpr int kRowsBelow = 16 - kPanelW;              // per DPP row
     const int nbelow = n + 1 - c0 - kPanelW;             // rows below the panel, rhs included
-    const int nw = max(1, (nbelow + 63 - kPanelW) / (64 - kPanelW));  // uniform
+    const int nw = max(1, (nbelow + 4 * kRowsBelow - 1) / (4 * kRowsBelow));  // uniform
     if (wid < nw) {
-      const bool piv = lane < kPanelW;
-      const int r = piv ? c0 + lane : c0 + kPanelW + (64 - kPanelW) * wid + (lane - kPanelW);
+      const int rl = lane & 15, rg = lane >> 4;
+      const bool piv = rl < kPanelW;
+      const int r = piv ? c0 + rl
+                        : c0 + kPanelW + 4 * kRowsBelow * wid + kRowsBelow * rg + (rl - kPanelW);
       const bool valid = r <= n;
       const double* pr = Pn + (r - c0) * kPanelW;
       double u[kPanelW];
 #pragma unroll
-      for (int j = 0; j < kPanelW; ++j) u[j] = valid && (!piv || j <= lane) ? pr[j] : 0.0;
+      for (int j = 0; j < kPanelW; ++j) u[j] = valid && (!piv || j <= rl) ? pr[j] : 0.0;
       double Dinv[kPanelW];
       bool bad = false;
 #ifdef SLAM_SOLVE_PROFILE_PANEL
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t qb1 = __builtin_amdgcn_s_memtime();
 #endif
-#pragma unroll
-      for (int j = 0; j < kPanelW; ++j) {
-        const double d = readlane_d(u[j], j);
+      static_for<0, kPanelW>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const double d = bcast16<j>(u[j]);
         bad |= !(d > 0.0) || !isfinite(d);
         Dinv[j] = rcp_f64(d);
         const double l = u[j] * Dinv[j];
-#pragma unroll
-        for (int i = j + 1; i < kPanelW; ++i) u[i] = __builtin_fma(-l, readlane_d(u[j], i), u[i]);
-      }
+        static_for<j + 1, kPanelW>([&](auto I) {
+          constexpr int i = decltype(I)::value;
+          u[i] = __builtin_fma(-l, bcast16<i>(u[j]), u[i]);
+        });
+      });
 #ifdef SLAM_SOLVE_PROFILE_PANEL
       {
         double chk = u[kPanelW - 1];
@@ -1284,7 +1294,7 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
       }
 #endif
       // stores grouped so that each lane class takes one exec-mask region
-      if (valid && (wid == 0 || !piv)) {
+      if (valid && ((wid == 0 && rg == 0) || !piv)) {
         double* wl = WL + r * kWLs;
         double* ll = LL + r * kWLs;
         double* lf = LF + r * (r - 1) / 2 + c0;
@@ -1305,11 +1315,11 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
           // pivot row m = lane: D_m and the lower part L(r, c0 + j), j < m
           double dm = u[0];
 #pragma unroll
-          for (int j = 1; j < kPanelW; ++j) dm = j == lane ? u[j] : dm;
+          for (int j = 1; j < kPanelW; ++j) dm = j == rl ? u[j] : dm;
           Dd[r] = dm;
 #pragma unroll
           for (int j = 0; j < kPanelW - 1; ++j)
-            if (j < lane) lf[j] = lj[j];
+            if (j < rl) lf[j] = lj[j];
         }
       }
       if (wid == 0 && lane == 0 && bad) *fail_p = 1;
@@ -1669,17 +1679,17 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
-      // rows of the 16x16 diagonal block in lanes 0..15 (lower part read)
+      // rows of the 16x16 diagonal block in lanes i = l & 15 of every 16-lane
+      // DPP row (lower part read; the four rows of the wave hold copies).  L(m, j)
+      // (= lane m's l_ij) reaches the other lanes of the row as a DPP
+      // row_newbcast operand: no LDS round trip and no SGPR hop in the pivot chain.
       const int i = l & 15;
       double v[16], rj[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
-      // column j of L goes through LDS (Lt[j][i] = L[i][j], one store per lane,
-      // broadcast reads back) instead of 15 v_readlane pairs per step
-      double* Lt = Tb;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const double djj = readlane_d(v[j], j);
+      static_for<0, 16>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const double djj = bcast16<j>(v[j]);
         ok = ok && djj > 0.0 && djj < INFINITY;
         double r = __builtin_amdgcn_rsq(djj);
         const double h = 0.5 * djj;
@@ -1688,27 +1698,27 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
         rj[j] = r;
         const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
         v[j] = lij;
-        if (l < 16) Lt[j * kBS17 + i] = lij;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int m = j + 1; m < 16; ++m) v[m] = __builtin_fma(-lij, Lt[j * kBS17 + m], v[m]);
-      }
+        static_for<j + 1, 16>([&](auto Mi) {
+          constexpr int m = decltype(Mi)::value;
+          v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
+        });
+      });
       // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
       // (column-oriented: once x_k is known, every later row's sum takes its
       // term -- the same k order per sum as the row form, a 16-step chain
-      // instead of 120 dependent FMAs)
+      // instead of 120 dependent FMAs); l_ik = lane ii's v[k], by row_newbcast
       const int c = l & 15;
       double x[16], sacc[16];
 #pragma unroll
       for (int ii = 0; ii < 16; ++ii) sacc[ii] = 0.0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
+      static_for<0, 16>([&](auto K) {
+        constexpr int k = decltype(K)::value;
         x[k] = k < c ? 0.0 : (k == c ? rj[k] : -sacc[k] * rj[k]);
-#pragma unroll
-        for (int ii = k + 1; ii < 16; ++ii) sacc[ii] = __builtin_fma(Lt[k * kBS17 + ii], x[k], sacc[ii]);
-      }
+        static_for<k + 1, 16>([&](auto II) {
+          constexpr int ii = decltype(II)::value;
+          sacc[ii] = __builtin_fma(bcast16<ii>(v[k]), x[k], sacc[ii]);
+        });
+      });
       if (l < 16) {
         double* X = Xb + blk_id(p, p) * 16 * kBS17;
 #pragma unroll

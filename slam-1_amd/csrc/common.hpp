@@ -7,6 +7,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <type_traits>
 
 #include "../../include/slam355.h"
 
@@ -41,3 +42,20 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 #define SLAM_LAUNCHED(name) SLAM_HIP(hipGetLastError())
 
 constexpr int kWave = 64;  // gfx950 wavefront
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Lane m of each 16-lane row, broadcast to the whole row (DPP row_newbcast,
+// gfx90a+; on f64 it lowers to v_mov_b64_dpp or folds into the consumer).
+template <int M>
+__device__ __forceinline__ double bcast16(double v) {
+  static_assert(M >= 0 && M < 16, "row lane");
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + M, 0xf, 0xf, false);
+}
