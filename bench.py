@@ -254,8 +254,14 @@ def run_tracking(args, world, rank):
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
     n_solves = max(1, B // args.ba_every)
+    # --ba-group G: the windows of G consecutive steps advance as one launch set,
+    # issued every G-th step (local mapping lags tracking by < G steps; the same
+    # windows x iterations per step on average; K and W rounded up to multiples of G)
+    G = max(1, args.ba_group)
+    args.steps, args.warmup = -(-args.steps // G) * G, -(-args.warmup // G) * G
+    n_launch = n_solves * G
     windows = []
-    for _ in range(n_solves):  # one C3 window per `ba_every` frames, each its own problem
+    for _ in range(n_launch):  # one C3 window per `ba_every` frames, each its own problem
         cams, pts, ci, pi, qs = ba_problem(rng, *C3)
         c0, p0 = perturb(rng, cams, pts)
         windows.append((c0, p0, ci, pi, qs))
@@ -289,6 +295,7 @@ def run_tracking(args, world, rank):
         return ev
 
     ba_done = [None]
+    step_no = [0]
 
     def step(marks):
         with torch.cuda.stream(tstream):
@@ -308,6 +315,11 @@ def run_tracking(args, world, rank):
             marks["orb"] = trk.orb_marks  # ORB's own stream: start -> done there
         if marks is None and args.keep_poses:
             all_poses[win] = trk.poses.clone()
+        step_no[0] += 1
+        if step_no[0] % G:
+            if marks is not None:
+                marks["track"] = tmarks
+            return  # this step's windows join the next step's launch set
         if args.ba_overlap == "after-orb":
             ba_stream.wait_event(trk.orb_event)
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
@@ -352,15 +364,15 @@ def run_tracking(args, world, rank):
     kp_mean = float(np.mean(cnt["orb"]))
     orb_bytes = n_img * (patch_bytes + kp_mean * ORB_OUT_BYTES)
     orb_ms = stages.get("orb", float("nan"))
-    # one batched LM iteration advances all n_solves windows
+    # one batched LM iteration advances all n_launch windows
     ba_ms_iter = stages.get("local_ba", float("nan")) / args.ba_iters
-    ba_flops = n_solves * ba_flops_per_iter(*C3[:2], C3[1] * C3[2], C3[2])
+    ba_flops = n_launch * ba_flops_per_iter(*C3[:2], C3[1] * C3[2], C3[2])
     roof = {
         "orb": {"bound": "hbm", "achieved": orb_bytes / (orb_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_solves} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     pmc = pmc_traffic()
@@ -373,7 +385,10 @@ def run_tracking(args, world, rank):
             r["traffic_unit"] = "bytes per launch (LM iteration for local_ba), HBM, from PMC"
             r["traffic_source"] = pmc["path"]
     per_step = {k: v for k, v in stages.items()}
-    dominant = max(("orb", orb_ms), ("local_ba", stages.get("local_ba", 0.0)), key=lambda kv: kv[1])[0]
+    if G > 1 and "local_ba" in per_step:  # one launch set per G steps
+        per_step["local_ba_per_launch_set"] = per_step["local_ba"]
+        per_step["local_ba"] /= G
+    dominant = max(("orb", orb_ms), ("local_ba", per_step.get("local_ba", 0.0)), key=lambda kv: kv[1])[0]
     rec = {
         "metric": "frames/sec tracking+local-BA @1280x720",
         "value": frames / dt,
@@ -390,7 +405,8 @@ def run_tracking(args, world, rank):
                  "1280x720 in pinned host memory, uploaded inside the timed region; GT poses)"),
         "config": {"workload": f"C2 tracking (1280x720, {args.kp_per_tile} ORB kp/tile) + "
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
-                               f"x {args.ba_iters} LM iters ({n_solves} windows per step, batched)",
+                               f"x {args.ba_iters} LM iters ({n_solves} windows per step, batched" +
+                               (f" over {G} steps per launch set)" if G > 1 else ")"),
                    "orb_kp_mean": kp_mean,
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
                    "h2d_upload": "in timed region (pinned, copy stream, double-buffered)",
@@ -400,7 +416,8 @@ def run_tracking(args, world, rank):
                    "tracking_cus": args.track_cus or "all",
                    "orb_stream": (f"pipelined, CUs 0..{args.orb_cus - 1}" if args.orb_cus else
                                   "pipelined, all CUs") if args.orb_pipeline else "tracking stream",
-                   "local_ba_cus": args.ba_cus or "all"},
+                   "local_ba_cus": args.ba_cus or "all",
+                   "local_ba_launch_set": f"{n_launch} windows every {G} step(s)"},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
         "stage_ms_per_step": per_step,
@@ -853,6 +870,8 @@ def main():
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
+    ap.add_argument("--ba-group", type=int, default=1,
+                    help="tracking: the local-BA windows of G consecutive steps advance as one launch set")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")

@@ -76,6 +76,8 @@ __device__ __forceinline__ int fdiv(int n, uint32_t m) {
 // Exact quick reject: any 9 consecutive circle positions contain two
 // adjacent compass points (0,4,8,12), so a corner needs such a pair to be
 // darker (or brighter) than v -/+ t.  p0/p4/p8/p12 are the compass pixels.
+// (A packed two-pixel form on v_pk_sub_u16 clamp measured slower overall:
+// 1.67 vs 1.49 ms per 65 images, the later phases lost more than FAST gained.)
 __device__ __forceinline__ bool fast_maybe(int v, int p0, int p4, int p8, int p12) {
   const int e0 = v - p0, e4 = v - p4, e8 = v - p8, e12 = v - p12;
   const unsigned dk = (e0 > kFastT ? 1u : 0u) | (e4 > kFastT ? 2u : 0u) |
@@ -107,55 +109,36 @@ __device__ __forceinline__ int fast_full(const uint8_t* c, int st) {
   d[13] = v - c[st - 3];
   d[14] = v - c[2 * st - 2];
   d[15] = v - c[3 * st - 1];
-  unsigned dark = 0, bright = 0;
+  // OpenCV cornerScore<16> is max(t, A_dark, A_bright) - 1 with A_dark = the
+  // largest min(d) over the 16 circular 9-arcs and A_bright the same for -d; a
+  // segment test pass (9 consecutive d > t, or -d > t) is exactly A > t, so
+  //   score = A > t ? A - 1 : 0,  A = max(A_dark, A_bright).
+  // Both sides at once on packed int16 pairs (d, -d) (v_pk_min/max_i16), the
+  // 9-arcs (k .. k+8) and (k+1 .. k+9), k even, sharing the min over k+1 .. k+8
+  // built from pairwise minima (m2 -> m4 -> m8).
+  typedef short s2 __attribute__((ext_vector_type(2)));
+  s2 p[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    dark |= (d[k] > kFastT ? 1u : 0u) << k;     // p < v - t
-    bright |= (d[k] < -kFastT ? 1u : 0u) << k;  // p > v + t
+  for (int k = 0; k < 16; ++k) p[k] = s2{(short)d[k], (short)-d[k]};
+  s2 m2[8], m4[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)  // min over 2k+1, 2k+2
+    m2[k] = __builtin_elementwise_min(p[(2 * k + 1) & 15], p[(2 * k + 2) & 15]);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m4[k] = __builtin_elementwise_min(m2[k], m2[(k + 1) & 7]);  // 2k+1 .. 2k+4
+  s2 acc = s2{(short)kFastT, (short)kFastT};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const s2 m8 = __builtin_elementwise_min(m4[k], m4[(k + 2) & 7]);  // 2k+1 .. 2k+8
+    acc = __builtin_elementwise_max(acc, __builtin_elementwise_min(m8, p[2 * k]));
+    acc = __builtin_elementwise_max(acc, __builtin_elementwise_min(m8, p[(2 * k + 9) & 15]));
   }
-  auto run9 = [](unsigned m) {
-    unsigned mm = m | (m << 16), r = mm;
-#pragma unroll
-    for (int i = 1; i <= 8; ++i) r &= mm >> i;
-    return (r & 0xFFFFu) != 0u;
-  };
-  if (!run9(dark) && !run9(bright)) return 0;
-  // OpenCV cornerScore<16>
-  int a0 = kFastT;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int a = d[(k + 1) & 15];
-#pragma unroll
-    for (int j = 2; j <= 8; ++j) a = min(a, d[(k + j) & 15]);
-    a0 = max(a0, min(a, d[k]));
-    a0 = max(a0, min(a, d[(k + 9) & 15]));
-  }
-  int b0 = -a0;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int b = d[(k + 1) & 15];
-#pragma unroll
-    for (int j = 2; j <= 8; ++j) b = max(b, d[(k + j) & 15]);
-    b0 = min(b0, max(b, d[k]));
-    b0 = min(b0, max(b, d[(k + 9) & 15]));
-  }
-  return -b0 - 1;
+  const int A = max((int)acc.x, (int)acc.y);
+  return A > kFastT ? A - 1 : 0;
 }
 
-__device__ __forceinline__ float harris(const uint8_t* im, int st, int x0, int y0) {
-  int a = 0, b = 0, c = 0;
-  for (int i = 0; i < 7; ++i) {
-    const uint8_t* row = im + (y0 - 3 + i) * st + (x0 - 3);
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const uint8_t* p = row + j;
-      const int Ix = (p[1] - p[-1]) * 2 + (p[-st + 1] - p[-st - 1]) + (p[st + 1] - p[st - 1]);
-      const int Iy = (p[st] - p[-st]) * 2 + (p[st - 1] - p[-st - 1]) + (p[st + 1] - p[-st + 1]);
-      a += Ix * Ix;
-      b += Iy * Iy;
-      c += Ix * Iy;
-    }
-  }
+// Harris response from the window sums a = sum Ix^2, b = sum Iy^2, c = sum Ix Iy
+__device__ __forceinline__ float harris_resp(int a, int b, int c) {
   const float scale = 1.f / ((1 << 2) * 7 * 255.f);
   const float ssss = scale * scale * scale * scale;
   const float k = 0.04f;
@@ -347,41 +330,54 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int SWd = W - 2 * kNMS0, SHd = H - 2 * kNMS0;
     const int SW4 = (SWd + 3) & ~3;
     uint8_t* Smap = U;
-    const uint32_t mS = div_magic(SWd), mS4 = div_magic(SW4);
+    const uint32_t mS4 = div_magic(SW4);
     // Four pixels per pass: the 20 quick-reject reads of the group are all
     // issued before any Smap store.  Survivors (~8% of pixels, but present
     // in ~30% of waves) are queued in a wave-private LDS list (the tail of
     // U past the score map) and take the full test packed 64 per pass
     // instead of diverging inside every wave that holds one.
-    const int SN = SWd * SHd;
+    // One dword of the map (4 adjacent pixels) per lane and pass: the centre
+    // row window [x-3, x+6] and the rows y -/+ 3 come from aligned dword LDS
+    // reads + v_alignbyte (8 reads per 4 pixels instead of 20 byte reads), and
+    // the 4 map bytes leave as one dword (survivors' scores overwrite theirs below).
+    const int NG4 = SW4 >> 2, SN4 = NG4 * SHd;
+    const uint32_t mG4 = div_magic(NG4);
     uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * 4 * 64;
-    for (int i0 = t; i0 < SN; i0 += 4 * kOrbWG) {
-      int v[4], p0[4], p4[4], p8[4], p12[4], si[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = min(i0 + q * kOrbWG, SN - 1);
-        const int y = fdiv(i, mS), x = i - y * SWd;
-        const uint8_t* c = I + (y + kNMS0) * W + x + kNMS0;
-        si[q] = y * SW4 + x;
-        v[q] = c[0];
-        p0[q] = c[3 * W];
-        p4[q] = c[3];
-        p8[q] = c[-3 * W];
-        p12[q] = c[-3];
-      }
+    auto win4 = [&](int a) {  // bytes a .. a+3 of the level image (any alignment)
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (a & ~3));
+      return __builtin_amdgcn_alignbyte(wp[1], wp[0], a & 3);
+    };
+    // (trip count wave-uniform: every lane of the wave takes part in the queue drain)
+    for (int gb = wid * 64; gb < SN4; gb += kOrbWG) {
+      const bool gv = gb + lane < SN4;
+      const int gi = min(gb + lane, SN4 - 1);
+      const int y = fdiv(gi, mG4), x = 4 * (gi - y * NG4);  // map coords of the first pixel
+      const int a = (y + kNMS0) * W + x + kNMS0;
+      const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + ((a - 3) & ~3));
+      const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3];
+      const int sh = (a - 3) & 3;
+      const uint32_t up = win4(a - 3 * W), dn = win4(a + 3 * W);
+      const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);  // bytes a-3 .. a
+      const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);  // a+1 .. a+4
+      const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // a+5 .. a+8
+      const uint64_t lo = ((uint64_t)q1 << 32) | q0;               // a-3 .. a+4
+      const uint32_t cc = (uint32_t)(lo >> 24);                    // a .. a+3
+      const uint32_t rt = (uint32_t)(((uint64_t)q2 << 32 | q1) >> 16);  // a+3 .. a+6
       int nq = 0;  // wave-uniform
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int i = i0 + q * kOrbWG;
-        const bool ok = i < SN && fast_maybe(v[q], p0[q], p4[q], p8[q], p12[q]);
-        if (i < SN && !ok) Smap[si[q]] = 0;
+        const bool in = gv && x + q < SWd;
+        const int v = (cc >> (8 * q)) & 255;
+        const bool ok = in && fast_maybe(v, (dn >> (8 * q)) & 255, (rt >> (8 * q)) & 255,
+                                         (up >> (8 * q)) & 255, (q0 >> (8 * q)) & 255);
         const uint64_t m = __ballot(ok);
         if (ok)
           fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-              (uint32_t)si[q];
+              (uint32_t)(y * SW4 + x + q);
         nq += __popcll(m);
       }
+      if (gv) *reinterpret_cast<uint32_t*>(Smap + y * SW4 + x) = 0u;
       for (int j = lane; j < nq; j += 64) {
         const int i = (int)fq[j];  // padded-map index: y * SW4 + x
         const int y = fdiv(i, mS4), x = i - y * SW4;
@@ -507,9 +503,28 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     const int nk = ctr[1];
     ORB_T(4);
-    for (int i = t; i < nk; i += kOrbWG) {
-      const uint32_t c = cand[i];
-      cresp[i] = harris(I, W, (int)(c & 4095u), (int)((c >> 12) & 2047u));
+    // Harris: one wave per survivor, lane 7i + j <-> pixel (i, j) of the 7x7
+    // window; the integer sums a, b, c are reduced across the wave (exact in
+    // any order), the response is formed once
+    for (int k = wid; k < nk; k += kOrbWG / 64) {
+      const uint32_t c = cand[k];
+      const int hx = (int)(c & 4095u), hy = (int)((c >> 12) & 2047u);
+      int a = 0, bq = 0, cq = 0;
+      if (lane < 49) {
+        const int i = lane / 7, j = lane - 7 * (lane / 7);
+        const uint8_t* pp = I + (hy - 3 + i) * W + (hx - 3 + j);
+        const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-W + 1] - pp[-W - 1]) + (pp[W + 1] - pp[W - 1]);
+        const int Iy = (pp[W] - pp[-W]) * 2 + (pp[W - 1] - pp[-W - 1]) + (pp[W + 1] - pp[-W + 1]);
+        a = Ix * Ix;
+        bq = Iy * Iy;
+        cq = Ix * Iy;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        bq += __shfl_xor(bq, off, 64);
+        cq += __shfl_xor(cq, off, 64);
+      }
+      if (lane == 0) cresp[k] = harris_resp(a, bq, cq);
     }
     __syncthreads();
     ORB_T(5);
@@ -519,7 +534,19 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       const uint32_t ci = cand[i];
       const uint32_t yxi = ci & 0x7FFFFFu;  // (y << 12) | x: y-major order
       int rank = 0;
-      for (int j = 0; j < nk; ++j) {
+      int j = 0;
+      for (; j + 4 <= nk; j += 4) {  // 8 LDS reads in flight per step
+        float rj[4];
+        uint32_t yxj[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          rj[u] = cresp[j + u];
+          yxj[u] = cand[j + u] & 0x7FFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rank += (rj[u] > ri || (rj[u] == ri && yxj[u] < yxi)) ? 1 : 0;
+      }
+      for (; j < nk; ++j) {
         const float rj = cresp[j];
         const uint32_t yxj = cand[j] & 0x7FFFFFu;
         rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
@@ -552,20 +579,25 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       overflow = 1;
       break;
     }
-    // ---- IC angle: one wave per keypoint, lanes 0..30 <-> u = -15..15
+    // ---- IC angle: one wave per keypoint, lanes 32h + (0..30) <-> u = -15..15;
+    // the disc column of u is |v| <= umax[|u|] (the umax table is symmetric:
+    // |u| <= umax[|v|] <=> |v| <= umax[|u|]), rows v = -1..-15 in h = 0 and
+    // 0..15 in h = 1, 16 independent masked reads per lane (integer moments:
+    // exact in any order)
+    const int ic_u = (lane & 31) - 15;
+    const int ic_vlim = (lane & 31) < 31 ? c_umax[ic_u < 0 ? -ic_u : ic_u] : -1;
     for (int k = wid; k < m; k += kOrbWG / 64) {
       const int cx = L[k].x, cy = L[k].y;
       int m10 = 0, m01 = 0;
-      const int u = lane - 15;
-      if (lane < 31) {
-        const int au = u < 0 ? -u : u;
-        for (int v = -15; v <= 15; ++v) {
-          const int av = v < 0 ? -v : v;
-          if (au <= c_umax[av]) {
-            const int val = I[(cy + v) * W + cx + u];
-            m10 += u * val;
-            m01 += v * val;
-          }
+      {
+        const int u = ic_u;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const int v = lane < 32 ? -(s + 1) : s;
+          const bool in = (lane < 32 ? s + 1 : s) <= ic_vlim;
+          const int val = I[(cy + (in ? v : 0)) * W + cx + (in ? u : 0)];
+          m10 += in ? u * val : 0;
+          m01 += in ? v * val : 0;
         }
       }
       for (int off = 32; off > 0; off >>= 1) {
