@@ -254,11 +254,12 @@ def run_tracking(args, world, rank):
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
     n_solves = max(1, B // args.ba_every)
-    # --ba-group G: the windows of G consecutive steps advance as one launch set,
-    # issued every G-th step (local mapping lags tracking by < G steps; the same
-    # windows x iterations per step on average; K and W rounded up to multiples of G)
+    # --ba-group G: the windows of G consecutive steps advance as one launch set
+    # (local mapping lags tracking by < G steps).  Pending windows are flushed at
+    # the end of the warmup and of the timed region as a whole set, so the timed
+    # region holds at least its K steps' windows x iterations.
     G = max(1, args.ba_group)
-    args.steps, args.warmup = -(-args.steps // G) * G, -(-args.warmup // G) * G
+    assert G == 1 or args.ba_streams == 1, "--ba-group > 1 needs --ba-streams 1"
     n_launch = n_solves * G
     windows = []
     for _ in range(n_launch):  # one C3 window per `ba_every` frames, each its own problem
@@ -295,7 +296,7 @@ def run_tracking(args, world, rank):
         return ev
 
     ba_done = [None]
-    step_no = [0]
+    step_no, pending = [0], [0]
 
     def step(marks):
         with torch.cuda.stream(tstream):
@@ -316,13 +317,19 @@ def run_tracking(args, world, rank):
         if marks is None and args.keep_poses:
             all_poses[win] = trk.poses.clone()
         step_no[0] += 1
-        if step_no[0] % G:
+        pending[0] += 1
+        k = step_no[0]
+        if pending[0] < G and k != args.warmup and k != args.warmup + args.steps:
             if marks is not None:
                 marks["track"] = tmarks
             return  # this step's windows join the next step's launch set
+        # (a set flushed early -- end of warmup, or a timed region of K not a
+        # multiple of G -- still advances all G steps' windows: extra work, never less)
+        full = pending[0] == G
+        pending[0] = 0
         if args.ba_overlap == "after-orb":
             ba_stream.wait_event(trk.orb_event)
-        bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
+        bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None and full else None
         for bt, s in zip(bas, ba_subs):
             if s is not ba_stream:
                 s.wait_stream(ba_stream)
@@ -339,9 +346,11 @@ def run_tracking(args, world, rank):
                 ba_stream.wait_stream(s)
         if args.ba_overlap == "after-orb":
             ba_done[0] = ev_on(ba_stream)
-        if marks is not None:
+        if bmarks is not None:
             bmarks.append(("local_ba", ev_on(ba_stream)))
-            marks["track"], marks["ba"] = tmarks, bmarks
+            marks["ba"] = bmarks
+        if marks is not None:
+            marks["track"] = tmarks
 
     dt, stages = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
     frames = reduce_scalar(float(B * args.steps), world, "sum")
@@ -417,7 +426,9 @@ def run_tracking(args, world, rank):
                    "orb_stream": (f"pipelined, CUs 0..{args.orb_cus - 1}" if args.orb_cus else
                                   "pipelined, all CUs") if args.orb_pipeline else "tracking stream",
                    "local_ba_cus": args.ba_cus or "all",
-                   "local_ba_launch_set": f"{n_launch} windows every {G} step(s)"},
+                   "local_ba_launch_set": (f"{n_launch} windows every {G} steps (pending steps flushed "
+                                           "as a whole set at the ends of warmup and timed region)" if G > 1 else
+                                           f"{n_launch} windows every step")},
         "roofline": dict(roof[dominant], stage=dominant),
         "roofline_stages": roof,
         "stage_ms_per_step": per_step,
@@ -870,7 +881,7 @@ def main():
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
-    ap.add_argument("--ba-group", type=int, default=1,
+    ap.add_argument("--ba-group", type=int, default=2,
                     help="tracking: the local-BA windows of G consecutive steps advance as one launch set")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
