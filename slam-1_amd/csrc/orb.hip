@@ -37,7 +37,6 @@ constexpr int kBl0 = 12;   // blurred region starts here (rotated samples within
 constexpr int kFq = (kOrbWG / 64) * 256 * 4;  // FAST survivor queues, bytes
 
 __constant__ int8_t c_pattern[256 * 4];
-__constant__ int c_umax[16] = {15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3};
 
 struct OrbGeom {
   int H, W, stride;
@@ -75,18 +74,26 @@ __device__ __forceinline__ int fdiv(int n, uint32_t m) {
 // ------------------------------------------------------------------ FAST
 // Exact quick reject: any 9 consecutive circle positions contain two
 // adjacent compass points (0,4,8,12), so a corner needs such a pair to be
-// darker (or brighter) than v -/+ t.  p0/p4/p8/p12 are the compass pixels.
-// (A packed two-pixel form on v_pk_sub_u16 clamp measured slower overall:
-// 1.67 vs 1.49 ms per 65 images, the later phases lost more than FAST gained.)
-__device__ __forceinline__ bool fast_maybe(int v, int p0, int p4, int p8, int p12) {
-  const int e0 = v - p0, e4 = v - p4, e8 = v - p8, e12 = v - p12;
-  const unsigned dk = (e0 > kFastT ? 1u : 0u) | (e4 > kFastT ? 2u : 0u) |
-                      (e8 > kFastT ? 4u : 0u) | (e12 > kFastT ? 8u : 0u);
-  const unsigned br = (e0 < -kFastT ? 1u : 0u) | (e4 < -kFastT ? 2u : 0u) |
-                      (e8 < -kFastT ? 4u : 0u) | (e12 < -kFastT ? 8u : 0u);
-  const unsigned dk2 = dk & ((dk >> 1) | (dk << 3));  // (0,4) (4,8) (8,12) (12,0)
-  const unsigned br2 = br & ((br >> 1) | (br << 3));
-  return ((dk2 | br2) & 0xFu) != 0u;
+// darker (or brighter) than v -/+ t.  Two pixels at once: the low bytes of the
+// 16-bit halves of v (centre) and of the compass pixels dn (0), rt (4), up (8),
+// lf (12); a half of the result is non-zero iff that pixel passes.  Every
+// adjacent compass pair is one of {dn, up} with one of {rt, lf}, so "a darker
+// adjacent pair" is (dn or up) and (rt or lf) darker, "p darker" being
+// sat(v - t - p) != 0 and "p brighter" sat(p - (v + t)) != 0 (v_pk_sub_u16 clamp).
+__device__ __forceinline__ uint32_t quick4(uint32_t v, uint32_t dn, uint32_t rt, uint32_t up,
+                                           uint32_t lf) {
+  typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+  auto h = [](uint32_t x) { return __builtin_bit_cast(u2, x & 0x00FF00FFu); };
+  const u2 vv = h(v), t2 = u2{(unsigned short)kFastT, (unsigned short)kFastT};
+  const u2 vlo = __builtin_elementwise_sub_sat(vv, t2), vhi = vv + t2;  // v - t (sat), v + t
+  const u2 pdn = h(dn), prt = h(rt), pup = h(up), plf = h(lf);
+  auto dk = [&](u2 p) { return __builtin_elementwise_sub_sat(vlo, p); };  // != 0: p < v - t
+  auto br = [&](u2 p) { return __builtin_elementwise_sub_sat(p, vhi); };  // != 0: p > v + t
+  const u2 d = __builtin_elementwise_min(__builtin_elementwise_max(dk(pdn), dk(pup)),
+                                         __builtin_elementwise_max(dk(prt), dk(plf)));
+  const u2 b = __builtin_elementwise_min(__builtin_elementwise_max(br(pdn), br(pup)),
+                                         __builtin_elementwise_max(br(prt), br(plf)));
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(d, b));
 }
 
 // Full segment test + OpenCV cornerScore<16> at c (past the quick reject).
@@ -363,13 +370,12 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       const uint64_t lo = ((uint64_t)q1 << 32) | q0;               // a-3 .. a+4
       const uint32_t cc = (uint32_t)(lo >> 24);                    // a .. a+3
       const uint32_t rt = (uint32_t)(((uint64_t)q2 << 32 | q1) >> 16);  // a+3 .. a+6
+      const uint32_t okv[2] = {quick4(cc, dn, rt, up, q0), quick4(cc >> 8, dn >> 8, rt >> 8, up >> 8, q0 >> 8)};
       int nq = 0;  // wave-uniform
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool in = gv && x + q < SWd;
-        const int v = (cc >> (8 * q)) & 255;
-        const bool ok = in && fast_maybe(v, (dn >> (8 * q)) & 255, (rt >> (8 * q)) & 255,
-                                         (up >> (8 * q)) & 255, (q0 >> (8 * q)) & 255);
+        const bool ok = in && ((okv[q & 1] >> (16 * (q >> 1))) & 0xFFFFu) != 0u;
         const uint64_t m = __ballot(ok);
         if (ok)
           fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -584,14 +590,20 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     // |u| <= umax[|v|] <=> |v| <= umax[|u|]), rows v = -1..-15 in h = 0 and
     // 0..15 in h = 1, 16 independent masked reads per lane (integer moments:
     // exact in any order)
-    const int ic_u = (lane & 31) - 15;
-    const int ic_vlim = (lane & 31) < 31 ? c_umax[ic_u < 0 ? -ic_u : ic_u] : -1;
     for (int k = wid; k < m; k += kOrbWG / 64) {
       const int cx = L[k].x, cy = L[k].y;
       int m10 = 0, m01 = 0;
       {
-        const int u = ic_u;
-#pragma unroll
+        // u and the column limit umax[|u|] (umax = {15,15,15,15,14,14,14,13,13,
+        // 12,11,10,9,8,6,3} as a packed 4-bit table) are formed in the loop:
+        // hoisted, they would hold registers across the whole kernel.  The
+        // rows stay a rolled loop: unrolled, the kernel spills (40-60 B/lane
+        // of scratch, 1.95 vs 1.52 ms per 65 images).
+        int ln = lane;
+        __asm__ volatile("" : "+v"(ln));
+        const int u = (ln & 31) - 15, au = u < 0 ? -u : u;
+        const int ic_vlim = (ln & 31) < 31 ? (int)((0x368'9abc'ddee'efff'fULL >> (4 * au)) & 15u) : -1;
+#pragma unroll 1
         for (int s = 0; s < 16; ++s) {
           const int v = lane < 32 ? -(s + 1) : s;
           const bool in = (lane < 32 ? s + 1 : s) <= ic_vlim;
