@@ -385,7 +385,7 @@ def run_tracking(args, world, rank):
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     pmc = pmc_traffic()
-    roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile", "k_orb_compact"))
+    roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_assemble", "k_solve_blk",
                                                   "k_back_trial<true>"))
     for r in roof.values():
