@@ -146,3 +146,80 @@ def test_gpu_step_distributed_matches_single_rank(tmp_path, C, P, k, iters):
     d = np.load(out)
     assert np.allclose(d["costs"], costs, rtol=1e-8)
     assert np.allclose(d["cams"], cams, rtol=1e-6, atol=1e-9)
+
+
+# ---------------------------------------------------------------- pose chain of frame-pair shards
+def _pose_results(n, seed=5):
+    """PnP results of n frame pairs: small motions, a few stale (-1) pairs."""
+    rng = np.random.default_rng(seed)
+    rv = rng.normal(0, 0.02, (n, 3))
+    tv = np.column_stack([rng.normal(0, 0.05, n), rng.normal(0, 0.05, n), rng.uniform(0.8, 1.2, n)])
+    ni = rng.integers(5, 200, n)
+    ni[[3, 5, 6]] = -1  # stale pairs, one of them the first pair of shard 1 (B = 5)
+    return rv, tv, ni
+
+
+def _chain_worker(rank, world, port, out, B, cuda):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "slam-1_amd")]
+    import torch
+    import torch.distributed as dist
+    from slam355.dist import gather_pose_chain
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    rv, tv, ni = _pose_results(world * B)
+    sl = slice(rank * B, (rank + 1) * B)
+    dev = "cuda" if cuda else "cpu"
+    if cuda:
+        torch.cuda.set_device(0)
+    pose0 = np.diag([1.0, 1.0, 1.0, 1.0])
+    pose0[:3, 3] = [0.5, -0.2, 3.0]
+    poses = gather_pose_chain(torch.tensor(rv[sl], device=dev), torch.tensor(tv[sl], device=dev),
+                              torch.tensor(ni[sl], dtype=torch.int32, device=dev), pose0=pose0)
+    if rank == 0:
+        np.save(out, poses.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_pose_chain_equals_one_chain(tmp_path):
+    """frame-pair shards + one gather of (rvec, tvec, n_inliers)
+    give the trajectory of one chain over all pairs, stale-T rule across the
+    shard boundary included (main.py:94-98, 120-124)."""
+    from slam355.pipeline import chain_poses
+
+    B, world = 5, 2
+    out = str(tmp_path / "poses.npy")
+    mp.spawn(_chain_worker, args=(world, _free_port(), out, B, False), nprocs=world, join=True)
+    rv, tv, ni = _pose_results(world * B)
+    pose0 = np.diag([1.0, 1.0, 1.0, 1.0])
+    pose0[:3, 3] = [0.5, -0.2, 3.0]
+    want, _ = chain_poses(pose0, rv, tv, ni)
+    assert np.array_equal(np.load(out), want)
+
+
+@pytest.mark.gpu
+def test_gpu_gather_pose_chain_equals_device_chain(tmp_path):
+    """The same on the device (k_pose_chain over the gathered results) against
+    one device chain over all pairs: bit-identical."""
+    import torch
+    from slam355 import _lib
+    from slam355.device import ptr, stream_ptr
+
+    B, world = 5, 2
+    out = str(tmp_path / "poses.npy")
+    mp.spawn(_chain_worker, args=(world, _free_port(), out, B, True), nprocs=world, join=True)
+    rv, tv, ni = _pose_results(world * B)
+    pose0 = np.diag([1.0, 1.0, 1.0, 1.0])
+    pose0[:3, 3] = [0.5, -0.2, 3.0]
+    n = world * B
+    d = "cuda"
+    trv, ttv = torch.tensor(rv, device=d), torch.tensor(tv, device=d)
+    tni = torch.tensor(ni, dtype=torch.int32, device=d)
+    state = torch.tensor(np.concatenate([pose0, np.eye(4)]).ravel(), device=d)
+    poses = torch.empty((n, 4, 4), dtype=torch.float64, device=d)
+    _lib.call("slam_pose_chain", ptr(trv), ptr(ttv), ptr(tni), n, ptr(state), ptr(poses),
+              stream_ptr(None))
+    assert np.array_equal(np.load(out), poses.cpu().numpy())
