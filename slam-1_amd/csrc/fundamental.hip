@@ -303,7 +303,14 @@ __device__ __forceinline__ float fm_error(const double* F, const double* p1, con
 // F's own slot (72 B per pair), which k_fm_finish then overwrites.
 constexpr int kSplit = 8;
 constexpr int kRound = 64;  // hypotheses per round (one per lane of wave 0)
+constexpr int kEv = 12;     // points per lane cached in registers (M <= 768 fully)
 static_assert(kSplit * 8 <= 9 * 8, "per-split bests must fit F[b]");
+#ifdef SLAM_FMH_TRACE
+__device__ unsigned long long g_fmh[8];
+#define FMH_T(i) do { if (threadIdx.x == 0 && blockIdx.x == 3 && blockIdx.y == 5) g_fmh[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define FMH_T(i) (void)0
+#endif
 
 __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all,
                                                 const double* __restrict__ m2all,
@@ -325,6 +332,10 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
   float my_best = INFINITY;
   int my_idx = 0x7FFFFFFF;
   const int need = M / 2 + 1;  // #errors below a value for the median to be below it
+  FMH_T(0);
+#ifdef SLAM_FMH_TRACE
+  int n_sel = 0, n_cand = 0;
+#endif
   for (int h0 = hb; h0 < he; h0 += kRound) {
     const int nh = min(kRound, he - h0);
     __syncthreads();
@@ -337,21 +348,58 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
       ncand[t] = seven_point(m1, m2, idx, cand[t]);
     }
     __syncthreads();
+    FMH_T(1);
+    // the candidates' errors at the lane's points i = lane + 64 j (j < kEv) are
+    // kept in registers for the median select (points past 64 kEv: recomputed);
+    // ln is opaque so that their addresses are not hoisted (live) across the
+    // seven-point solves, which need the whole register file
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    double pc[kEv][4];  // the points themselves, read once per round
+#pragma unroll
+    for (int j = 0; j < kEv; ++j) {
+      const int i = min(ln + 64 * j, M - 1);
+      pc[j][0] = m1[2 * i];
+      pc[j][1] = m1[2 * i + 1];
+      pc[j][2] = m2[2 * i];
+      pc[j][3] = m2[2 * i + 1];
+    }
     for (int hl = w; hl < nh; hl += kWaves) {
       for (int k = 0; k < ncand[hl]; ++k) {
         const double* F = cand[hl][k];
         int below = 0;
-        for (int i = lane; i < M; i += 64)
+        float ev[kEv];
+#pragma unroll
+        for (int j = 0; j < kEv; ++j) {
+          ev[j] = INFINITY;
+          if (ln + 64 * j < M) {
+            ev[j] = fm_error(F, pc[j], pc[j] + 2);
+            below += ev[j] < my_best ? 1 : 0;
+          }
+        }
+        for (int i = ln + 64 * kEv; i < M; i += 64)
           below += fm_error(F, m1 + 2 * i, m2 + 2 * i) < my_best ? 1 : 0;
         for (int off = 32; off > 0; off >>= 1) below += __shfl_xor(below, off, 64);
+#ifdef SLAM_FMH_TRACE
+        ++n_cand;
+#endif
         if (below < need) continue;  // median >= my_best: cannot improve (uniform)
+#ifdef SLAM_FMH_TRACE
+        ++n_sel;
+#endif
         // exact median = (M/2)-th smallest error, radix select on the float bits
         uint32_t prefix = 0, pmask = 0;
         int krank = M / 2;
         for (int shift = 24; shift >= 0; shift -= 8) {
           for (int j = lane; j < 256; j += 64) hist[w][j] = 0;
           __builtin_amdgcn_wave_barrier();
-          for (int i = lane; i < M; i += 64) {
+#pragma unroll
+          for (int j = 0; j < kEv; ++j) {
+            const uint32_t bits = __float_as_uint(ev[j]);
+            if (ln + 64 * j < M && (bits & pmask) == prefix)
+              atomicAdd(&hist[w][(bits >> shift) & 255u], 1);
+          }
+          for (int i = ln + 64 * kEv; i < M; i += 64) {
             const uint32_t bits = __float_as_uint(fm_error(F, m1 + 2 * i, m2 + 2 * i));
             if ((bits & pmask) == prefix) atomicAdd(&hist[w][(bits >> shift) & 255u], 1);
           }
@@ -391,11 +439,16 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
       }
     }
   }
+  FMH_T(2);
+#ifdef SLAM_FMH_TRACE
+  if (threadIdx.x == 0 && blockIdx.x == 3 && blockIdx.y == 5) { g_fmh[5] = n_cand; g_fmh[6] = n_sel; g_fmh[7] = M; }
+#endif
   if (lane == 0) {
     wbest[w] = my_best;
     wbidx[w] = my_idx;
   }
   __syncthreads();
+  FMH_T(3);
   if (t == 0) {
     float bm = INFINITY;
     int bi = 0x7FFFFFFF;
@@ -551,3 +604,11 @@ extern "C" int slam_filter_pairs(const int32_t* d_pairs, const int32_t* d_count,
   SLAM_LAUNCHED("k_filter_pairs");
   return SLAM_OK;
 }
+
+#ifdef SLAM_FMH_TRACE
+extern "C" int slam_fmh_trace(unsigned long long* out) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fmh), 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
+#endif

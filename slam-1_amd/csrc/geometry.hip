@@ -225,6 +225,7 @@ __device__ inline bool solve6(const double H[21], const double g[6], double lam,
 constexpr int kMinSample = 5;
 constexpr int kPnPWG = 256;
 constexpr int kMaxHyp = 256;
+constexpr int kRc = 4;  // refinement points per lane held in registers (L <= 256 fully)
 
 // Levenberg-Marquardt on a hypothesis' sample (oracle/geometry.c lm with idx)
 // on a 16-lane group (lane k = lane & 15): lanes s < n evaluate
@@ -237,9 +238,9 @@ constexpr int kMaxHyp = 256;
 __device__ void lm_group(const double* Q, const double* q, int n, const Cam& K, int iters,
                          double p[6], int k, double (*t)[28], double* sums) {
   double lam = 1e-3;
+  double R[9];  // rotation of p: carried over from the trial pose when a step is accepted
+  rodrigues(p, R);
   for (int it = 0; it < iters; ++it) {
-    double R[9];
-    rodrigues(p, R);
     if (k < n) {
       double r[2], J[2][6];
       pnp_residual<true>(p, R, Q + 3 * k, q + 2 * k, K, r, J);
@@ -296,6 +297,7 @@ __device__ void lm_group(const double* Q, const double* q, int n, const Cam& K, 
     __syncthreads();
     if (cn < cost) {
       for (int i = 0; i < 6; ++i) p[i] = pn[i];
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
       lam = fmax(lam * 0.1, 1e-12);
     } else {
       lam = fmin(lam * 10.0, 1e12);
@@ -308,6 +310,41 @@ __device__ __forceinline__ double wave_allsum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Sums of 32 values over the 64 lanes of a wave, every lane ends with all 32
+// totals (v[k] = total k).  Reduce-scatter by halving: at offset 32, 16, .., 2
+// a lane keeps the half of its values its partner does not (one shuffle per
+// kept value: 16 + 8 + 4 + 2 + 1, then one at offset 1), so total j ends on
+// lanes 2j and 2j+1 and is broadcast by v_readlane -- 32 double shuffles
+// instead of 6 per value of the xor butterfly.
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const unsigned long long u = __double_as_longlong(x);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int OFF>
+__device__ __forceinline__ void allsum_halve(double (&v)[32], int lane) {
+  constexpr int half = OFF / 2;
+  const bool hi = (lane & OFF) != 0;
+#pragma unroll
+  for (int k = 0; k < half; ++k) {
+    const double send = hi ? v[k] : v[k + half];
+    const double keep = hi ? v[k + half] : v[k];
+    v[k] = keep + __shfl_xor(send, OFF, 64);
+  }
+}
+__device__ __forceinline__ void wave_allsum32(double (&v)[32]) {
+  const int lane = threadIdx.x & 63;
+  allsum_halve<32>(v, lane);
+  allsum_halve<16>(v, lane);
+  allsum_halve<8>(v, lane);
+  allsum_halve<4>(v, lane);
+  allsum_halve<2>(v, lane);
+  const double tot = v[0] + __shfl_xor(v[0], 1, 64);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) v[j] = readlane_d(tot, 2 * j);
 }
 
 // PnP-RANSAC hypotheses: kHypGroups per one-wave workgroup, a 16-lane group
@@ -494,17 +531,27 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
   // ---- LM refinement over the winner's inliers (fixed set), wave 0
   double p[6];
   for (int i = 0; i < 6; ++i) p[i] = hp[bh][i];
-  double lam = 1e-3;
-  for (int it = 0; it < refine_iters; ++it) {
-    double R[9];
-    rodrigues(p, R);
-    double acc[28];
+  // the lane's points i = lane + 64 j (j < kRc) and their inlier flags in
+  // registers for all refine_iters iterations (points past 64 kRc: re-read)
+  double rq[kRc][5];
+  bool rin[kRc];
 #pragma unroll
-    for (int i = 0; i < 28; ++i) acc[i] = 0.0;
-    for (int i = lane; i < L; i += 64) {
-      if (!mk[i]) continue;
+  for (int j = 0; j < kRc; ++j) {
+    const int i = lane + 64 * j, ic = min(i, L - 1);
+    rin[j] = i < L && mk[i] != 0;
+    for (int d = 0; d < 3; ++d) rq[j][d] = Q[3 * ic + d];
+    for (int d = 0; d < 2; ++d) rq[j][3 + d] = q[2 * ic + d];
+  }
+  double lam = 1e-3;
+  double R[9];  // rotation of p: carried over from the trial pose when a step is accepted
+  rodrigues(p, R);
+  for (int it = 0; it < refine_iters; ++it) {
+    double acc[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc[i] = 0.0;
+    auto add_terms = [&](const double* Qi, const double* qi) {
       double r[2], J[2][6];
-      pnp_residual<true>(p, R, Q + 3 * i, q + 2 * i, K, r, J);
+      pnp_residual<true>(p, R, Qi, qi, K, r, J);
 #pragma unroll
       for (int a = 0; a < 2; ++a) {
         int k = 0;
@@ -516,19 +563,32 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
         }
         acc[27] += r[a] * r[a];
       }
-    }
+    };
+#pragma unroll
+    for (int j = 0; j < kRc; ++j)
+      if (rin[j]) add_terms(rq[j], rq[j] + 3);
+    for (int i = lane + 64 * kRc; i < L; i += 64)
+      if (mk[i]) add_terms(Q + 3 * i, q + 2 * i);
+    wave_allsum32(acc);
     double H[21], g[6];
 #pragma unroll
-    for (int i = 0; i < 21; ++i) H[i] = wave_allsum(acc[i]);
+    for (int i = 0; i < 21; ++i) H[i] = acc[i];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) g[i] = wave_allsum(acc[21 + i]);
-    const double cost = wave_allsum(acc[27]);
+    for (int i = 0; i < 6; ++i) g[i] = acc[21 + i];
+    const double cost = acc[27];
     double d[6], pn[6], Rn[9];
     const bool ok = solve6(H, g, lam, d);
     for (int i = 0; i < 6; ++i) pn[i] = ok ? p[i] + d[i] : p[i];
     rodrigues(pn, Rn);
     double cn = 0.0;
-    for (int i = lane; i < L; i += 64) {
+#pragma unroll
+    for (int j = 0; j < kRc; ++j)
+      if (rin[j]) {
+        double r[2], J[2][6];
+        pnp_residual<false>(pn, Rn, rq[j], rq[j] + 3, K, r, J);
+        cn += r[0] * r[0] + r[1] * r[1];
+      }
+    for (int i = lane + 64 * kRc; i < L; i += 64) {
       if (!mk[i]) continue;
       double r[2], J[2][6];
       pnp_residual<false>(pn, Rn, Q + 3 * i, q + 2 * i, K, r, J);
@@ -537,6 +597,7 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
     cn = wave_allsum(cn);
     if (ok && cn < cost) {
       for (int i = 0; i < 6; ++i) p[i] = pn[i];
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
       lam = fmax(lam * 0.1, 1e-12);
     } else {
       lam = fmin(lam * 10.0, 1e12);
