@@ -23,8 +23,13 @@
 
 namespace {
 
-constexpr int kWG = 512;
-constexpr int kWaves = kWG / 64;
+#ifndef SLAM_FMH_WG
+#define SLAM_FMH_WG 256
+#endif
+// k_fm_hyp workgroup: its ~254-VGPR waves need a whole SIMD's register file two
+// at a time, so the size decides which CUs (next to ORB's waves or idle) take it
+constexpr int kHWG = SLAM_FMH_WG, kHWaves = kHWG / 64;
+constexpr int kFWG = 64;  // k_fm_finish: one wave (lane 0 recomputes the winner, then the mask)
 constexpr int kS = 7;
 
 __device__ inline uint64_t splitmix64(uint64_t& s) {
@@ -312,16 +317,16 @@ __device__ unsigned long long g_fmh[8];
 #define FMH_T(i) (void)0
 #endif
 
-__global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all,
+__global__ __launch_bounds__(kHWG) void k_fm_hyp(const double* __restrict__ m1all,
                                                 const double* __restrict__ m2all,
                                                 const int32_t* __restrict__ count, int cap,
                                                 uint64_t seed, int item0, int n_hyp,
                                                 double* __restrict__ Fout) {
   __shared__ double cand[kRound][3][9];  // hypotheses processed in rounds of kRound
   __shared__ int ncand[kRound];
-  __shared__ int hist[kWaves][256];
-  __shared__ float wbest[kWaves];
-  __shared__ int wbidx[kWaves];
+  __shared__ int hist[kHWaves][256];
+  __shared__ float wbest[kHWaves];
+  __shared__ int wbidx[kHWaves];
   const int b = blockIdx.x, sp = blockIdx.y, t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int M = min(max(count[b], 0), cap);
@@ -364,7 +369,7 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
       pc[j][2] = m2[2 * i];
       pc[j][3] = m2[2 * i + 1];
     }
-    for (int hl = w; hl < nh; hl += kWaves) {
+    for (int hl = w; hl < nh; hl += kHWaves) {
       for (int k = 0; k < ncand[hl]; ++k) {
         const double* F = cand[hl][k];
         int below = 0;
@@ -452,7 +457,7 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
   if (t == 0) {
     float bm = INFINITY;
     int bi = 0x7FFFFFFF;
-    for (int i = 0; i < kWaves; ++i)
+    for (int i = 0; i < kHWaves; ++i)
       if (wbest[i] < bm || (wbest[i] == bm && wbidx[i] < bi)) {
         bm = wbest[i];
         bi = wbidx[i];
@@ -463,7 +468,7 @@ __global__ __launch_bounds__(kWG) void k_fm_hyp(const double* __restrict__ m1all
   }
 }
 
-__global__ __launch_bounds__(kWG) void k_fm_finish(const double* __restrict__ m1all,
+__global__ __launch_bounds__(kFWG) void k_fm_finish(const double* __restrict__ m1all,
                                                    const double* __restrict__ m2all,
                                                    const int32_t* __restrict__ count, int cap,
                                                    uint64_t seed, int item0,
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(kWG) void k_fm_finish(const double* __restrict__ m1
   const double* m2 = m2all + (size_t)b * cap * 2;
   uint8_t* mk = mask + (size_t)b * cap;
   if (M < 8) {
-    for (int i = t; i < M; i += kWG) mk[i] = 0;
+    for (int i = t; i < M; i += kFWG) mk[i] = 0;
     if (t == 0) ninl[b] = -1;
     return;
   }
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(kWG) void k_fm_finish(const double* __restrict__ m1
   }
   __syncthreads();
   if (!found_s) {
-    for (int i = t; i < M; i += kWG) mk[i] = 0;
+    for (int i = t; i < M; i += kFWG) mk[i] = 0;
     if (t == 0) ninl[b] = -1;
     return;
   }
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(kWG) void k_fm_finish(const double* __restrict__ m1
   double F[9];
   for (int i = 0; i < 9; ++i) F[i] = Fb[i];
   int c = 0;
-  for (int i = t; i < M; i += kWG) {
+  for (int i = t; i < M; i += kFWG) {
     const uint8_t in = (double)fm_error(F, m1 + 2 * i, m2 + 2 * i) <= thr ? 1 : 0;
     mk[i] = in;
     c += in;
@@ -582,9 +587,9 @@ extern "C" int slam_fundamental_lmeds(const double* d_m1, const double* d_m2,
   SLAM_REQUIRE(d_m1 && d_m2 && d_count && d_mask && d_F && d_ninliers,
                "slam_fundamental_lmeds: null pointer");
   hipStream_t s = slam::as_stream(stream);
-  k_fm_hyp<<<dim3(batch, kSplit), kWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, n_hyp, d_F);
+  k_fm_hyp<<<dim3(batch, kSplit), kHWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, n_hyp, d_F);
   SLAM_LAUNCHED("k_fm_hyp");
-  k_fm_finish<<<batch, kWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, d_mask, d_F,
+  k_fm_finish<<<batch, kFWG, 0, s>>>(d_m1, d_m2, d_count, cap, seed, item0, d_mask, d_F,
                                     d_ninliers);
   SLAM_LAUNCHED("k_fm_finish");
   return SLAM_OK;
