@@ -393,10 +393,12 @@ def run_tracking(args, world, rank):
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_assemble", "k_solve_blk",
                                                   "k_back_trial<true>"))
-    for r in roof.values():
+    units = {"orb": f"bytes per ORB launch ({n_img} images), HBM, from PMC",
+             "local_ba": f"bytes per batched LM iteration ({n_launch} windows), HBM, from PMC"}
+    for name, r in roof.items():
         r["frac"] = r["achieved"] / r["peak"]
         if r["traffic"] is not None:
-            r["traffic_unit"] = "bytes per launch (LM iteration for local_ba), HBM, from PMC"
+            r["traffic_unit"] = units[name]
             r["traffic_source"] = pmc["path"]
     per_step = {k: v for k, v in stages.items()}
     if G > 1 and "local_ba" in per_step:  # one launch set per G steps
