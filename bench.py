@@ -661,11 +661,18 @@ def run_ba_batch(args, world, rank):
     C, P, k = 10, 5000, 6
     rng = np.random.default_rng(7 + rank)
     probs = []
+    # chunks per linearisation workgroup: with the whole GPU to itself a batch
+    # of 8 windows is fastest at 5 (3 -> 46.1k, 5 -> 50.3k, 8 -> 41.0k
+    # window-iters/s; 4 windows: 3 and 5 within noise, 121.5 / 123.4 us); the
+    # tracking bench, which leaves BA about 40 CUs beside ORB, uses 8
+    cpw = args.chunks_per_wg
+    if cpw is None and args.ba_batch >= 8:
+        cpw = 5
     for _ in range(args.ba_batch):
         cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
         c0, p0 = perturb(rng, cams, pts)
         probs.append(BAProblem(c0, p0, ci, pi, qs, lin_mode=args.lin_mode,
-                               chunks_per_wg=args.chunks_per_wg))
+                               chunks_per_wg=cpw))
     # --ba-streams S: the windows split into S batches on S streams, so one
     # batch's latency-bound camera solve overlaps another's linearisation
     ns = max(1, min(args.ba_streams, len(probs)))
