@@ -756,41 +756,49 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 // Concatenate the tiles of each image in orb.py order.
-__global__ __launch_bounds__(256) void k_orb_compact(const float* __restrict__ ws_kp,
-                                                     const int32_t* __restrict__ ws_oct,
-                                                     const uint8_t* __restrict__ ws_desc,
-                                                     const int32_t* __restrict__ ws_cnt,
-                                                     int n_tiles, int tcap, float* __restrict__ kp,
-                                                     int32_t* __restrict__ oct,
-                                                     uint8_t* __restrict__ desc,
-                                                     int32_t* __restrict__ count, int kp_cap) {
-  __shared__ int off[kMaxTiles + 1];
-  __shared__ int bad;
-  const int b = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int s = 0, ovf = 0;
-    for (int i = 0; i < n_tiles; ++i) {
-      off[i] = s;
-      const int c = ws_cnt[(size_t)b * n_tiles + i];
-      if (c < 0) ovf = 1;
-      s += c < 0 ? 0 : c;
-    }
-    off[n_tiles] = s;
-    bad = ovf || s > kp_cap;
-    count[b] = bad ? -s - 1 : s;
+// One wave per (image, tile): the tile's offset is the sum of the counts of the
+// tiles before it (every wave reads the image's counts, <= kMaxTiles), its
+// keypoints, octaves and descriptors are copied to [off, off + n).  A negative
+// tile count (retained ties overflowed the tile's slots) or a total above
+// kp_cap marks the image with count = -total - 1 and copies nothing.  (One
+// workgroup per image walking its tiles in turn was 36 dependent load/store
+// rounds: 63 us per 65 images.)
+__global__ __launch_bounds__(64) void k_orb_compact(const float* __restrict__ ws_kp,
+                                                    const int32_t* __restrict__ ws_oct,
+                                                    const uint8_t* __restrict__ ws_desc,
+                                                    const int32_t* __restrict__ ws_cnt,
+                                                    int n_tiles, int tcap, float* __restrict__ kp,
+                                                    int32_t* __restrict__ oct,
+                                                    uint8_t* __restrict__ desc,
+                                                    int32_t* __restrict__ count, int kp_cap) {
+  const int b = blockIdx.x, i = blockIdx.y, lane = threadIdx.x;
+  const int32_t* cnt = ws_cnt + (size_t)b * n_tiles;
+  int before = 0, total = 0, ovf = 0;
+  for (int t0 = 0; t0 < n_tiles; t0 += 64) {
+    const int tt = t0 + lane;
+    const int c = tt < n_tiles ? cnt[tt] : 0;
+    ovf |= c < 0 ? 1 : 0;
+    const int cc = c < 0 ? 0 : c;
+    total += cc;
+    before += tt < i ? cc : 0;
   }
-  __syncthreads();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    total += __shfl_xor(total, o, 64);
+    before += __shfl_xor(before, o, 64);
+    ovf |= __shfl_xor(ovf, o, 64);
+  }
+  const bool bad = ovf != 0 || total > kp_cap;
+  if (i == 0 && lane == 0) count[b] = bad ? -total - 1 : total;
   if (bad) return;
-  for (int i = 0; i < n_tiles; ++i) {
-    const int n = off[i + 1] - off[i];
-    const size_t src = ((size_t)b * n_tiles + i) * tcap;
-    const size_t dst = (size_t)b * kp_cap + off[i];
-    for (int j = threadIdx.x; j < n * 5; j += 256) kp[dst * 5 + j] = ws_kp[src * 5 + j];
-    for (int j = threadIdx.x; j < n; j += 256) oct[dst + j] = ws_oct[src + j];
-    for (int j = threadIdx.x; j < n * 8; j += 256)
-      reinterpret_cast<uint32_t*>(desc)[dst * 8 + j] =
-          reinterpret_cast<const uint32_t*>(ws_desc)[src * 8 + j];
-  }
+  const int n = cnt[i];
+  const size_t src = ((size_t)b * n_tiles + i) * tcap;
+  const size_t dst = (size_t)b * kp_cap + before;
+  for (int j = lane; j < n * 5; j += 64) kp[dst * 5 + j] = ws_kp[src * 5 + j];
+  for (int j = lane; j < n; j += 64) oct[dst + j] = ws_oct[src + j];
+  for (int j = lane; j < n * 8; j += 64)
+    reinterpret_cast<uint32_t*>(desc)[dst * 8 + j] =
+        reinterpret_cast<const uint32_t*>(ws_desc)[src * 8 + j];
 }
 
 // ---------------------------------------------------------------- host side
@@ -1004,8 +1012,9 @@ extern "C" int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int
                                                                   ws_desc, ws_cnt, ws_cand,
                                                                   ws_lvl);
   SLAM_LAUNCHED("k_orb_tile");
-  k_orb_compact<<<batch, 256, 0, s>>>(ws_kp, ws_oct, ws_desc, ws_cnt, g.n_tiles, g.tcap, d_kp,
-                                      d_octave, d_desc, d_count, kp_cap);
+  k_orb_compact<<<dim3(batch, g.n_tiles), 64, 0, s>>>(ws_kp, ws_oct, ws_desc, ws_cnt, g.n_tiles,
+                                                      g.tcap, d_kp, d_octave, d_desc, d_count,
+                                                      kp_cap);
   SLAM_LAUNCHED("k_orb_compact");
   return SLAM_OK;
 }
