@@ -1005,39 +1005,60 @@ __global__ __launch_bounds__(kBS) void k_vo_residuals(
 // previous T is reused (stale); pose_{b+1} = pose_b @ T_b.  state [32] =
 // (pose 4x4, T 4x4) row-major carries the chain across calls, so consecutive
 // tracking batches chain without a host round trip.  One lane: B 4x4 products.
-__global__ void k_pose_chain(const double* __restrict__ rvec, const double* __restrict__ tvec,
-                             const int32_t* __restrict__ ninl, int B, double* __restrict__ state,
-                             double* __restrict__ poses) {
-  if (threadIdx.x != 0) return;
-  double P[16], T[16];
-  for (int i = 0; i < 16; ++i) {
-    P[i] = state[i];
-    T[i] = state[16 + i];
+// Pose chain of a batch (main.py:94-98,120-124): lanes build the pairs' T_b
+// (Rodrigues of -rvec, -tvec) in parallel into LDS, then 16 lanes advance
+// P <- P T one element each (the same expression as the serial form, so the
+// poses are bit-identical), a pair with ninl < 0 keeping the previous T.
+// (One lane doing both for every pair was 41 us per 32 pairs.)
+__global__ __launch_bounds__(64) void k_pose_chain(const double* __restrict__ rvec,
+                                                   const double* __restrict__ tvec,
+                                                   const int32_t* __restrict__ ninl, int B,
+                                                   double* __restrict__ state,
+                                                   double* __restrict__ poses) {
+  __shared__ double Tb[64][16];
+  __shared__ int val[64];
+  __shared__ double P[16], T[16];
+  const int t = threadIdx.x;
+  if (t < 16) {
+    P[t] = state[t];
+    T[t] = state[16 + t];
   }
-  for (int b = 0; b < B; ++b) {
-    if (ninl[b] >= 0) {
-      const double r[3] = {-rvec[3 * b], -rvec[3 * b + 1], -rvec[3 * b + 2]};
-      double R[9];
-      rodrigues(r, R);
-      for (int i = 0; i < 3; ++i) {
-        for (int j = 0; j < 3; ++j) T[4 * i + j] = R[3 * i + j];
-        T[4 * i + 3] = -tvec[3 * b + i];
+  const int ei = (t & 15) >> 2, ej = t & 3;
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    const int nb = min(64, B - b0), b = b0 + t;
+    if (t < nb) {
+      const bool v = ninl[b] >= 0;
+      val[t] = v ? 1 : 0;
+      if (v) {
+        const double r[3] = {-rvec[3 * b], -rvec[3 * b + 1], -rvec[3 * b + 2]};
+        double R[9];
+        rodrigues(r, R);
+        for (int i = 0; i < 3; ++i) {
+          for (int j = 0; j < 3; ++j) Tb[t][4 * i + j] = R[3 * i + j];
+          Tb[t][4 * i + 3] = -tvec[3 * b + i];
+        }
+        Tb[t][12] = 0.0; Tb[t][13] = 0.0; Tb[t][14] = 0.0; Tb[t][15] = 1.0;
       }
-      T[12] = 0.0; T[13] = 0.0; T[14] = 0.0; T[15] = 1.0;
     }
-    double N[16];
-    for (int i = 0; i < 4; ++i)
-      for (int j = 0; j < 4; ++j)
-        N[4 * i + j] = P[4 * i] * T[j] + P[4 * i + 1] * T[4 + j] + P[4 * i + 2] * T[8 + j] +
-                       P[4 * i + 3] * T[12 + j];
-    for (int i = 0; i < 16; ++i) {
-      P[i] = N[i];
-      poses[16 * b + i] = N[i];
+    __syncthreads();
+    for (int k = 0; k < nb; ++k) {
+      if (val[k] && t < 16) T[t] = Tb[k][t];
+      __syncthreads();
+      double n = 0.0;
+      if (t < 16)
+        n = P[4 * ei] * T[ej] + P[4 * ei + 1] * T[4 + ej] + P[4 * ei + 2] * T[8 + ej] +
+            P[4 * ei + 3] * T[12 + ej];
+      __syncthreads();
+      if (t < 16) {
+        P[t] = n;
+        poses[16 * (b0 + k) + t] = n;
+      }
+      __syncthreads();
     }
   }
-  for (int i = 0; i < 16; ++i) {
-    state[i] = P[i];
-    state[16 + i] = T[i];
+  if (t < 16) {
+    state[t] = P[t];
+    state[16 + t] = T[t];
   }
 }
 
