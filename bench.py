@@ -34,7 +34,9 @@ for _p in (ROOT, os.path.join(ROOT, "slam-1_amd")):
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from slam355.pipeline import Tracker  # noqa: E402
+# slam355 (libslam355.so) is imported inside the workloads only: with --gpus N > 1
+# and no WORLD_SIZE in the environment, main() starts the N ranks as a child
+# process before anything here touches HIP (launch_ranks)
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -65,6 +67,24 @@ def dist_init():
     else:
         torch.cuda.set_device(0)
     return world, rank
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: run N ranks of this same command
+    under torch.distributed.run as a CHILD process (this process has not touched
+    HIP and never execs), rendezvous on 127.0.0.1; rank 0's JSON line reaches
+    stdout through the child's inherited stdout.  Returns the child's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:  # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS=os.environ.get(
+        "OMP_NUM_THREADS", "1"))).returncode
 
 
 def barrier(world):
@@ -215,6 +235,7 @@ class FrameFeed:
 
 def run_tracking(args, world, rank):
     from slam355.ba import BABatch, BAProblem
+    from slam355.pipeline import Tracker
     from slam355.synthetic import ba_problem, corridor_sequence, perturb
 
     B = args.batch
@@ -935,6 +956,12 @@ def main():
     ap.add_argument("--ba-cus", type=int, default=0,
                     help="disjoint CU partition: local BA on the last N CUs, tracking on the rest")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')} but --gpus {args.gpus}",
+              file=sys.stderr)
+        sys.exit(2)
     world, rank = dist_init()
     run = {"tracking": run_tracking, "ba": run_ba, "matcher": run_matcher,
            "vo": run_vo}[args.workload]

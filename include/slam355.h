@@ -141,8 +141,10 @@ int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32_t* d_count
                     int batch, const double* d_K, uint64_t seed, int item0, int n_hyp,
                     double reproj_thresh, int hyp_iters, int refine_iters, double* d_rvec,
                     double* d_tvec, int32_t* d_ninliers, uint8_t* d_mask, double* d_ws,
-                    void* stream);
-/* Doubles of slam_pnp_ransac's workspace d_ws (the hypothesis poses). */
+                    long long ws_len, void* stream);
+/* Doubles of slam_pnp_ransac's workspace d_ws (the hypothesis poses); a d_ws of
+ * fewer than this many doubles (ws_len) returns SLAM_ERR_WORKSPACE.  The
+ * workspace is the caller's: calls that may overlap (other streams) need their own. */
 long long slam_pnp_workspace_len(int batch, int n_hyp);
 
 /* Pose chain of main.py:94-98, 120-124 (pose_{b+1} = pose_b @ T_b with
@@ -279,8 +281,12 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
 #define SLAM_BA_ST_ITERS 8
 #define SLAM_BA_ST_NACCEPT 9
 #define SLAM_BA_ST_PRED_CAM 10
-#define SLAM_BA_ST_CHOL_FAIL 11
-#define SLAM_BA_ST_SLOTS 16
+#define SLAM_BA_ST_CHOL_FAIL 11 /* last solve: 0 ok, 1 not SPD, 2 dataflow solve timed out */
+/* slots 12..15: phase timers of the profiling builds */
+#define SLAM_BA_ST_SOLVE_FAULT 16 /* sticky: camera solves that timed out waiting for a
+                                     * co-resident workgroup (never set by a correct launch;
+                                     * the Python layer raises when it is non-zero) */
+#define SLAM_BA_ST_SLOTS 20
 
 /* Everything the LM iteration touches; all pointers are device pointers.
  * Built by the host planner (slam355/ba.py): observations sorted by

@@ -56,10 +56,14 @@ int main(void) {
   expect_arg(slam_fundamental_lmeds(NULL, P, P, 16, 1, 0, 0, 10, P, P, P, NULL), "fm null");
   expect_arg(slam_filter_pairs(P, P, P, -1, 1, P, P, NULL), "filter cap<0");
   expect_arg(slam_triangulate(P, P, P, 10, 1, P, P, 0, NULL, NULL), "tri null X");
-  expect_arg(slam_pnp_ransac(P, P, P, 16, 1, P, 0, 0, 0, 2.0, 10, 10, P, P, P, P, P, NULL),
+  expect_arg(slam_pnp_ransac(P, P, P, 16, 1, P, 0, 0, 0, 2.0, 10, 10, P, P, P, P, P, 0, NULL),
              "pnp n_hyp=0");
-  expect_arg(slam_pnp_ransac(P, P, P, 16, 1, P, 0, 0, 64, 2.0, 10, 10, P, P, P, P, NULL, NULL),
+  expect_arg(slam_pnp_ransac(P, P, P, 16, 1, P, 0, 0, 64, 2.0, 10, 10, P, P, P, P, NULL, 384, NULL),
              "pnp null workspace");
+  expect_rc(slam_pnp_ransac(P, P, P, 16, 2, P, 0, 0, 64, 2.0, 10, 10, P, P, P, P, P, 767, NULL),
+            SLAM_ERR_WORKSPACE, "pnp workspace too short");
+  expect_arg(slam_ba_iterate_batch(NULL, 3, 1, NULL), "ba iterate_batch null array");
+  expect_arg(slam_ba_reset_batch(NULL, 2, 1e-4, NULL), "ba reset_batch null array");
   expect(slam_pnp_workspace_len(4, 128) == 4LL * 128 * 6, "pnp workspace len");
   expect(slam_pnp_workspace_len(1 << 30, 1 << 30) > 0, "pnp workspace len no int overflow");
   expect_arg(slam_pose_chain(P, P, P, 1, NULL, P, NULL), "pose_chain null state");

@@ -15,7 +15,7 @@
 //                             b = -Jc^T r - Jc^T u, g, diag U, cost
 //   (all-reduce of sys over ranks happens here for multi-GPU)
 //   k_solve_blk     1 WG   -> damp, blocked LDL^T (MFMA trailing updates), camera
-//                             step, pred_cam, trial cameras (tiled k_tl_* for 9C > 120)
+//                             step, pred_cam, trial cameras (tiled k_tl3_flow / k_tl2_* for 9C > 120)
 //   k_back_trial    point group -> point step, trial points, trial |r|^2 and
 //                                  pred partials; the last group sums them into
 //                                  small (and, single rank, decides)
@@ -1011,13 +1011,13 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
 // ---------------------------------------------------------------- solve
 // Reduced camera system S x = b, S SPD (damped).  Two solvers: k_solve_blk
 // (one workgroup, whole system in LDS/registers) for the local-BA window
-// (9C <= kLdsMaxN), and the tiled multi-workgroup Cholesky k_tl_* below for
+// (9C <= kLdsMaxN), and the tiled multi-workgroup Cholesky (k_tl3_flow, k_tl2_*) for
 // larger systems.
 constexpr int kLdsMaxN = kDenseMaxN;  // k_solve_blk keeps the system in LDS up to 9C = 120
 constexpr int kSolveHdr = 32;   // doubles of LDS header in k_solve_blk
 
 // Inputs of the epilogue: camera gradient, Gram diagonal, live cameras and the
-// per-camera cost partials (global memory in k_tl_epilogue, LDS copies prefetched at
+// per-camera cost partials (global memory in the tiled solves, LDS copies prefetched at
 // kernel start in k_solve_blk so their latency is off the critical path).
 struct EpiSrc {
   const double *g, *dU, *cam, *costc;
@@ -1026,7 +1026,7 @@ struct EpiSrc {
 // Shared epilogue: camera step, trial cameras, predicted reduction of the camera
 // part, LM cost at the live parameters.
 __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool ok, double* red,
-                               const EpiSrc& e) {
+                               const EpiSrc& e, int fail_code = 1) {
   const int C9 = 9 * p.n_cams, t = threadIdx.x;
   double* state = p.state;
   const double lam = state[SLAM_BA_ST_LAMBDA];
@@ -1046,7 +1046,8 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
     for (int c = 0; c < p.n_cams; ++c) cost += e.costc[c];
     state[SLAM_BA_ST_COST] = 0.5 * cost;
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
-    state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : 1.0;
+    state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : (double)fail_code;
+    if (!ok && fail_code == 2) state[SLAM_BA_ST_SOLVE_FAULT] += 1.0;
   }
 }
 
@@ -1446,24 +1447,17 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
 
 // ---------------------------------------------------------------- tiled solve
 // Large reduced camera systems (9C > kLdsMaxN: the sharded C4 window, global
-// BA): right-looking blocked Cholesky LL^T over 64x64 f64 tiles, spread over
-// many workgroups, one launch per phase:
-//   k_tl_load         lower tile (I, J): damped S -> A (padded to N = 64T,
-//                     identity on the padded diagonal), b, tile-nonzero flags
-//   k_tl_panel(k)     WG per row tile I >= k: every WG factors A_kk and
-//                     inverts it (blocked over 16x16 blocks: diagonal blocks
-//                     in wave 0's registers, panel / trailing / inverse
-//                     blocks on the f64 matrix cores); WG I = k stores
-//                     L_kk^-1 (dinv[k]) and y_k = L_kk^-1 b_k; WG I > k
-//                     forms L_Ik = A_Ik L_kk^-T on the f64 matrix cores and
-//                     updates b_I -= L_Ik y_k (forward substitution fused)
-//   k_tl_update(k)    WG per trailing lower tile (I >= J > k) with both L_Ik
-//                     and L_Jk nonzero: A_IJ -= L_Ik L_Jk^T (MFMA f64 16x16x4)
-//   k_tl_back(k)      k = T-1 .. 0: x_k = L_kk^-T y_k; WG J < k: y_J -= L_kJ^T x_k
-//   k_tl_epilogue     1 WG: camera step, trial cameras, predicted reduction
-// Tiles that stay structurally zero (cameras without common points: banded
-// windows, long trajectories) are skipped: nz[I][J] is set by the load and by
-// any update that writes the tile, so fill-in is tracked exactly.
+// BA): blocked Cholesky LL^T over 64x64 f64 tiles in the nested-dissection
+// tile order of ba.tl_schedule (symbolic structure on the host), two forms:
+//   k_tl3_flow    one launch, one persistent workgroup per tile column; device
+//                 flags replace launch boundaries (the default);
+//   k_tl2_*       the same tile operations level by level as separate launches
+//                 (when the columns cannot all be resident: more tiles than
+//                 the stream's CUs, or tl_mode "levels").
+// Both start from k_tl2_load / k_tl2_scatter (damped S -> lower tiles, b) and
+// end in solve_epilogue.  The diagonal-tile factor + inverse is
+// tile_chol_inv_blk (16x16 diagonal blocks in wave 0's registers, the rest on
+// the f64 matrix cores).
 constexpr int kTB = 64;        // tile edge
 constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
 
@@ -1531,56 +1525,6 @@ __device__ __forceinline__ void gemm_xyT(const double* Xf, const double* Yf, d4 
 
 __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayout& L) {
   return *reinterpret_cast<const volatile int*>(p.chol + L.fail) != 0;
-}
-
-// Lower tile (I, J): zeros (identity on the padded diagonal), tile flag
-// cleared (diagonal tiles always live); the diagonal tiles also load b.
-__global__ __launch_bounds__(kTlWG) void k_tl_load(slam_ba_problem p) {
-  lm_wave_priority();
-  const int n = 9 * p.n_cams;
-  const TlLayout L(n);
-  const int idx = blockIdx.x;
-  int I = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
-  while ((I + 1) * (I + 2) / 2 <= idx) ++I;
-  while (I * (I + 1) / 2 > idx) --I;
-  const int J = idx - I * (I + 1) / 2;
-  double* A = p.chol + L.a;
-  for (int e = threadIdx.x; e < kTB * kTB; e += kTlWG) {
-    const int i = I * kTB + (e >> 6), j = J * kTB + (e & 63);
-    A[(size_t)i * L.N + j] = (i == j && i >= n) ? 1.0 : 0.0;
-  }
-  if (threadIdx.x == 0) reinterpret_cast<uint8_t*>(p.chol + L.nz)[I * L.T + J] = I == J ? 1 : 0;
-  if (I == J && threadIdx.x < kTB) {
-    const int i = I * kTB + threadIdx.x;
-    p.chol[L.b + i] = i < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + i] : 0.0;
-  }
-  if (idx == 0 && threadIdx.x == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 0;
-}
-
-// One workgroup per packed block (c1 <= c2) of sys: its 81 values into the
-// lower tiles of A (transposed for c1 < c2), mirrored inside diagonal tiles,
-// camera damping lam * clamp(diag U) on the diagonal; flags the tiles it hits.
-__global__ __launch_bounds__(128) void k_tl_scatter(slam_ba_problem p) {
-  lm_wave_priority();
-  const int n = 9 * p.n_cams;
-  const TlLayout L(n);
-  const int blk = blockIdx.x, t = threadIdx.x;
-  if (t >= 81) return;
-  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
-  const double* vec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
-  const int i = t / 9, j = t - 9 * (t / 9);
-  const int r = 9 * c1 + i, c = 9 * c2 + j;  // element (r, c) of S
-  double v = p.sys[(size_t)blk * 81 + t];
-  if (r == c) v += p.state[SLAM_BA_ST_LAMBDA] * clampd(vec[2 * n + r]);
-  double* A = p.chol + L.a;
-  uint8_t* nz = reinterpret_cast<uint8_t*>(p.chol + L.nz);
-  const int tr = r / kTB, tc = c / kTB;
-  if (r >= c || tr == tc) A[(size_t)r * L.N + c] = v;  // lower, or inside a diagonal tile
-  if (r > c && tr != tc) nz[tr * L.T + tc] = 1;        // a diagonal block across a tile edge
-  if (c1 != c2) {
-    A[(size_t)c * L.N + r] = v;                       // the mirrored element (lower)
-    if (tr != tc) nz[tc * L.T + tr] = 1;
-  }
 }
 
 // Blocked factor + inverse of the 64x64 diagonal tile (4 x 4 blocks of 16):
@@ -1780,188 +1724,6 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   TL_STAMP(3);
   FAC_T(13);
   return *okp != 0;
-}
-
-__global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_tl_panel(slam_ba_problem p, int k) {
-  lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
-  if (tl_failed(p, L)) return;
-  const int I = k + blockIdx.x;
-  const uint8_t* nz = reinterpret_cast<const uint8_t*>(p.chol + L.nz);
-  if (I > k && !nz[I * L.T + k]) return;  // L_Ik = 0, b_I unchanged
-  // Vf and Xf2 are one buffer: the blocked factor's M / Xb / Tb live in it until
-  // L_kk^-1 has been read into registers
-  __shared__ double VX[2 * kTB * kTB];
-  double* Vf = VX;                        // L_kk^-1, fragment order
-  double* Xf2 = VX + kTB * kTB;           // terms of y_k = L_kk^-1 b_k
-  __shared__ double Xf[kTB * kTB];        // A_Ik, fragment order; then L_Ik row-major (stride 64)
-  __shared__ double yk[kTB];
-  __shared__ int okf;
-  double* A = p.chol + L.a;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const double* Akk = A + (size_t)k * kTB * L.N + k * kTB;
-#ifdef SLAM_TL_PROFILE
-  const uint64_t pt0 = wall_clock64();
-#endif
-  double* AIk = A + (size_t)I * kTB * L.N + k * kTB;
-  if (I > k && w >= 2) tile_to_frag(AIk, L.N, Xf, w - 2, 2);  // waves 2, 3 (published by the factor's barriers)
-  // wave 1, lane c: column c of L_kk^-1 (x[m] = Linv[m][c]) into registers
-  double x[kTB];
-  double* Mb = VX;
-  double* Xb = VX + kTB * kMS;
-  double* Tb = Xb + 10 * 16 * kBS17;
-#ifdef SLAM_TL_PROFILE
-  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf, k == 0);
-#else
-  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf);
-#endif
-  if (w == 1) {
-    const int cb16 = lane >> 4;
-#pragma unroll
-    for (int m = 0; m < kTB; ++m)
-      x[m] = (m >> 4) >= cb16 ? Xb[blk_id(m >> 4, cb16) * 16 * kBS17 + (m & 15) * kBS17 + (lane & 15)]
-                              : 0.0;
-  }
-  __syncthreads();  // VX is reused below
-  if (w == 1) {
-    const double bc = p.chol[L.b + k * kTB + lane];
-    if (I == k) {
-      double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;
-#pragma unroll
-      for (int m = 0; m < kTB; ++m) Vkk[m * kTB + lane] = x[m];
-      // y_k[m] = sum_c Linv[m][c] b_k[c]: lane c's terms, summed across the wave in LDS
-#pragma unroll
-      for (int m = 0; m < kTB; ++m) Vf[m * kTB + lane] = x[m] * bc;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      double y = 0.0;
-      for (int c = 0; c < kTB; ++c) y += Vf[lane * kTB + ((c + lane) & 63)];
-      p.chol[L.y + k * kTB + lane] = y;
-      if (!ok && lane == 0) *reinterpret_cast<int*>(p.chol + L.fail) = 1;
-    } else {
-#pragma unroll
-      for (int m = 0; m < kTB; ++m) {
-        Vf[frag_idx(m, lane)] = x[m];
-        Xf2[m * kTB + lane] = x[m] * bc;  // y_k terms (Xf2: scratch rows of the yk sum)
-      }
-    }
-  }
-  if (I == k || !ok) return;
-  __syncthreads();
-  if (t < kTB) {
-    double y = 0.0;
-    for (int c = 0; c < kTB; ++c) y += Xf2[t * kTB + ((c + t) & 63)];
-    yk[t] = y;
-  }
-#ifdef SLAM_TL_PROFILE
-  const uint64_t pt1 = wall_clock64();
-#endif
-  d4 acc[4];
-  gemm_xyT(Xf, Vf, acc);  // L_Ik = A_Ik (L_kk^-1)^T
-  __syncthreads();        // Xf free
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = w * 16 + (lane >> 4) + 4 * r, col = s * 16 + (lane & 15);
-      AIk[(size_t)row * L.N + col] = acc[s][r];
-      Xf[row * kTB + col] = acc[s][r];
-    }
-  __syncthreads();
-  if (t < kTB) {
-    double s = 0.0;
-    for (int m = 0; m < kTB; ++m) s = __builtin_fma(Xf[t * kTB + ((m + t) & 63)], yk[(m + t) & 63], s);
-    p.chol[L.b + I * kTB + t] -= s;
-  }
-#ifdef SLAM_TL_PROFILE
-  // WG I = k + 1 of step 0, wall clock (100 MHz) -> ns: start -> factor done, -> end
-  if (k == 0 && I == 1 && t == 0) {
-    const uint64_t pt3 = wall_clock64();
-    p.chol[L.fail + 1] = 10.0 * (double)(pt1 - pt0);
-    p.chol[L.fail + 2] = 10.0 * (double)(pt3 - pt1);
-  }
-#endif
-}
-
-__global__ __launch_bounds__(kTlWG) void k_tl_update(slam_ba_problem p, int k) {
-  lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
-  if (tl_failed(p, L)) return;
-  const int idx = blockIdx.x;
-  int Ii = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
-  while ((Ii + 1) * (Ii + 2) / 2 <= idx) ++Ii;
-  while (Ii * (Ii + 1) / 2 > idx) --Ii;
-  const int I = k + 1 + Ii, J = k + 1 + (idx - Ii * (Ii + 1) / 2);
-  uint8_t* nz = reinterpret_cast<uint8_t*>(p.chol + L.nz);
-  if (!nz[I * L.T + k] || !nz[J * L.T + k]) return;
-  __shared__ double Xf[kTB * kTB], Yf[kTB * kTB];
-  double* A = p.chol + L.a;
-  tile_to_frag(A + (size_t)I * kTB * L.N + k * kTB, L.N, Xf);
-  tile_to_frag(A + (size_t)J * kTB * L.N + k * kTB, L.N, Yf);
-  __syncthreads();
-  d4 acc[4];
-  gemm_xyT(Xf, Yf, acc);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double* AIJ = A + (size_t)I * kTB * L.N + J * kTB;
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = w * 16 + (lane >> 4) + 4 * r, col = s * 16 + (lane & 15);
-      AIJ[(size_t)row * L.N + col] -= acc[s][r];
-    }
-  if (threadIdx.x == 0) nz[I * L.T + J] = 1;
-}
-
-// x_k = L_kk^-T y_k (every WG, from the stored inverse); WG 0 stores it, WG j > 0
-// updates y_J -= L_kJ^T x_k for J = j - 1 < k.
-__global__ __launch_bounds__(kTlWG) void k_tl_back(slam_ba_problem p, int k) {
-  lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
-  if (tl_failed(p, L)) return;
-  const int J = (int)blockIdx.x - 1;
-  const uint8_t* nz = reinterpret_cast<const uint8_t*>(p.chol + L.nz);
-  if (J >= 0 && !nz[k * L.T + J]) return;
-  __shared__ double xk[kTB];
-  __shared__ double part[4][kTB];
-  const double* A = p.chol + L.a;
-  const double* Vkk = p.chol + L.dinv + (size_t)k * kTB * kTB;  // L_kk^-1
-  const int t = threadIdx.x, c = t & 63, q = t >> 6;
-  {
-    // x_k[c] = sum_m Linv[m][c] y_k[m]: thread (q, c) sums m in [16q, 16q + 16)
-    double s = 0.0;
-    for (int m = 16 * q; m < 16 * q + 16; ++m)
-      s = __builtin_fma(Vkk[m * kTB + c], p.chol[L.y + k * kTB + m], s);
-    part[q][c] = s;
-  }
-  __syncthreads();
-  if (t < kTB) xk[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-  __syncthreads();
-  if (J < 0) {
-    if (t < kTB) p.chol[L.x + k * kTB + t] = xk[t];
-    return;
-  }
-  // y_J[c] -= sum_m L_kJ[m][c] x_k[m]
-  const double* LkJ = A + (size_t)k * kTB * L.N + J * kTB;
-  double s = 0.0;
-  for (int m = 16 * q; m < 16 * q + 16; ++m) s = __builtin_fma(LkJ[(size_t)m * L.N + c], xk[m], s);
-  part[q][c] = s;
-  __syncthreads();
-  if (t < kTB) p.chol[L.y + J * kTB + t] -= ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-}
-
-__global__ __launch_bounds__(1024) void k_tl_epilogue(slam_ba_problem p) {
-  lm_wave_priority();
-  __shared__ double red[32];
-  const int n = 9 * p.n_cams;
-  const TlLayout L(n);
-  const bool ok = !tl_failed(p, L);
-  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
-  const double* gvec = bvec + n;
-  solve_epilogue(p, p.chol + L.x, ok, red,
-                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
 }
 
 // ---------------------------------------------------------------- level-scheduled tiled solve
@@ -2577,20 +2339,27 @@ void k_tl3_flow(slam_ba_problem p) {
   if (t == 0) okf = ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1);
   __syncthreads();
   if (!okf) return;
-  const bool good = ld_flag(fail) == 0;
+  const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
+  const bool good = fcode == 0;
   double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
   for (int i = t; i < n; i += kTlWG) xs[i] = good ? ld_sc1(p.chol + L.xo + i) : 0.0;
   __syncthreads();
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
   const double* gvec = bvec + n;
   solve_epilogue(p, xs, good, &part[0][0],
-                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n}, fcode);
   FLOW_T(7);
 }
 
 static int g_cu_count = 0;
 
-static bool tl_flow_ok(const slam_ba_problem& p) {
+// The dataflow solve needs its T workgroups resident together (one per CU):
+// T must not exceed the CUs the stream may use (a CU-masked stream counts only
+// its mask).  Otherwise the level-scheduled launches run instead.  (Kernels of
+// other streams can still hold CUs for a while; a wait that outlasts
+// kFlowSpinMax marks the solve failed with code 2, which the Python layer
+// turns into an error: SLAM_BA_ST_SOLVE_FAULT.)
+static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t s) {
   if (p.tl_mode != 0 || p.tl_sched_host == nullptr || p.tl_sched_host[5] <= 0) return false;
   if (g_cu_count == 0) {
     int dev = 0, cu = 0;
@@ -2600,7 +2369,18 @@ static bool tl_flow_ok(const slam_ba_problem& p) {
     g_cu_count = cu;
   }
   const TlLayout L(9 * p.n_cams);
-  return L.T <= SLAM_TL_FLOW_MAX_T && L.T <= g_cu_count && 9 * p.n_cams <= 2 * kTB * kTB;
+  if (!(L.T <= SLAM_TL_FLOW_MAX_T && L.T <= g_cu_count && 9 * p.n_cams <= 2 * kTB * kTB))
+    return false;
+  if (s != nullptr) {
+    uint32_t mask[16] = {};
+    const int words = min(16, (g_cu_count + 31) / 32);
+    if (hipExtStreamGetCUMask(s, (uint32_t)words, mask) == hipSuccess) {
+      int n = 0;
+      for (int w = 0; w < words; ++w) n += __builtin_popcount(mask[w]);
+      if (n > 0 && L.T > n) return false;
+    }
+  }
+  return true;
 }
 
 static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
@@ -2635,21 +2415,6 @@ static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
   k_tl2_epilogue<<<1, 1024, 0, s>>>(p);
   SLAM_LAUNCHED("k_tl2_*");
   return SLAM_OK;
-}
-
-static void tl_solve(const slam_ba_problem& p, hipStream_t s) {
-  const TlLayout L(9 * p.n_cams);
-  const int T = L.T;
-  k_tl_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p);
-  k_tl_scatter<<<p.n_blocks, 128, 0, s>>>(p);
-  for (int k = 0; k < T; ++k) {
-    k_tl_panel<<<T - k, kTlWG, 0, s>>>(p, k);
-    const int m = T - 1 - k;
-    if (m > 0) k_tl_update<<<m * (m + 1) / 2, kTlWG, 0, s>>>(p, k);
-  }
-  // y of the last tile is final after its panel; the back pass walks up
-  for (int k = T - 1; k >= 0; --k) k_tl_back<<<k + 1, kTlWG, 0, s>>>(p, k);
-  k_tl_epilogue<<<1, 1024, 0, s>>>(p);
 }
 
 __device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
@@ -2845,6 +2610,9 @@ int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(!sys_packed(p->n_cams) || p->chol != nullptr,
                "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
                kLdsMaxN);
+  SLAM_REQUIRE(!sys_packed(p->n_cams) || p->tl_sched != nullptr,
+               "slam_ba: the tile schedule (tl_sched, ba.tl_schedule) is required for 9C > %d",
+               kLdsMaxN);
   return SLAM_OK;
 }
 
@@ -2957,13 +2725,10 @@ static int launch_solve(const Launch& L, bool fuse_decide, hipStream_t s) {
     k_solve_blk<<<dim3(1, L.n), kBlkWG, L.solve_lds, s>>>(L.b);
     SLAM_LAUNCHED("k_solve_blk");
   } else {
-    if (tl_flow_ok(L.b.p[0])) {
+    if (tl_flow_ok(L.b.p[0], s)) {
       if (int rc = tl_solve_flow(L.b.p[0], s)) return rc;
-    } else if (L.b.p[0].tl_sched != nullptr) {
-      if (int rc = tl_solve_levels(L.b.p[0], s)) return rc;
     } else {
-      tl_solve(L.b.p[0], s);
-      SLAM_LAUNCHED("k_tl_*");
+      if (int rc = tl_solve_levels(L.b.p[0], s)) return rc;
     }
   }
   if (fuse_decide)
@@ -2989,6 +2754,7 @@ extern "C" int slam_ba_reset(const slam_ba_problem* prob, double lambda0, void* 
 extern "C" int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0,
                                    void* stream) {
   SLAM_REQUIRE(n_probs >= 0, "slam_ba_reset_batch: n_probs < 0");
+  SLAM_REQUIRE(n_probs == 0 || probs != nullptr, "slam_ba_reset_batch: null problem array");
   for (int i0 = 0; i0 < n_probs; i0 += kBaMaxBatch) {
     Launch L;
     const int n = min(kBaMaxBatch, n_probs - i0);
@@ -3028,6 +2794,7 @@ extern "C" int slam_ba_iterate(const slam_ba_problem* prob, int n_iter, void* st
 extern "C" int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, int n_iter,
                                      void* stream) {
   SLAM_REQUIRE(n_probs >= 0 && n_iter >= 0, "slam_ba_iterate_batch: negative count");
+  SLAM_REQUIRE(n_probs == 0 || probs != nullptr, "slam_ba_iterate_batch: null problem array");
   hipStream_t s = slam::as_stream(stream);
   // dense problems in chunks of kBaMaxBatch share launches; a packed (tiled
   // solver) problem iterates on its own

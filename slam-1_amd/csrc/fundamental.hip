@@ -485,8 +485,9 @@ __global__ __launch_bounds__(kFWG) void k_fm_finish(const double* __restrict__ m
   const double* m1 = m1all + (size_t)b * cap * 2;
   const double* m2 = m2all + (size_t)b * cap * 2;
   uint8_t* mk = mask + (size_t)b * cap;
-  if (M < 8) {
+  if (M < 8) {  // no hypothesis: empty mask, F = 0
     for (int i = t; i < M; i += kFWG) mk[i] = 0;
+    if (t < 9) Fout[9 * b + t] = 0.0;
     if (t == 0) ninl[b] = -1;
     return;
   }
@@ -517,8 +518,9 @@ __global__ __launch_bounds__(kFWG) void k_fm_finish(const double* __restrict__ m
     }
   }
   __syncthreads();
-  if (!found_s) {
+  if (!found_s) {  // F[b] still holds k_fm_hyp's per-split slots: overwrite with 0
     for (int i = t; i < M; i += kFWG) mk[i] = 0;
+    if (t < 9) Fout[9 * b + t] = 0.0;
     if (t == 0) ninl[b] = -1;
     return;
   }

@@ -361,16 +361,36 @@ __device__ unsigned long long g_pnph[8];
 #else
 #define PNPH_T(i) (void)0
 #endif
+// Sample h of pair b (lane 0 of its group): 5 distinct indices from
+// splitmix64(seed, item, h); Q[idx], q[idx] in draw order into pw / uv.
+__device__ void pnp_sample(uint64_t seed, int item, int h, int L, const double* Q, const double* q,
+                           double* pw, double* uv, int* sidx) {
+  uint64_t s = seed ^ ((uint64_t)item * 0xD1B54A32D192ED03ull) ^
+               ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
+  int idx[kMinSample];
+  for (int kk = 0; kk < kMinSample; ++kk) {
+    int v;
+    bool dup;
+    do {
+      v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
+      dup = false;
+      for (int j = 0; j < kk; ++j) dup |= idx[j] == v;
+    } while (dup);
+    idx[kk] = v;
+    sidx[kk] = v;
+    for (int d = 0; d < 3; ++d) pw[3 * kk + d] = Q[3 * v + d];
+    for (int d = 0; d < 2; ++d) uv[2 * kk + d] = q[2 * v + d];
+  }
+}
+
 __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
                                                 const double* __restrict__ qall,
                                                 const int32_t* __restrict__ count, int cap,
                                                 const double* __restrict__ Kp, uint64_t seed,
-                                                int item0, int n_hyp, int hyp_iters,
-                                                double* __restrict__ ws) {
+                                                int item0, int n_hyp, double* __restrict__ ws) {
   __shared__ slam_epnp::EpGroup grp[kHypGroups];
   __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
   __shared__ int sidx[kHypGroups][kMinSample];
-  __shared__ double lmt[kHypGroups][2 * kMinSample][28], lms[kHypGroups][28 + kMinSample];
   const int b = blockIdx.x, t = threadIdx.x;
   const int g = t >> 4, k = t & 15;
   const int h = blockIdx.y * kHypGroups + g;
@@ -382,24 +402,8 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
   const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
   slam_epnp::EpGroup& G = grp[g];
   PNPH_T(0);
-  // sample h: 5 distinct indices from splitmix64(seed, item0 + b, h)
   if (k == 0 && live) {
-    uint64_t s = seed ^ ((uint64_t)(item0 + b) * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)h * 0x8CB92BA72F3D8DD7ull);
-    int idx[kMinSample];
-    for (int kk = 0; kk < kMinSample; ++kk) {
-      int v;
-      bool dup;
-      do {
-        v = (int)((splitmix64(s) >> 32) % (uint64_t)L);
-        dup = false;
-        for (int j = 0; j < kk; ++j) dup |= idx[j] == v;
-      } while (dup);
-      idx[kk] = v;
-      sidx[g][kk] = v;
-      for (int d = 0; d < 3; ++d) spw[g][3 * kk + d] = Q[3 * v + d];
-      for (int d = 0; d < 2; ++d) suv[g][2 * kk + d] = q[2 * v + d];
-    }
+    pnp_sample(seed, item0 + b, h, L, Q, q, spw[g], suv[g], sidx[g]);
     G.flag = slam_epnp::ep_bary<kMinSample>(spw[g], G);
   }
   __syncthreads();
@@ -419,24 +423,53 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
   if (ok && k < 3) slam_epnp::ep_approx<kMinSample>(k, spw[g], suv[g], K.fx, K.fy, K.cx, K.cy, G);
   __syncthreads();
   PNPH_T(5);
-  if (k == 0) {
+  if (k == 0 && live) {  // the EPnP pose (a degenerate sample: r = t = 0) -> ws
     double p[6] = {0, 0, 0, 0, 0, 0};
     if (!(ok && slam_epnp::ep_choose(G, p)))
       for (int i = 0; i < 6; ++i) p[i] = 0.0;
-    for (int i = 0; i < 6; ++i) G.res[0][i] = p[i];  // the EPnP pose to the group
-  }
-  __syncthreads();
-  // LM on the same 5 points from the EPnP pose (a degenerate sample: r = t = 0),
-  // read from the sample's LDS copy (spw / suv hold Q[idx], q[idx] in order);
-  // a dead group (h >= n_hyp) runs along on its zeros and writes nothing
-  double p[6];
-  for (int i = 0; i < 6; ++i) p[i] = G.res[0][i];
-  lm_group(spw[g], suv[g], kMinSample, K, hyp_iters, p, k, lmt[g], lms[g]);
-  if (k == 0 && live) {
     double* o = ws + ((size_t)b * n_hyp + h) * 6;
     for (int i = 0; i < 6; ++i) o[i] = p[i];
   }
   PNPH_T(6);
+}
+
+// Hypothesis LM (the second half of a hypothesis, split from k_pnp_hyp so each
+// kernel fits beside ORB's workgroups): hyp_iters LM steps on the same 5
+// points from the EPnP pose in ws, the result written back in place.  The
+// sample is redrawn (same splitmix64 stream) into LDS.  A dead group
+// (h >= n_hyp) runs along on zeros and writes nothing.
+__global__ __launch_bounds__(64) void k_pnp_hyp_lm(const double* __restrict__ Qall,
+                                                   const double* __restrict__ qall,
+                                                   const int32_t* __restrict__ count, int cap,
+                                                   const double* __restrict__ Kp, uint64_t seed,
+                                                   int item0, int n_hyp, int hyp_iters,
+                                                   double* __restrict__ ws) {
+  __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
+  __shared__ int sidx[kHypGroups][kMinSample];
+  __shared__ double lmt[kHypGroups][2 * kMinSample][28], lms[kHypGroups][28 + kMinSample];
+  __shared__ double p0[kHypGroups][6];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int g = t >> 4, k = t & 15;
+  const int h = blockIdx.y * kHypGroups + g;
+  const int L = min(max(count[b], 0), cap);
+  if (L < kMinSample) return;  // uniform over the workgroup
+  const bool live = h < n_hyp;
+  const double* Q = Qall + (size_t)b * cap * 3;
+  const double* q = qall + (size_t)b * cap * 2;
+  const Cam K{Kp[0], Kp[4], Kp[2], Kp[5]};
+  double* o = ws + ((size_t)b * n_hyp + (live ? h : 0)) * 6;
+  if (k == 0) {
+    if (live) pnp_sample(seed, item0 + b, h, L, Q, q, spw[g], suv[g], sidx[g]);
+    else
+      for (int i = 0; i < 3 * kMinSample; ++i) spw[g][i] = suv[g][i % (2 * kMinSample)] = 0.0;
+  }
+  if (k < 6) p0[g][k] = live ? o[k] : 0.0;
+  __syncthreads();
+  double p[6];
+  for (int i = 0; i < 6; ++i) p[i] = p0[g][i];
+  lm_group(spw[g], suv[g], kMinSample, K, hyp_iters, p, k, lmt[g], lms[g]);
+  if (k == 0 && live)
+    for (int i = 0; i < 6; ++i) o[i] = p[i];
 }
 
 // One workgroup per frame pair:
@@ -1121,7 +1154,7 @@ extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32
                                int cap, int batch, const double* d_K, uint64_t seed, int item0,
                                int n_hyp, double reproj_thresh, int hyp_iters, int refine_iters,
                                double* d_rvec, double* d_tvec, int32_t* d_ninliers,
-                               uint8_t* d_mask, double* d_ws, void* stream) {
+                               uint8_t* d_mask, double* d_ws, long long ws_len, void* stream) {
   SLAM_REQUIRE(batch >= 0 && cap >= 0, "slam_pnp_ransac: bad shape");
   SLAM_REQUIRE(n_hyp >= 1 && n_hyp <= kMaxHyp, "slam_pnp_ransac: n_hyp in [1, %d]", kMaxHyp);
   SLAM_REQUIRE(hyp_iters >= 0 && refine_iters >= 0 && reproj_thresh > 0,
@@ -1129,10 +1162,18 @@ extern "C" int slam_pnp_ransac(const double* d_Q, const double* d_q, const int32
   if (batch == 0) return SLAM_OK;
   SLAM_REQUIRE(d_Q && d_q && d_count && d_K && d_rvec && d_tvec && d_ninliers && d_mask && d_ws,
                "slam_pnp_ransac: null pointer");
+  if (ws_len < slam_pnp_workspace_len(batch, n_hyp)) {
+    slam::set_error("slam_pnp_ransac: workspace %lld < %lld doubles", ws_len,
+                    slam_pnp_workspace_len(batch, n_hyp));
+    return SLAM_ERR_WORKSPACE;
+  }
   hipStream_t s = slam::as_stream(stream);
-  k_pnp_hyp<<<dim3(batch, (n_hyp + kHypGroups - 1) / kHypGroups), 64, 0, s>>>(
-      d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, hyp_iters, d_ws);
+  const dim3 hgrid(batch, (n_hyp + kHypGroups - 1) / kHypGroups);
+  k_pnp_hyp<<<hgrid, 64, 0, s>>>(d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, d_ws);
   SLAM_LAUNCHED("k_pnp_hyp");
+  k_pnp_hyp_lm<<<hgrid, 64, 0, s>>>(d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, hyp_iters,
+                                    d_ws);
+  SLAM_LAUNCHED("k_pnp_hyp_lm");
   k_pnp<<<batch, kPnPWG, 0, s>>>(d_Q, d_q, d_count, cap, d_K, seed, item0, n_hyp, reproj_thresh,
                                  hyp_iters, refine_iters, d_rvec, d_tvec, d_ninliers, d_mask,
                                  d_ws);

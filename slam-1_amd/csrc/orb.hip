@@ -61,6 +61,7 @@ struct OrbGeom {
 };
 
 __device__ __forceinline__ int rne_f(float v) { return (int)rintf(v); }
+__host__ __device__ __forceinline__ int lpitch(int w) { return (w + 3) & ~3; }
 
 // Exact n / d for n >= 0, d >= 1 with n * d < 2^32, by a multiply-high with
 // m = ceil(2^32 / d): the error n (m - 2^32/d) / 2^32 < n / 2^32 < 1/d never
@@ -251,21 +252,25 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
   float* gsvr = reinterpret_cast<float*>(gsvc + g.cand_cap);
 
   ORB_T0();
+  // Level images are stored with a row pitch of the width rounded up to 4 bytes
+  // (lpitch), so 4 adjacent pixels of a row are one aligned dword for the
+  // resize stores and the blur's row windows.
   // ---- stage the patch (level 0) into LDS, 16 B per lane where aligned
   {
     const uint8_t* src = img + (size_t)b * g.H * g.stride + (size_t)y0 * g.stride + x0;
     uint8_t* dst = A;
+    const int P0 = lpitch(pw);
     if ((pw & 15) == 0 && (((uintptr_t)src) & 15) == 0 && (g.stride & 15) == 0) {
       const int vpr = pw >> 4;
       for (int i = t; i < vpr * ph; i += kOrbWG) {
         const int r = i / vpr, c = i - r * vpr;
-        *reinterpret_cast<uint4*>(dst + r * pw + 16 * c) =
+        *reinterpret_cast<uint4*>(dst + r * P0 + 16 * c) =
             *reinterpret_cast<const uint4*>(src + (size_t)r * g.stride + 16 * c);
       }
     } else {
       for (int i = t; i < pw * ph; i += kOrbWG) {
         const int r = i / pw, c = i - r * pw;
-        dst[i] = src[(size_t)r * g.stride + c];
+        dst[r * P0 + c] = src[(size_t)r * g.stride + c];
       }
     }
   }
@@ -277,44 +282,48 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
   const int nlev = g.nlev[shp];
   for (int l = 0; l < nlev; ++l) {
     const int W = g.lw[shp][l], H = g.lh[shp][l];
+    const int P = lpitch(W);  // row pitch of the level image
     if (l > 0) {
       // ---- resize level l-1 (A) -> l (U, INTER_LINEAR_EXACT), then U -> A
       const int SW = g.lw[shp][l - 1], SH = g.lh[shp][l - 1];
+      const int SP = lpitch(SW);
       const uint8_t* S = A;
-      for (int i = t; i < W; i += kOrbWG) tabx[i] = lin_coeff(i, W, SW);
+      // x coefficients for the padded row (columns past W: any in-bounds source)
+      for (int i = t; i < P; i += kOrbWG) tabx[i] = i < W ? lin_coeff(i, W, SW) : 0;
       for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
       __syncthreads();
-      const uint32_t mW = div_magic(W);
-      // Four pixels per pass with all LDS reads of the group issued before
-      // any store (the compiler cannot reorder loads over U stores itself).
-      const int WH = W * H;
-      for (int i0 = t; i0 < WH; i0 += 4 * kOrbWG) {
-        int ii[4], cx[4], cy[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          ii[q] = min(i0 + q * kOrbWG, WH - 1);
-          const int y = fdiv(ii[q], mW), x = ii[q] - y * W;
-          cx[q] = tabx[x];
-          cy[q] = taby[y];
-        }
+      // Four adjacent destination pixels per lane: their x coefficients are one
+      // 16-byte LDS read, the row coefficient one, the 16 source bytes are read
+      // before the four results leave as one dword (consecutive lanes write
+      // consecutive dwords).  The padding bytes of a row get junk, never read.
+      const int NG = P >> 2, NT = NG * H;
+      const uint32_t mNG = div_magic(NG);
+      for (int i = t; i < NT; i += kOrbWG) {
+        const int y = fdiv(i, mNG), x = 4 * (i - y * NG);
+        const int cy = taby[y];
+        const int4 c4 = *reinterpret_cast<const int4*>(tabx + x);
+        const int cx[4] = {c4.x, c4.y, c4.z, c4.w};
+        const uint8_t* r0 = S + (cy >> 9) * SP;
+        const int d1 = cy & 511, d0 = 256 - d1;
         int p00[4], p01[4], p10[4], p11[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint8_t* r0 = S + (cy[q] >> 9) * SW + (cx[q] >> 9);
+          const uint8_t* rp = r0 + (cx[q] >> 9);
           // the +1 neighbours are only read with a non-zero weight (the
           // last column / row may sit on the source edge)
-          p00[q] = r0[0];
-          p01[q] = (cx[q] & 511) ? r0[1] : 0;
-          p10[q] = (cy[q] & 511) ? r0[SW] : 0;
-          p11[q] = ((cx[q] & 511) && (cy[q] & 511)) ? r0[SW + 1] : 0;
+          p00[q] = rp[0];
+          p01[q] = (cx[q] & 511) ? rp[1] : 0;
+          p10[q] = d1 ? rp[SP] : 0;
+          p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
         }
+        uint32_t w = 0u;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c1 = cx[q] & 511, c0 = 256 - c1;
-          const int d1 = cy[q] & 511, d0 = 256 - d1;
           const int v = d0 * (c0 * p00[q] + c1 * p01[q]) + d1 * (c0 * p10[q] + c1 * p11[q]);
-          if (i0 + q * kOrbWG < WH) U[ii[q]] = (uint8_t)min((v + 32768) >> 16, 255);
+          w |= (uint32_t)min((v + 32768) >> 16, 255) << (8 * q);
         }
+        *reinterpret_cast<uint32_t*>(U + y * P + x) = w;
       }
       __syncthreads();
       if (kGlob) {  // global level buffers: swap roles instead of copying
@@ -322,7 +331,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
         A = U;
         U = tmp;
       } else {
-        for (int i = t; i < (W * H + 15) >> 4; i += kOrbWG)
+        for (int i = t; i < (P * H + 15) >> 4; i += kOrbWG)
           reinterpret_cast<uint4*>(A)[i] = reinterpret_cast<const uint4*>(U)[i];
         __syncthreads();
       }
@@ -359,11 +368,11 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       const bool gv = gb + lane < SN4;
       const int gi = min(gb + lane, SN4 - 1);
       const int y = fdiv(gi, mG4), x = 4 * (gi - y * NG4);  // map coords of the first pixel
-      const int a = (y + kNMS0) * W + x + kNMS0;
+      const int a = (y + kNMS0) * P + x + kNMS0;
       const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + ((a - 3) & ~3));
       const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3];
       const int sh = (a - 3) & 3;
-      const uint32_t up = win4(a - 3 * W), dn = win4(a + 3 * W);
+      const uint32_t up = win4(a - 3 * P), dn = win4(a + 3 * P);
       const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);  // bytes a-3 .. a
       const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);  // a+1 .. a+4
       const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);  // a+5 .. a+8
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       for (int j = lane; j < nq; j += 64) {
         const int i = (int)fq[j];  // padded-map index: y * SW4 + x
         const int y = fdiv(i, mS4), x = i - y * SW4;
-        Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * W + x + kNMS0, W);
+        Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * P + x + kNMS0, P);
       }
     }
     for (int i = t; i < 256; i += kOrbWG) hist[i] = 0;
@@ -518,9 +527,9 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       int a = 0, bq = 0, cq = 0;
       if (lane < 49) {
         const int i = lane / 7, j = lane - 7 * (lane / 7);
-        const uint8_t* pp = I + (hy - 3 + i) * W + (hx - 3 + j);
-        const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-W + 1] - pp[-W - 1]) + (pp[W + 1] - pp[W - 1]);
-        const int Iy = (pp[W] - pp[-W]) * 2 + (pp[W - 1] - pp[-W - 1]) + (pp[W + 1] - pp[-W + 1]);
+        const uint8_t* pp = I + (hy - 3 + i) * P + (hx - 3 + j);
+        const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-P + 1] - pp[-P - 1]) + (pp[P + 1] - pp[P - 1]);
+        const int Iy = (pp[P] - pp[-P]) * 2 + (pp[P - 1] - pp[-P - 1]) + (pp[P + 1] - pp[-P + 1]);
         a = Ix * Ix;
         bq = Iy * Iy;
         cq = Ix * Iy;
@@ -607,7 +616,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int s = 0; s < 16; ++s) {
           const int v = lane < 32 ? -(s + 1) : s;
           const bool in = (lane < 32 ? s + 1 : s) <= ic_vlim;
-          const int val = I[(cy + (in ? v : 0)) * W + cx + (in ? u : 0)];
+          const int val = I[(cy + (in ? v : 0)) * P + cx + (in ? u : 0)];
           m10 += in ? u * val : 0;
           m01 += in ? v * val : 0;
         }
@@ -620,18 +629,23 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
     // ---- 7x7 Gaussian (float path) over [9, W-10] x [9, H-10] into U
     const int BW = W - 2 * kBl0, BH = H - 2 * kBl0;
+    const int BP = lpitch(BW);  // row pitch of the blurred level
     uint8_t* Bl = U;
     __syncthreads();  // Smap and the survivor lists are dead from here (L holds the level)
     ORB_T(7);
     {
-      // 4 adjacent output columns per lane: one aligned 16-byte LDS window per
-      // source row (v_alignbyte to the 10 needed bytes, v_cvt_f32_ubyteN), four
-      // independent FMA chains; rows slide down a per-lane segment.  Every
-      // output keeps the exact operation order of the scalar form (row: fmaf
-      // k0..k6 from 0; column: w3*k3 then fmaf(w[+d]+w[-d], k[3+d])).
+      // 4 adjacent output columns per lane (x = kBl0 + 4 cg: a dword boundary of
+      // the pitched level): the 10 source bytes x-3 .. x+6 of a row are the
+      // three aligned dwords at x-4, x, x+4 (consecutive lanes read consecutive
+      // dwords: no bank conflicts) shifted by v_alignbyte; four independent FMA
+      // chains; rows slide down a per-lane segment; the four results leave as
+      // one dword of the pitched blurred level.  Every output keeps the exact
+      // operation order of the scalar form (row: fmaf k0..k6 from 0; column:
+      // w3*k3 then fmaf(w[+d]+w[-d], k[3+d])).
+      static_assert((kBl0 & 3) == 0, "blur origin must be dword aligned");
       const float k0 = g.gk[0], k1 = g.gk[1], k2 = g.gk[2], k3 = g.gk[3];
       const float k4 = g.gk[4], k5 = g.gk[5], k6 = g.gk[6];
-      const int ncg = (BW + 3) >> 2;
+      const int ncg = BP >> 2;
       const int nseg = max(1, kOrbWG / ncg);
       const int seg = (BH + nseg - 1) / nseg;
       for (int item = t; item < ncg * nseg; item += kOrbWG) {
@@ -640,13 +654,11 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (r0 >= r1) continue;
         const int c4 = 4 * cg, x = c4 + kBl0;
         auto rowf4 = [&](int y, float4& o) {
-          const int addr = y * W + x - 3;
-          const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (addr & ~3));
-          const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3];
-          const int sh = addr & 3;
-          const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-          const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-          const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + y * P + x - 4);
+          const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2];
+          const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, 1);  // bytes x-3 .. x
+          const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, 1);  // x+1 .. x+4
+          const uint32_t q2 = d2 >> 8;                                // x+5 .. x+7
           float p[10];
           p[0] = (float)((q0 >> 0) & 0xFFu);
           p[1] = (float)((q0 >> 8) & 0xFFu);
@@ -682,7 +694,6 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
         rowf4(yb + 1, w4);
         rowf4(yb + 2, w5);
         rowf4(yb + 3, w6);
-        const int nc = min(4, BW - c4);
         for (int r = r0; r < r1; ++r) {
           float v4[4];
           const float a0[4] = {w0.x, w0.y, w0.z, w0.w}, a1[4] = {w1.x, w1.y, w1.z, w1.w};
@@ -697,12 +708,13 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
             s0 = fmaf(a6[j] + a0[j], k6, s0);
             v4[j] = s0;
           }
-          uint8_t* out = Bl + r * BW + c4;
+          uint32_t packed = 0u;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int v = (int)rintf(v4[j]);
-            if (j < nc) out[j] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+            packed |= (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v) << (8 * j);
           }
+          *reinterpret_cast<uint32_t*>(Bl + r * BP + c4) = packed;
           if (r + 1 < r1) {
             w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
             rowf4(r + 1 + kBl0 + 3, w6);
@@ -732,8 +744,8 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
           const float px2 = (float)pp[2], py2 = (float)pp[3];
           const int ix1 = rne_f(px1 * a - py1 * bb), iy1 = rne_f(px1 * bb + py1 * a);
           const int ix2 = rne_f(px2 * a - py2 * bb), iy2 = rne_f(px2 * bb + py2 * a);
-          const int t0 = Bl[(cy + iy1) * BW + cx + ix1];
-          const int t1 = Bl[(cy + iy2) * BW + cx + ix2];
+          const int t0 = Bl[(cy + iy1) * BP + cx + ix1];
+          const int t1 = Bl[(cy + iy2) * BP + cx + ix2];
           val |= (t0 < t1 ? 1 : 0) << bit;
         }
         const int o = nout + k;
@@ -878,13 +890,13 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
           if (g->lw[s][l] > 2 * kEdge && g->lh[s][l] > 2 * kEdge && g->nl[l] > 0) last = l;
         }
         g->nlev[s] = last + 1;
-        max_a = max(max_a, w * h);
-        if (last >= 1) max_b = max(max_b, g->lw[s][1] * g->lh[s][1]);
+        max_a = max(max_a, lpitch(w) * h);
+        if (last >= 1) max_b = max(max_b, lpitch(g->lw[s][1]) * g->lh[s][1]);
         const int W0 = w, H0 = h;
         if (W0 > 2 * kEdge && H0 > 2 * kEdge) {
           const int cand = ((W0 - 2 * kEdge + 1) / 2) * ((H0 - 2 * kEdge + 1) / 2);
           const int smap = (((((W0 - 2 * kNMS0) + 3) & ~3) * (H0 - 2 * kNMS0)) + 15) & ~15;
-          const int bl = (W0 - 2 * kBl0) * (H0 - 2 * kBl0);
+          const int bl = lpitch(W0 - 2 * kBl0) * (H0 - 2 * kBl0);
           max_cand = max(max_cand, cand);
           max_smap = max(max_smap, smap);
           max_bl = max(max_bl, bl);

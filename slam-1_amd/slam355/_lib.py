@@ -19,6 +19,7 @@ c_double = ctypes.c_double
 c_size_t = ctypes.c_size_t
 c_p = ctypes.c_void_p
 c_uint64 = ctypes.c_uint64
+c_longlong = ctypes.c_longlong
 
 c_i32 = ctypes.c_int32
 
@@ -61,7 +62,7 @@ SIGNATURES = {
                              c_p],
     "slam_triangulate": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_int, c_p, c_p],
     "slam_pnp_ransac": [c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int, c_double, c_int,
-                        c_int, c_p, c_p, c_p, c_p, c_p, c_p],
+                        c_int, c_p, c_p, c_p, c_p, c_p, c_longlong, c_p],
     "slam_pnp_workspace_len": [c_int, c_int],
     "slam_pose_chain": [c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_vo_estimate_pose": [c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_uint64, c_int, c_int,

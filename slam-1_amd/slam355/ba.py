@@ -22,8 +22,8 @@ from .device import ptr, require_gpu, stream_ptr
 from ._lib import BAProblemStruct as _Prob
 
 ST = dict(LAMBDA=0, NU=1, COST=2, COST_NEW=3, PRED=4, RHO=5, ACCEPTED=6, CUR=7, ITERS=8,
-          NACCEPT=9, PRED_CAM=10, CHOL_FAIL=11)
-N_STATE = 16
+          NACCEPT=9, PRED_CAM=10, CHOL_FAIL=11, SOLVE_FAULT=16)
+N_STATE = 20  # SLAM_BA_ST_SLOTS
 LDS_MAX_N = 120  # k_solve_blk keeps S in LDS up to 9C <= 120 (dense sys); tiled solver above
 
 
@@ -635,17 +635,15 @@ class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
-                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_levels=True,
-                 tl_mode="flow"):
+                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow"):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
-        every point is seen by <= MF_CAMS cameras).  tl_levels: the tiled
-        camera solve (9C > 120) runs the nested-dissection level schedule
-        (tl_schedule); False keeps one panel step per tile column.  tl_mode
-        (with the schedule): "flow" runs it as one dataflow launch (k_tl3_flow;
-        the library falls back to levels when the tile count exceeds the CU
-        count), "levels" one launch pair per elimination-tree level."""
+        every point is seen by <= MF_CAMS cameras).  The tiled camera solve
+        (9C > 120) follows the nested-dissection schedule of tl_schedule;
+        tl_mode "flow" runs it as one dataflow launch (k_tl3_flow; the library
+        falls back to levels when the tile count exceeds the CUs the stream
+        may use), "levels" one launch pair per elimination-tree level."""
         if tl_mode not in ("flow", "levels"):
             raise ValueError(f"tl_mode must be 'flow' or 'levels', not {tl_mode!r}")
         dev = require_gpu()
@@ -689,7 +687,7 @@ class BAProblem:
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
         t["sys"] = z(self.sys_len)
         t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
-        self.tl_levels = tl_levels and C9 > LDS_MAX_N
+        self.tl_levels = C9 > LDS_MAX_N
         if self.tl_levels:  # level schedule of the tiled solve (host + device copies)
             self._sched_host = tl_schedule(C, pl["blocks"])
             t["tl_sched"] = T(self._sched_host)
@@ -813,8 +811,15 @@ class BAProblem:
 
     # -- host views ---------------------------------------------------------------
     def state(self) -> dict:
+        """The LM state; raises SlamError when a camera solve ever timed out
+        waiting for a co-resident workgroup (SOLVE_FAULT: the dataflow solve was
+        launched where its columns could not all be resident)."""
         s = self.t["state"].cpu().numpy()
-        return {k: float(s[v]) for k, v in ST.items()}
+        st = {k: float(s[v]) for k, v in ST.items()}
+        if st["SOLVE_FAULT"] != 0.0:
+            raise _lib.SlamError(f"BA camera solve timed out {int(st['SOLVE_FAULT'])} time(s): its "
+                                 "workgroups were not co-resident (the LM steps were rejected)")
+        return st
 
     def params(self):
         """(cams [C,9], pts [P,3]) at the live parameters, points in the caller's order."""

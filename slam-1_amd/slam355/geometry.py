@@ -90,8 +90,12 @@ def triangulate(ptl, ptr_, count, P_l, P_r, out=None, stream=None):
     return X
 
 
-def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, **kw):
-    """Q [B,cap,3], q [B,cap,2] f64 -> (rvec [B,3], tvec [B,3], ninliers [B], mask [B,cap])."""
+def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, ws=None, **kw):
+    """Q [B,cap,3], q [B,cap,2] f64 -> (rvec [B,3], tvec [B,3], ninliers [B], mask [B,cap]).
+
+    ws: the hypothesis-pose workspace (pnp_workspace(B, n_hyp)); calls that may
+    run concurrently (other streams) must each pass their own.  Without one, a
+    fresh buffer is allocated for this call (and kept alive for `stream`)."""
     prm = dict(PNP_DEFAULTS, **kw)
     B, cap, _ = Q.shape
     dev = Q.device
@@ -103,24 +107,21 @@ def pnp_ransac(Q, q, count, K, seed=0, item0=0, out=None, stream=None, **kw):
         mask = torch.zeros((B, max(cap, 1)), dtype=torch.uint8, device=dev)
     else:
         rvec, tvec, ninl, mask = out
-    ws = _pnp_ws(B, prm["n_hyp"], dev)
+    if ws is None:
+        ws = pnp_workspace(B, prm["n_hyp"], dev)
+        if stream is not None and stream != torch.cuda.current_stream(dev):
+            ws.record_stream(stream)  # freed by the caching allocator only after `stream`
     _lib.call("slam_pnp_ransac", ptr(Q), ptr(q), ptr(count), cap, B, ptr(Kt.contiguous()),
               int(seed) & ((1 << 64) - 1), int(item0), prm["n_hyp"], float(prm["reproj_thresh"]),
               prm["hyp_iters"], prm["refine_iters"], ptr(rvec), ptr(tvec), ptr(ninl), ptr(mask),
-              ptr(ws), stream_ptr(stream))
+              ptr(ws), ws.numel(), stream_ptr(stream))
     return rvec, tvec, ninl, mask
 
 
-_PNP_WS: dict = {}
-
-
-def _pnp_ws(B, n_hyp, dev):
-    """Hypothesis-pose workspace of slam_pnp_ransac (cached per device, grown)."""
+def pnp_workspace(B, n_hyp=PNP_DEFAULTS["n_hyp"], dev="cuda"):
+    """Hypothesis-pose workspace of slam_pnp_ransac for B items (f64)."""
     n = int(_lib.lib.slam_pnp_workspace_len(B, n_hyp))
-    ws = _PNP_WS.get(dev)
-    if ws is None or ws.numel() < n:
-        ws = _PNP_WS[dev] = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
-    return ws
+    return torch.empty(max(n, 1), dtype=torch.float64, device=dev)
 
 
 VO_DEFAULTS = dict(max_iter=100, lm_iters=20, early_stop=5)

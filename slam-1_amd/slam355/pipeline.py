@@ -83,6 +83,7 @@ class Tracker:
         self.tvec = torch.zeros((B, 3), **f64)
         self.p_ninl = torch.zeros((B,), **i32)
         self.p_mask = torch.zeros((B, cap), **u8)
+        self.p_ws = geometry.pnp_workspace(B, dev=d)  # this Tracker's PnP hypotheses
         self.imgs = torch.zeros((2 * B + 1, H, W), **u8)
         # device pose chain (main.py:120-124): (pose, T) carried across batches
         self.chain_state = torch.zeros((32,), **f64)
@@ -179,7 +180,8 @@ class Tracker:
         mark("triangulate_temporal")
         # PnP-RANSAC (transformation.py:11-13)
         geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,
-                            out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st)
+                            out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st,
+                            ws=self.p_ws)
         mark("pnp")
         if chain:
             _lib.call("slam_pose_chain", ptr(self.rvec), ptr(self.tvec), ptr(self.p_ninl), B,
@@ -198,15 +200,21 @@ class Tracker:
         """Synchronises: raise if any ORB count since the last check was negative
         (keypoint workspace overflow: too many tied responses in a tile, or more
         keypoints than kp_cap), then reset the flag."""
+        cur = torch.cuda.current_stream()
+        streams = [x for x in (self.stream, self.orb_stream) if x is not None]
+        for x in streams:  # the host read below follows every queued ORB count update
+            cur.wait_stream(x)
         m = int(self.orb_min.item())
         self.orb_min.fill_(1 << 30)
+        for x in streams:  # and the next batch's updates follow the reset
+            x.wait_stream(cur)
         if m < 0:
             raise _lib.SlamError("Tracker: ORB keypoint workspace overflow (a tile kept more tied "
                                  "responses than the workspace holds, or kp_cap was exceeded); "
                                  "the frame would have been tracked with no matches")
 
     def counters(self):
-        self.check()
+        self.check()  # also orders the current stream after the tracking / ORB streams
         return dict(orb=self.ows.count.cpu().numpy(), stereo=self.s_cnt.cpu().numpy(),
                     f_inliers=self.f_cnt.cpu().numpy(), temporal=self.t_cnt.cpu().numpy(),
                     pnp_inliers=self.p_ninl.cpu().numpy())
@@ -267,6 +275,8 @@ class LocalMap:
         for b in range(t.B):
             self.store.append(self.abs[b], t.Q1[b], t.q1[b], frame0 + b, self.threshold,
                               count=t.t_cnt[b:b + 1], rows=self.rows[b], stream=st)
+        if st is not None:  # the host reads below follow the launches queued on `st`
+            torch.cuda.current_stream().wait_stream(st)
         cnt = t.t_cnt.cpu().numpy()
         rows = self.rows.cpu().numpy()
         self._rows_host += [rows[b, :cnt[b]] for b in range(t.B)]

@@ -172,23 +172,28 @@ def test_gpu_jacobian_matches_oracle(g):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dup", [0, 5])
-def test_gpu_lm_iterates_match_oracle(dup):
+@pytest.mark.parametrize("dup,C,k,lin_mode", [(0, 6, 4, "auto"), (5, 6, 4, "auto"),
+                                              (0, 6, 4, "slot"), (5, 6, 4, "slot"),
+                                              (0, 12, 9, "auto")])
+def test_gpu_lm_iterates_match_oracle(dup, C, k, lin_mode):
     """dup > 0: some points are observed twice by the same camera (a (c, c)
-    pair inside the point's Schur block)."""
+    pair inside the point's Schur block).  lin_mode "slot" runs the general
+    linearisation (k_linearize) that points seen by more than MF_CAMS cameras
+    need; the 9-camera tracks of the last case take it under "auto"."""
     from slam355 import ba
 
-    cams, pts, ci, pi, qs = make_problem(3, 6, 150, 4)
+    cams, pts, ci, pi, qs = make_problem(3, C, 150, k)
     rng = np.random.default_rng(4)
     if dup:
-        k = rng.choice(len(ci), dup, replace=False)
-        ci, pi = np.append(ci, ci[k]), np.append(pi, pi[k])
-        qs = np.vstack([qs, qs[k] + rng.normal(0, 0.5, (dup, 2))])
+        kk = rng.choice(len(ci), dup, replace=False)
+        ci, pi = np.append(ci, ci[kk]), np.append(pi, pi[kk])
+        qs = np.vstack([qs, qs[kk] + rng.normal(0, 0.5, (dup, 2))])
     cams0 = cams.copy()
-    cams0[:, :3] += rng.normal(0, 1e-3, (6, 3))
-    cams0[:, 3:6] += rng.normal(0, 1e-2, (6, 3))
+    cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
     pts0 = pts + rng.normal(0, 0.05, pts.shape)
-    prob = ba.BAProblem(cams0, pts0, ci, pi, qs)
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs, lin_mode=lin_mode)
+    assert prob.lin_mode == ("slot" if lin_mode == "slot" or k > ba.MF_CAMS else "mfma")
     st = oba.LMState(1e-4)
     oc, op = cams0.copy(), pts0.copy()
     for it in range(8):
@@ -281,7 +286,7 @@ def test_gpu_local_ba_config3_converges(C, P, k):
 @pytest.mark.parametrize("C,P,k", [(14, 400, 4), (40, 1500, 5), (130, 3000, 6)])
 def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
     """9C > 120: the reduced camera system goes through the tiled Cholesky
-    (k_tl_*; 2, 6 and 19 tiles of 64).  The 130-camera trajectory window is
+    (k_tl3_flow or k_tl2_*; 2, 6 and 19 tiles of 64).  The 130-camera trajectory window is
     block-banded (points seen by 6 consecutive keyframes), so most tiles stay
     structurally zero and are skipped.  LM iterates equal the oracle's Schur LM."""
     from slam355 import ba
@@ -419,6 +424,44 @@ def test_gpu_c4_window_iterates_match_oracle():
         gc, gp = prob.params()
         assert np.allclose(gc, oc, rtol=1e-6, atol=1e-9), it
         assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), it
+
+
+@pytest.mark.gpu
+def test_gpu_flow_solve_under_concurrent_orb():
+    """k_tl3_flow needs its T column workgroups resident together.  C4 LM
+    iterations (9 tile columns) on one stream while ORB batches (79 KB of LDS
+    per workgroup, thousands of workgroups) hold the CUs from another stream:
+    the iterates equal those of the same solve alone, bit for bit -- or the
+    state raises SlamError (a timed-out wait); never a silent difference."""
+    import torch
+    from slam355 import _lib, ba, orb
+    from slam355.synthetic import ba_problem, perturb
+
+    rng = np.random.default_rng(7)
+    cams, pts, ci, pi, qs = ba_problem(rng, 64, 50000, 6)
+    c0, p0 = perturb(rng, cams, pts)
+    solo = ba.BAProblem(c0, p0, ci, pi, qs)
+    solo.iterate(3)
+    torch.cuda.synchronize()
+    imgs = torch.randint(0, 256, (65, 720, 1280), dtype=torch.uint8, device="cuda")
+    ows = orb.OrbWorkspace(65, 720, 1280, 64)
+    s_orb, s_ba = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s_ba):
+        prob = ba.BAProblem(c0, p0, ci, pi, qs, stream=s_ba)
+    torch.cuda.synchronize()
+    ows.run(imgs, s_orb)  # the first ORB batch is queued ahead of the solve
+    with torch.cuda.stream(s_ba):
+        prob.iterate(3)
+    for _ in range(3):
+        ows.run(imgs, s_orb)
+    torch.cuda.synchronize()
+    try:
+        st = prob.state()
+    except _lib.SlamError:
+        return  # loud: acceptable
+    assert st == solo.state()
+    for x, y in zip(prob.params(), solo.params()):
+        assert np.array_equal(x, y)
 
 
 @pytest.mark.gpu

@@ -21,11 +21,11 @@ def _free_port():
     return p
 
 
-def _problem(C=8, P=600, k=4):
-    from slam355.synthetic import ba_problem, perturb
+def _problem(C=8, P=600, k=4, loop=False):
+    from slam355.synthetic import ba_problem, ba_problem_loop, perturb
 
     rng = np.random.default_rng(21)
-    cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+    cams, pts, ci, pi, qs = (ba_problem_loop if loop else ba_problem)(rng, C, P, k)
     c0, p0 = perturb(rng, cams, pts)
     return c0, p0, ci, pi, qs
 
@@ -98,7 +98,7 @@ def test_shards_partition_points_and_observations():
     assert (sum(m[1].astype(int) for m in masks) == 1).all()
 
 
-def _gpu_worker(rank, world, port, out, C=8, P=600, k=4, iters=6):
+def _gpu_worker(rank, world, port, out, C=8, P=600, k=4, iters=6, loop=False):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -111,7 +111,7 @@ def _gpu_worker(rank, world, port, out, C=8, P=600, k=4, iters=6):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    c0, p0, ci, pi, qs = _problem(C, P, k)
+    c0, p0, ci, pi, qs = _problem(C, P, k, loop)
     mine, keep, lpi = shard_by_anchor(len(c0), len(p0), ci, pi, rank, world)
     # packed layout (9C > 120): every rank lists the blocks of the GLOBAL problem
     prob = BAProblem(c0, p0[mine], ci[keep], lpi, qs[keep], block_list=upper_blocks(C, ci, pi))
@@ -126,15 +126,19 @@ def _gpu_worker(rank, world, port, out, C=8, P=600, k=4, iters=6):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,P,k,iters", [(8, 600, 4, 6), (30, 1500, 4, 6), (64, 50000, 6, 2)])
-def test_gpu_step_distributed_matches_single_rank(tmp_path, C, P, k, iters):
+@pytest.mark.parametrize("C,P,k,iters,loop", [(8, 600, 4, 6, False), (30, 1500, 4, 6, False),
+                                              (64, 50000, 6, 2, False),
+                                              (500, 200000, 6, 1, True)])
+def test_gpu_step_distributed_matches_single_rank(tmp_path, C, P, k, iters, loop):
     """C = 8: dense system, one-workgroup solver; C = 30: packed block layout
     (only camera pairs with common points are all-reduced) and tiled solver;
     C = 64, 50k points, 300k observations: the C4 window split
-    over two ranks, two LM iterations."""
+    over two ranks, two LM iterations; C = 500, 200k points, 1.2M observations
+    on a closed loop: the C5 global BA (BASELINE config 5) split over two
+    ranks, the first LM iteration."""
     from slam355.ba import BAProblem
 
-    c0, p0, ci, pi, qs = _problem(C, P, k)
+    c0, p0, ci, pi, qs = _problem(C, P, k, loop)
     prob = BAProblem(c0, p0, ci, pi, qs)
     costs = []
     for _ in range(iters):
@@ -142,7 +146,8 @@ def test_gpu_step_distributed_matches_single_rank(tmp_path, C, P, k, iters):
         costs.append(prob.state()["COST_NEW"])
     cams, _ = prob.params()
     out = str(tmp_path / "d.npz")
-    mp.spawn(_gpu_worker, args=(2, _free_port(), out, C, P, k, iters), nprocs=2, join=True)
+    del prob
+    mp.spawn(_gpu_worker, args=(2, _free_port(), out, C, P, k, iters, loop), nprocs=2, join=True)
     d = np.load(out)
     assert np.allclose(d["costs"], costs, rtol=1e-8)
     assert np.allclose(d["cams"], cams, rtol=1e-6, atol=1e-9)

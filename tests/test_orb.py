@@ -316,6 +316,18 @@ def test_gpu_orb_c2_frames_bit_exact():
 
 
 @pytest.mark.gpu
+def test_gpu_orb_bench_config_bit_exact():
+    """The headline bench's ORB input exactly: textured-corridor frames
+    (bench.py seed 1000) at 1280x720 with 64 kp per tile (~2090 kp/frame):
+    every keypoint, octave and descriptor bit vs the restatement."""
+    from slam355.synthetic import corridor_sequence
+
+    L, R, _, _ = corridor_sequence(4, 1280, 720, seed=1000, device="cuda", as_numpy=True)
+    cnt = _gpu_vs_oracle(np.concatenate([L[:3], R[:2]]), 64)
+    assert (cnt > 1900).all()
+
+
+@pytest.mark.gpu
 def test_gpu_orb_c1_and_reference_cap_bit_exact():
     L, R = _frames(1, 640, 480, seed=1)
     _gpu_vs_oracle(np.concatenate([L, R]), 14)
