@@ -34,7 +34,8 @@ constexpr int kMaxTiles = 256;
 constexpr int kMaxShapes = 4;
 constexpr int kNMS0 = 29;  // score-map region starts here (needs [30, w-31])
 constexpr int kBl0 = 12;   // blurred region starts here (rotated samples within +-18 of [31, w-32])
-constexpr int kFq = (kOrbWG / 64) * 256 * 4;  // FAST survivor queues, bytes
+constexpr int kFqW = 320;  // queue entries per wave: < 64 carried + 256 appended per pass
+constexpr int kFq = (kOrbWG / 64) * kFqW * 4;  // FAST / NMS work queues, bytes
 
 __constant__ int8_t c_pattern[256 * 4];
 
@@ -358,13 +359,24 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     // the 4 map bytes leave as one dword (survivors' scores overwrite theirs below).
     const int NG4 = SW4 >> 2, SN4 = NG4 * SHd;
     const uint32_t mG4 = div_magic(NG4);
-    uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * 4 * 64;
+    uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * kFqW;
     auto win4 = [&](int a) {  // bytes a .. a+3 of the level image (any alignment)
       const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (a & ~3));
       return __builtin_amdgcn_alignbyte(wp[1], wp[0], a & 3);
     };
-    // (trip count wave-uniform: every lane of the wave takes part in the queue drain)
-    for (int gb = wid * 64; gb < SN4; gb += kOrbWG) {
+    // The queue carries over passes and is drained 64 entries at a time (full
+    // waves), the rest after the loop; the trip count is wave-uniform, so every
+    // lane of the wave takes part in each drain.  A survivor's score byte is
+    // stored after its dword of the map was zeroed (same wave, program order).
+    auto fast_drain = [&](int j0) {
+      const int i = (int)fq[j0 + lane];  // padded-map index: y * SW4 + x
+      const int y = fdiv(i, mS4), x = i - y * SW4;
+      Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * P + x + kNMS0, P);
+    };
+    int nq = 0;  // wave-uniform queue length
+    for (int gb = wid * 64;; gb += kOrbWG) {
+      const bool more = gb < SN4;  // wave-uniform
+      if (more) {
       const bool gv = gb + lane < SN4;
       const int gi = min(gb + lane, SN4 - 1);
       const int y = fdiv(gi, mG4), x = 4 * (gi - y * NG4);  // map coords of the first pixel
@@ -380,7 +392,6 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       const uint32_t cc = (uint32_t)(lo >> 24);                    // a .. a+3
       const uint32_t rt = (uint32_t)(((uint64_t)q2 << 32 | q1) >> 16);  // a+3 .. a+6
       const uint32_t okv[2] = {quick4(cc, dn, rt, up, q0), quick4(cc >> 8, dn >> 8, rt >> 8, up >> 8, q0 >> 8)};
-      int nq = 0;  // wave-uniform
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const bool in = gv && x + q < SWd;
@@ -393,11 +404,15 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
         nq += __popcll(m);
       }
       if (gv) *reinterpret_cast<uint32_t*>(Smap + y * SW4 + x) = 0u;
-      for (int j = lane; j < nq; j += 64) {
-        const int i = (int)fq[j];  // padded-map index: y * SW4 + x
-        const int y = fdiv(i, mS4), x = i - y * SW4;
-        Smap[i] = (uint8_t)fast_full(I + (y + kNMS0) * P + x + kNMS0, P);
       }
+      // full waves while the map is scanned, the remainder at the end (one
+      // drain site: the cornerScore code is instantiated once)
+      while (nq >= 64 || (!more && nq > 0)) {
+        const int n = min(nq, 64);
+        nq -= n;
+        if (lane < n) fast_drain(nq);
+      }
+      if (!more) break;
     }
     for (int i = t; i < 256; i += kOrbWG) hist[i] = 0;
     if (t < 8) ctr[t] = 0;
@@ -406,16 +421,30 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     // ---- strict 3x3 NMS + border [31, W-32] -> candidates: one dword of
     // the score map (4 pixels) per lane; the scored pixels (FAST corners,
     // ~8 %) are queued in the wave-private list and take the 8-neighbour test
-    // packed 64 per pass.  The loop trip count is wave-uniform (every lane
-    // stays in it), so a pass drains the whole queue.  The candidate order is
-    // immaterial: the list is ranked by (response, y, x) below and the
-    // histogram is order-free.
+    // 64 at a time (full waves; the queue carries over passes, the rest is
+    // drained after the loop, whose trip count is wave-uniform).  The candidate
+    // order is immaterial: the list is ranked by (response, y, x) below and
+    // the histogram is order-free.
     {
       const int CH = H - 2 * kEdge;
       const int NG = SW4 >> 2, NT = CH * NG;
       const uint32_t mG = div_magic(NG);
-      for (int base = wid * 64; base < NT; base += kOrbWG) {
-        const int i = base + lane;
+      auto nms_drain = [&](int j0) {
+        const uint32_t yx = fq[j0 + lane];
+        const int yq = (int)(yx >> 12), xq = (int)(yx & 4095u);
+        const uint8_t* sp = Smap + (yq - kNMS0) * SW4 + (xq - kNMS0);
+        const int s = sp[0];
+        if (s > sp[-1] && s > sp[1] && s > sp[-SW4 - 1] && s > sp[-SW4] && s > sp[-SW4 + 1] &&
+            s > sp[SW4 - 1] && s > sp[SW4] && s > sp[SW4 + 1]) {
+          const int k = atomicAdd(&ctr[0], 1);
+          if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 23) | yx;
+          atomicAdd(&hist[s], 1);
+        }
+      };
+      int nq = 0;  // wave-uniform
+      for (int base = wid * 64;; base += kOrbWG) {
+        const bool more = base < NT;  // wave-uniform
+        const int i = more ? base + lane : NT;
         uint32_t w4 = 0u;
         int y = 0, g4 = 0;
         if (i < NT) {
@@ -424,7 +453,6 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
           y = yy + kEdge;
           w4 = *reinterpret_cast<const uint32_t*>(Smap + (y - kNMS0) * SW4 + 4 * g4);
         }
-        int nq = 0;  // wave-uniform
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
           const int x = kNMS0 + 4 * g4 + bb;
@@ -436,18 +464,12 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
                 ((uint32_t)y << 12) | (uint32_t)x;
           nq += __popcll(m);
         }
-        for (int j = lane; j < nq; j += 64) {
-          const uint32_t yx = fq[j];
-          const int yq = (int)(yx >> 12), xq = (int)(yx & 4095u);
-          const uint8_t* sp = Smap + (yq - kNMS0) * SW4 + (xq - kNMS0);
-          const int s = sp[0];
-          if (s > sp[-1] && s > sp[1] && s > sp[-SW4 - 1] && s > sp[-SW4] && s > sp[-SW4 + 1] &&
-              s > sp[SW4 - 1] && s > sp[SW4] && s > sp[SW4 + 1]) {
-            const int k = atomicAdd(&ctr[0], 1);
-            if (k < g.cand_cap) gcand[k] = ((uint32_t)s << 23) | yx;
-            atomicAdd(&hist[s], 1);
-          }
+        while (nq >= 64 || (!more && nq > 0)) {
+          const int n = min(nq, 64);
+          nq -= n;
+          if (lane < n) nms_drain(nq);
         }
+        if (!more) break;
       }
     }
     __syncthreads();
@@ -518,74 +540,113 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     const int nk = ctr[1];
     ORB_T(4);
-    // Harris: one wave per survivor, lane 7i + j <-> pixel (i, j) of the 7x7
-    // window; the integer sums a, b, c are reduced across the wave (exact in
-    // any order), the response is formed once
-    for (int k = wid; k < nk; k += kOrbWG / 64) {
-      const uint32_t c = cand[k];
-      const int hx = (int)(c & 4095u), hy = (int)((c >> 12) & 2047u);
-      int a = 0, bq = 0, cq = 0;
-      if (lane < 49) {
-        const int i = lane / 7, j = lane - 7 * (lane / 7);
-        const uint8_t* pp = I + (hy - 3 + i) * P + (hx - 3 + j);
-        const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-P + 1] - pp[-P - 1]) + (pp[P + 1] - pp[P - 1]);
-        const int Iy = (pp[P] - pp[-P]) * 2 + (pp[P - 1] - pp[-P - 1]) + (pp[P + 1] - pp[-P + 1]);
-        a = Ix * Ix;
-        bq = Iy * Iy;
-        cq = Ix * Iy;
+    // Harris: 16 lanes per survivor (4 per wave): lane s of the group takes window
+    // pixels s, s + 16, s + 32, s + 48 (< 49) of the 7x7 block; the integer sums
+    // a, b, c are reduced over the 16 lanes (exact in any order).
+    {
+      const int sub = lane >> 4, sl = lane & 15;
+      for (int k0 = 4 * wid; k0 < nk; k0 += 4 * (kOrbWG / 64)) {
+        const int k = k0 + sub;
+        const uint32_t c = cand[k < nk ? k : k0];
+        const int hx = (int)(c & 4095u), hy = (int)((c >> 12) & 2047u);
+        int a = 0, bq = 0, cq = 0;
+#pragma unroll 2  // (fully unrolled, its 32 loads in flight spill the kernel)
+        for (int u = 0; u < 4; ++u) {
+          const int e = sl + 16 * u;
+          if (e < 49) {
+            const int i = e / 7, j = e - 7 * (e / 7);
+            const uint8_t* pp = I + (hy - 3 + i) * P + (hx - 3 + j);
+            const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-P + 1] - pp[-P - 1]) + (pp[P + 1] - pp[P - 1]);
+            const int Iy = (pp[P] - pp[-P]) * 2 + (pp[P - 1] - pp[-P - 1]) + (pp[P + 1] - pp[-P + 1]);
+            a += Ix * Ix;
+            bq += Iy * Iy;
+            cq += Ix * Iy;
+          }
+        }
+#pragma unroll
+        for (int off = 8; off > 0; off >>= 1) {
+          a += __shfl_xor(a, off, 64);
+          bq += __shfl_xor(bq, off, 64);
+          cq += __shfl_xor(cq, off, 64);
+        }
+        if (sl == 0 && k < nk) cresp[k] = harris_resp(a, bq, cq);
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        a += __shfl_xor(a, off, 64);
-        bq += __shfl_xor(bq, off, 64);
-        cq += __shfl_xor(cq, off, 64);
-      }
-      if (lane == 0) cresp[k] = harris_resp(a, bq, cq);
     }
     __syncthreads();
     ORB_T(5);
-    // ---- exact rank by (response desc, y asc, x asc); L[rank] holds the sorted list
-    for (int i = t; i < nk; i += kOrbWG) {
-      const float ri = cresp[i];
-      const uint32_t ci = cand[i];
-      const uint32_t yxi = ci & 0x7FFFFFu;  // (y << 12) | x: y-major order
-      int rank = 0;
-      int j = 0;
-      for (; j + 4 <= nk; j += 4) {  // 8 LDS reads in flight per step
-        float rj[4];
-        uint32_t yxj[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          rj[u] = cresp[j + u];
-          yxj[u] = cand[j + u] & 0x7FFFFFu;
+    // ---- exact rank by (response desc, y asc, x asc); L[rank] holds the sorted
+    // list; then retainBest(n_l): everything at least as good as the n_l-th
+    // response (ties kept).  Up to 64 survivors (the usual case): wave 0 alone,
+    // lane i holding survivor i, the others' keys broadcast by v_readlane.
+    if (nk <= 64) {
+      if (wid == 0) {
+        const bool live = lane < nk;
+        const uint32_t ci = live ? cand[lane] : 0u;
+        const float ri = live ? cresp[lane] : 0.f;
+        const uint32_t yxi = ci & 0x7FFFFFu;  // (y << 12) | x: y-major order
+        int rank = 0;
+        for (int j = 0; j < nk; ++j) {
+          const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ri), j));
+          const uint32_t yxj = (uint32_t)__builtin_amdgcn_readlane((int)yxi, j);
+          rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
         }
+        if (live) {
+          L[rank].x = (int)(ci & 4095u);
+          L[rank].y = (int)((ci >> 12) & 2047u);
+          L[rank].resp = ri;
+        }
+        int mm = nk;
+        if (nk > n_l) {  // the n_l-th response, then the run of its ties after it
+          const uint64_t bm = __ballot(live && rank == n_l - 1);
+          const float rs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ri),
+                                                                    (int)__builtin_ctzll(bm)));
+          mm = n_l + (int)__popcll(__ballot(live && rank >= n_l && ri == rs));
+        }
+        if (lane == 0) ctr[3] = mm;
+      }
+    } else {
+      for (int i = t; i < nk; i += kOrbWG) {
+        const float ri = cresp[i];
+        const uint32_t ci = cand[i];
+        const uint32_t yxi = ci & 0x7FFFFFu;
+        int rank = 0;
+        int j = 0;
+        for (; j + 4 <= nk; j += 4) {  // 8 LDS reads in flight per step
+          float rj[4];
+          uint32_t yxj[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) rank += (rj[u] > ri || (rj[u] == ri && yxj[u] < yxi)) ? 1 : 0;
+          for (int u = 0; u < 4; ++u) {
+            rj[u] = cresp[j + u];
+            yxj[u] = cand[j + u] & 0x7FFFFFu;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) rank += (rj[u] > ri || (rj[u] == ri && yxj[u] < yxi)) ? 1 : 0;
+        }
+        for (; j < nk; ++j) {
+          const float rj = cresp[j];
+          const uint32_t yxj = cand[j] & 0x7FFFFFu;
+          rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
+        }
+        if (rank < g.list_cap) {
+          L[rank].x = (int)(ci & 4095u);
+          L[rank].y = (int)((ci >> 12) & 2047u);
+          L[rank].resp = ri;
+        }
       }
-      for (; j < nk; ++j) {
-        const float rj = cresp[j];
-        const uint32_t yxj = cand[j] & 0x7FFFFFu;
-        rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
+      __syncthreads();
+      if (t == 0) {
+        int mm = nk;
+        int ovf = 0;
+        if (nk > n_l) {
+          const float rs = L[n_l - 1].resp;
+          mm = n_l;
+          while (mm < nk && mm < g.list_cap && L[mm].resp == rs) ++mm;
+          if (mm == g.list_cap && mm < nk) ovf = 1;
+        } else if (nk > g.list_cap) {
+          ovf = 1;
+        }
+        ctr[3] = ovf ? -1 : mm;
       }
-      if (rank < g.list_cap) {
-        L[rank].x = (int)(ci & 4095u);
-        L[rank].y = (int)((ci >> 12) & 2047u);
-        L[rank].resp = ri;
-      }
-    }
-    __syncthreads();
-    // retainBest(n_l): everything at least as good as the n_l-th response (ties kept)
-    if (t == 0) {
-      int m = nk;
-      int ovf = 0;
-      if (nk > n_l) {
-        const float rs = L[n_l - 1].resp;
-        m = n_l;
-        while (m < nk && m < g.list_cap && L[m].resp == rs) ++m;
-        if (m == g.list_cap && m < nk) ovf = 1;
-      } else if (nk > g.list_cap) {
-        ovf = 1;
-      }
-      ctr[3] = ovf ? -1 : m;
     }
     __syncthreads();
     const int m = ctr[3];
