@@ -204,6 +204,16 @@ __device__ unsigned long long g_orb_prof[16];
 #define ORB_T0() (void)0
 #define ORB_T(ph) (void)0
 #endif
+// -DSLAM_ORB_CUT=k (profiling builds only, scripts/gpu_r3_orbcut.sh): every
+// level stops after phase k (1 resize, 2 FAST, 3 NMS, 6 rank, 7 IC angle,
+// 8 blur), so the SQ counters of successive cuts split the LDS instructions /
+// bank conflicts by phase (profiles/r3_orb_lds_phases_v1.json).
+#ifdef SLAM_ORB_CUT
+#define ORB_CUT(ph) \
+  if ((ph) == SLAM_ORB_CUT) continue
+#else
+#define ORB_CUT(ph) (void)0
+#endif
 
 struct KP {  // one kept keypoint of the current level (LDS)
   int x, y;
@@ -338,6 +348,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       }
       ORB_T(1);
     }
+    ORB_CUT(1);
     uint8_t* I = A;
     const int n_l = g.nl[l];
     if (W <= 2 * kEdge || H <= 2 * kEdge || n_l == 0) continue;  // uniform
@@ -418,6 +429,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (t < 8) ctr[t] = 0;
     __syncthreads();
     ORB_T(2);
+    ORB_CUT(2);
     // ---- strict 3x3 NMS + border [31, W-32] -> candidates: one dword of
     // the score map (4 pixels) per lane; the scored pixels (FAST corners,
     // ~8 %) are queued in the wave-private list and take the 8-neighbour test
@@ -474,6 +486,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
     __syncthreads();
     ORB_T(3);
+    ORB_CUT(3);
     const int ncand = ctr[0];
     if (ncand > g.cand_cap) {  // cannot happen for strict maxima (density <= 1/4); guard anyway
       overflow = 1;
@@ -651,6 +664,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     const int m = ctr[3];
     ORB_T(6);
+    ORB_CUT(6);
     if (m < 0 || nout + m > g.tcap) {
       overflow = 1;
       break;
@@ -694,6 +708,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     uint8_t* Bl = U;
     __syncthreads();  // Smap and the survivor lists are dead from here (L holds the level)
     ORB_T(7);
+    ORB_CUT(7);
     {
       // 4 adjacent output columns per lane (x = kBl0 + 4 cg: a dword boundary of
       // the pitched level): the 10 source bytes x-3 .. x+6 of a row are the
@@ -747,44 +762,48 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
           o = make_float4(r[0], r[1], r[2], r[3]);
         };
         const int yb = r0 + kBl0;  // first output row (image coords)
-        float4 w0, w1, w2, w3, w4, w5, w6;
-        rowf4(yb - 3, w0);
-        rowf4(yb - 2, w1);
-        rowf4(yb - 1, w2);
-        rowf4(yb, w3);
-        rowf4(yb + 1, w4);
-        rowf4(yb + 2, w5);
-        rowf4(yb + 3, w6);
-        for (int r = r0; r < r1; ++r) {
-          float v4[4];
-          const float a0[4] = {w0.x, w0.y, w0.z, w0.w}, a1[4] = {w1.x, w1.y, w1.z, w1.w};
-          const float a2[4] = {w2.x, w2.y, w2.z, w2.w}, a3[4] = {w3.x, w3.y, w3.z, w3.w};
-          const float a4[4] = {w4.x, w4.y, w4.z, w4.w}, a5[4] = {w5.x, w5.y, w5.z, w5.w};
-          const float a6[4] = {w6.x, w6.y, w6.z, w6.w};
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float s0 = a3[j] * k3;
-            s0 = fmaf(a4[j] + a2[j], k4, s0);
-            s0 = fmaf(a5[j] + a1[j], k5, s0);
-            s0 = fmaf(a6[j] + a0[j], k6, s0);
-            v4[j] = s0;
-          }
-          uint32_t packed = 0u;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int v = (int)rintf(v4[j]);
-            packed |= (uint32_t)(v < 0 ? 0 : v > 255 ? 255 : v) << (8 * j);
-          }
-          *reinterpret_cast<uint32_t*>(Bl + r * BP + c4) = packed;
-          if (r + 1 < r1) {
-            w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6;
-            rowf4(r + 1 + kBl0 + 3, w6);
-          }
+        // the 7 row sums of the window in a ring of registers: output row r0 + k
+        // reads slots (k .. k + 6) mod 7 and its successor's new row replaces
+        // slot k mod 7 -- the loop is unrolled 7 times so the ring rotates by
+        // renaming (a shifted window costs 14 register moves per row).  Column
+        // pass on packed pairs (columns 0-1, 2-3: v_pk_add / v_pk_mul / v_pk_fma,
+        // per element the scalar form's operations); rounded results packed by
+        // v_cvt_pk_u8_f32 (exact: they are integers in [0, 255])
+        float4 w[7];
+        static_for<0, 7>([&](auto I) { rowf4(yb - 3 + decltype(I)::value, w[decltype(I)::value]); });
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 kk3 = {k3, k3}, kk4 = {k4, k4}, kk5 = {k5, k5}, kk6 = {k6, k6};
+        for (int r = r0; r < r1; r += 7) {
+          static_for<0, 7>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if (r + k < r1) {
+              const float4 a0 = w[k % 7], a1 = w[(k + 1) % 7], a2 = w[(k + 2) % 7];
+              const float4 a3 = w[(k + 3) % 7], a4 = w[(k + 4) % 7], a5 = w[(k + 5) % 7];
+              const float4 a6 = w[(k + 6) % 7];
+              auto col = [&](f2 x0, f2 x1, f2 x2, f2 x3, f2 x4, f2 x5, f2 x6) {
+                f2 s0 = x3 * kk3;
+                s0 = __builtin_elementwise_fma(x4 + x2, kk4, s0);
+                s0 = __builtin_elementwise_fma(x5 + x1, kk5, s0);
+                return __builtin_elementwise_fma(x6 + x0, kk6, s0);
+              };
+              const f2 lo = col(f2{a0.x, a0.y}, f2{a1.x, a1.y}, f2{a2.x, a2.y}, f2{a3.x, a3.y},
+                                f2{a4.x, a4.y}, f2{a5.x, a5.y}, f2{a6.x, a6.y});
+              const f2 hi = col(f2{a0.z, a0.w}, f2{a1.z, a1.w}, f2{a2.z, a2.w}, f2{a3.z, a3.w},
+                                f2{a4.z, a4.w}, f2{a5.z, a5.w}, f2{a6.z, a6.w});
+              uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(lo.x), 0, 0u);
+              packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(lo.y), 1, packed);
+              packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(hi.x), 2, packed);
+              packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(hi.y), 3, packed);
+              *reinterpret_cast<uint32_t*>(Bl + (r + k) * BP + c4) = packed;
+              if (r + k + 1 < r1) rowf4(r + k + 1 + kBl0 + 3, w[k]);
+            }
+          });
         }
       }
     }
     __syncthreads();
     ORB_T(8);
+    ORB_CUT(8);
     // ---- rBRIEF: 32 lanes per keypoint, one byte per lane; write the keypoint
     {
       const float ls = g.ls[l];
