@@ -37,7 +37,7 @@ constexpr int kBl0 = 12;   // blurred region starts here (rotated samples within
 constexpr int kFqW = 320;  // queue entries per wave: < 64 carried + 256 appended per pass
 constexpr int kFq = (kOrbWG / 64) * kFqW * 4;  // FAST / NMS work queues, bytes
 
-__constant__ int8_t c_pattern[256 * 4];
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[256 * 4];
 
 struct OrbGeom {
   int H, W, stride;
@@ -101,24 +101,24 @@ __device__ __forceinline__ uint32_t quick4(uint32_t v, uint32_t dn, uint32_t rt,
 // Full segment test + OpenCV cornerScore<16> at c (past the quick reject).
 __device__ __forceinline__ int fast_full(const uint8_t* c, int st) {
   const int v = c[0];
-  int d[16];
-  d[0] = v - c[3 * st];
-  d[1] = v - c[3 * st + 1];
-  d[2] = v - c[2 * st + 2];
-  d[3] = v - c[st + 3];
-  d[4] = v - c[3];
-  d[5] = v - c[-st + 3];
-  d[6] = v - c[-2 * st + 2];
-  d[7] = v - c[-3 * st + 1];
-  d[8] = v - c[-3 * st];
-  d[9] = v - c[-3 * st - 1];
-  d[10] = v - c[-2 * st - 2];
-  d[11] = v - c[-st - 3];
-  d[12] = v - c[-3];
-  d[13] = v - c[st - 3];
-  d[14] = v - c[2 * st - 2];
-  d[15] = v - c[3 * st - 1];
-  // OpenCV cornerScore<16> is max(t, A_dark, A_bright) - 1 with A_dark = the
+  int cc[16];  // the circle pixels, d[k] = v - cc[k]
+  cc[0] = c[3 * st];
+  cc[1] = c[3 * st + 1];
+  cc[2] = c[2 * st + 2];
+  cc[3] = c[st + 3];
+  cc[4] = c[3];
+  cc[5] = c[-st + 3];
+  cc[6] = c[-2 * st + 2];
+  cc[7] = c[-3 * st + 1];
+  cc[8] = c[-3 * st];
+  cc[9] = c[-3 * st - 1];
+  cc[10] = c[-2 * st - 2];
+  cc[11] = c[-st - 3];
+  cc[12] = c[-3];
+  cc[13] = c[st - 3];
+  cc[14] = c[2 * st - 2];
+  cc[15] = c[3 * st - 1];
+  // OpenCV cornerScore<16> (d = v - cc) is max(t, A_dark, A_bright) - 1 with A_dark = the
   // largest min(d) over the 16 circular 9-arcs and A_bright the same for -d; a
   // segment test pass (9 consecutive d > t, or -d > t) is exactly A > t, so
   //   score = A > t ? A - 1 : 0,  A = max(A_dark, A_bright).
@@ -127,8 +127,15 @@ __device__ __forceinline__ int fast_full(const uint8_t* c, int st) {
   // built from pairwise minima (m2 -> m4 -> m8).
   typedef short s2 __attribute__((ext_vector_type(2)));
   s2 p[16];
+  // (v - c, c - v) as ONE packed subtract of X = (v, c) and its swapped
+  // halves (op_sel), X built by one v_lshl_or: 2 ops per circle pixel, not 3
 #pragma unroll
-  for (int k = 0; k < 16; ++k) p[k] = s2{(short)d[k], (short)-d[k]};
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t X = (uint32_t)v | ((uint32_t)cc[k] << 16);
+    uint32_t r;  // lo = X.lo - X.hi, hi = X.hi - X.lo (the compiler would materialise X.yx)
+    __asm__("v_pk_sub_i16 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(X));
+    p[k] = __builtin_bit_cast(s2, r);
+  }
   s2 m2[8], m4[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k)  // min over 2k+1, 2k+2
@@ -309,6 +316,10 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       // consecutive dwords).  The padding bytes of a row get junk, never read.
       const int NG = P >> 2, NT = NG * H;
       const uint32_t mNG = div_magic(NG);
+      // an opaque 1 (H > 0 is checked on the host): rp[0] / rp[1] stay two
+      // byte reads (merged, they become a ds_read_u16 at odd addresses, which
+      // made the kernel 1.5x slower)
+      const int one = g.H > 0 ? 1 : 0;
       for (int i = t; i < NT; i += kOrbWG) {
         const int y = fdiv(i, mNG), x = 4 * (i - y * NG);
         const int cy = taby[y];
@@ -320,12 +331,21 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint8_t* rp = r0 + (cx[q] >> 9);
-          // the +1 neighbours are only read with a non-zero weight (the
-          // last column / row may sit on the source edge)
           p00[q] = rp[0];
-          p01[q] = (cx[q] & 511) ? rp[1] : 0;
-          p10[q] = d1 ? rp[SP] : 0;
-          p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
+          if (kGlob) {
+            // global level buffers: the +1 neighbours are only read with a
+            // non-zero weight (the last column / row may sit on the buffer's end)
+            p01[q] = (cx[q] & 511) ? rp[1] : 0;
+            p10[q] = d1 ? rp[SP] : 0;
+            p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
+          } else {
+            // LDS: past the last source row / column lies more of the LDS
+            // allocation (U follows A), and a neighbour outside the source has
+            // weight 0 -- read unconditionally (no exec-mask code per byte)
+            p01[q] = rp[one];
+            p10[q] = rp[SP];
+            p11[q] = rp[SP + one];
+          }
         }
         uint32_t w = 0u;
 #pragma unroll
@@ -709,6 +729,34 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();  // Smap and the survivor lists are dead from here (L holds the level)
     ORB_T(7);
     ORB_CUT(7);
+    // ---- keypoint records (one lane per keypoint, wave 0): the output row, and
+    // L[k] becomes what rBRIEF needs -- the sample centre in blurred-level
+    // coordinates and cos / sin of the angle -- computed once per keypoint
+    // instead of by each of its 32 rBRIEF lanes (the f64 sin / cos sequences
+    // were issued once per half wave); published by the barrier after the blur
+    if (wid == 0) {
+      const float ls = g.ls[l];
+      for (int k = lane; k < m; k += 64) {
+        const KP kp = L[k];
+        const float xl = (float)kp.x * ls, yl = (float)kp.y * ls;  // pt *= layerScale
+        const float inv = 1.f / ls;
+        const int o = nout + k;
+        okp[(size_t)o * 5 + 0] = (float)((double)xl + (double)x0);
+        okp[(size_t)o * 5 + 1] = (float)((double)yl + (double)y0);
+        okp[(size_t)o * 5 + 2] = 31.f * ls;
+        okp[(size_t)o * 5 + 3] = kp.angle;
+        okp[(size_t)o * 5 + 4] = kp.resp;
+        ooct[o] = l;
+        float ang = kp.angle;
+        ang *= (float)(3.14159265358979323846 / 180.f);
+        KP q;
+        q.x = rne_f(xl * inv) - kBl0;
+        q.y = rne_f(yl * inv) - kBl0;
+        q.resp = (float)cos((double)ang);
+        q.angle = (float)sin((double)ang);
+        L[k] = q;
+      }
+    }
     {
       // 4 adjacent output columns per lane (x = kBl0 + 4 cg: a dword boundary of
       // the pitched level): the 10 source bytes x-3 .. x+6 of a row are the
@@ -804,40 +852,34 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     ORB_T(8);
     ORB_CUT(8);
-    // ---- rBRIEF: 32 lanes per keypoint, one byte per lane; write the keypoint
+    // ---- rBRIEF: 32 lanes per keypoint, one descriptor byte per lane
     {
-      const float ls = g.ls[l];
       const int half = lane >> 5, byte = lane & 31;
+      // the lane's 8 pattern pairs, one dword each (x1, y1, x2, y2 as int8),
+      // kept across keypoints; converted per use (32 converted floats kept
+      // live across the loop made the kernel spill)
+      uint32_t pat[8];
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit)
+        pat[bit] = reinterpret_cast<const uint32_t*>(c_pattern)[byte * 8 + bit];
       for (int k = 2 * wid + half; k < m; k += 2 * (kOrbWG / 64)) {
-        const KP kp = L[k];
-        const float xl = (float)kp.x * ls, yl = (float)kp.y * ls;  // pt *= layerScale
-        const float inv = 1.f / ls;
-        const int cx = rne_f(xl * inv) - kBl0, cy = rne_f(yl * inv) - kBl0;
-        float ang = kp.angle;
-        ang *= (float)(3.14159265358979323846 / 180.f);
-        const float a = (float)cos((double)ang), bb = (float)sin((double)ang);
+        const KP kp = L[k];  // (centre x, centre y, cos, sin), see above
+        const int cx = kp.x, cy = kp.y;
+        const float a = kp.resp, bb = kp.angle;
         int val = 0;
 #pragma unroll
         for (int bit = 0; bit < 8; ++bit) {
-          const int8_t* pp = c_pattern + (byte * 8 + bit) * 4;
-          const float px1 = (float)pp[0], py1 = (float)pp[1];
-          const float px2 = (float)pp[2], py2 = (float)pp[3];
+          uint32_t pw = pat[bit];
+          __asm__ volatile("" : "+v"(pw));
+          const float px1 = (float)(int8_t)(pw & 0xFFu), py1 = (float)(int8_t)((pw >> 8) & 0xFFu);
+          const float px2 = (float)(int8_t)((pw >> 16) & 0xFFu), py2 = (float)(int8_t)(pw >> 24);
           const int ix1 = rne_f(px1 * a - py1 * bb), iy1 = rne_f(px1 * bb + py1 * a);
           const int ix2 = rne_f(px2 * a - py2 * bb), iy2 = rne_f(px2 * bb + py2 * a);
           const int t0 = Bl[(cy + iy1) * BP + cx + ix1];
           const int t1 = Bl[(cy + iy2) * BP + cx + ix2];
           val |= (t0 < t1 ? 1 : 0) << bit;
         }
-        const int o = nout + k;
-        odesc[(size_t)o * 32 + byte] = (uint8_t)val;
-        if (byte == 0) {
-          okp[(size_t)o * 5 + 0] = (float)((double)xl + (double)x0);
-          okp[(size_t)o * 5 + 1] = (float)((double)yl + (double)y0);
-          okp[(size_t)o * 5 + 2] = 31.f * ls;
-          okp[(size_t)o * 5 + 3] = kp.angle;
-          okp[(size_t)o * 5 + 4] = kp.resp;
-          ooct[o] = l;
-        }
+        odesc[(size_t)(nout + k) * 32 + byte] = (uint8_t)val;
       }
     }
     nout += m;
