@@ -410,12 +410,24 @@ def run_tracking(args, world, rank):
                      "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
+    # the stereo matcher launch (keypoint.py:44: B pairs of ~2000 x ~2000
+    # descriptors): integer-VALU bound, pairs x ops / VALU peak
+    oc = cnt["orb"].astype(np.int64)
+    m_pairs = float((oc[:B] * oc[B + 1:2 * B + 1]).sum())
+    m_ms = stages.get("stereo_knn2", float("nan"))
+    roof["matcher"] = {"bound": "valu", "achieved": m_pairs * MATCH_OPS_PER_PAIR / (m_ms * 1e-3) / 1e12,
+                       "peak": VALU_PEAK_TOPS, "unit": "Tops/s", "kernel": "knn2_kernel (stereo, in the pipeline)",
+                       "ms_per_launch": m_ms, "pairs_per_launch": m_pairs,
+                       "ops_per_pair": MATCH_OPS_PER_PAIR,
+                       "unique_descriptor_bytes": float(oc[:B].sum() + oc[B + 1:2 * B + 1].sum()) * 32}
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_assemble", "k_solve_blk",
                                                   "k_back_trial<true>"))
+    roof["matcher"]["traffic"] = pmc_bytes(pmc, ("knn2_kernel",))
     units = {"orb": f"bytes per ORB launch ({n_img} images), HBM, from PMC",
-             "local_ba": f"bytes per batched LM iteration ({n_launch} windows), HBM, from PMC"}
+             "local_ba": f"bytes per batched LM iteration ({n_launch} windows), HBM, from PMC",
+             "matcher": "bytes per knn2_kernel dispatch (mean of the stereo and temporal launches), HBM, from PMC"}
     for name, r in roof.items():
         r["frac"] = r["achieved"] / r["peak"]
         if r["traffic"] is not None:
@@ -454,6 +466,11 @@ def run_tracking(args, world, rank):
                    "orb_stream": (f"pipelined, CUs 0..{args.orb_cus - 1}" if args.orb_cus else
                                   "pipelined, all CUs") if args.orb_pipeline else "tracking stream",
                    "local_ba_cus": args.ba_cus or "all",
+                   # the headline's windows are fixed synthetic C3 problems (clean
+                   # tracks, sigma 0.5 px), restored and re-solved every launch set;
+                   # BA over windows built from the tracked frames is measured
+                   # beside it in "tracked_window_ba" (its per-window build cost there)
+                   "local_ba_source": "synthetic C3",
                    "local_ba_launch_set": (f"{n_launch} windows every {G} steps (pending steps flushed "
                                            "as a whole set at the ends of warmup and timed region)" if G > 1 else
                                            f"{n_launch} windows every step")},

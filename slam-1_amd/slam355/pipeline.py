@@ -151,6 +151,7 @@ class Tracker:
         kpL1, dL1, nL1 = kp[1:B + 1], desc[1:B + 1], cnt[1:B + 1]
         # stereo: kNN-2 + ratio (keypoint.py:44-51), gather (:96-97)
         matcher.knn2_batch(dL, nL, dR, nR, out=(self.s_idx2, self.s_dist2, self.s_good), stream=st)
+        mark("stereo_knn2")
         matcher.compact_matches(self.s_idx2, self.s_good, nL, out=(self.s_pairs, self.s_cnt),
                                 stream=st)
         geometry.gather_matches(kpL, kpR, self.s_pairs, self.s_cnt,
