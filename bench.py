@@ -42,7 +42,9 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0
 F64_PEAK_TFLOPS = 78.6        # FP64 vector == FP64 matrix on gfx950 (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 78.6 T lane-ops/s (4 x SIMD32 per CU)
-MATCH_OPS_PER_PAIR = 19       # 8 v_xor + 8 v_bcnt(+acc) + v_lshl_or + v_min + v_med3
+MATCH_OPS_PER_PAIR = 19       # 8 v_xor + 8 v_bcnt(+acc) + v_lshl_or + v_min + v_med3 (VALU kernel)
+FP4_PEAK_TFLOPS = 10000.0     # FP4 MFMA dense ~10 PF (MI355X_MICROARCH.md chip-level table)
+MX_FLOPS_PER_PAIR = 2 * 256   # the fp4 matrix-core matcher: 256 MACs per descriptor pair
 ORB_OUT_BYTES = 56            # per keypoint: 5 f32 + octave i32 + 32 B descriptor
 W_IMG, H_IMG = 1280, 720
 
@@ -233,6 +235,24 @@ class FrameFeed:
         self.k += 1
 
 
+def matcher_roofline(pairs, ms, t_cap, where, force_valu=False):
+    """Roofline of one kNN-2 launch: the fp4 matrix-core kernel (t_cap <= 16383)
+    against the FP4 MFMA dense peak (256 MACs per pair), the integer-VALU kernel
+    against the VALU peak (19 ops per pair); both fractions reported."""
+    mx = t_cap <= 16383 and not force_valu
+    valu_tops = pairs * MATCH_OPS_PER_PAIR / (ms * 1e-3) / 1e12
+    if mx:
+        r = {"bound": "mfma", "achieved": pairs * MX_FLOPS_PER_PAIR / (ms * 1e-3) / 1e12,
+             "peak": FP4_PEAK_TFLOPS, "unit": "TFLOP/s (fp4)", "kernel": f"knn2_mx_kernel ({where})",
+             "flops_per_pair": MX_FLOPS_PER_PAIR}
+    else:
+        r = {"bound": "valu", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
+             "kernel": f"knn2_kernel ({where})", "ops_per_pair": MATCH_OPS_PER_PAIR}
+    r.update(ms_per_launch=ms, pairs_per_launch=pairs, gpairs_per_s=pairs / (ms * 1e-3) / 1e9,
+             valu_equivalent_frac=valu_tops / VALU_PEAK_TOPS)
+    return r
+
+
 def run_tracking(args, world, rank):
     from slam355.ba import BABatch, BAProblem
     from slam355.pipeline import Tracker
@@ -415,19 +435,16 @@ def run_tracking(args, world, rank):
     oc = cnt["orb"].astype(np.int64)
     m_pairs = float((oc[:B] * oc[B + 1:2 * B + 1]).sum())
     m_ms = stages.get("stereo_knn2", float("nan"))
-    roof["matcher"] = {"bound": "valu", "achieved": m_pairs * MATCH_OPS_PER_PAIR / (m_ms * 1e-3) / 1e12,
-                       "peak": VALU_PEAK_TOPS, "unit": "Tops/s", "kernel": "knn2_kernel (stereo, in the pipeline)",
-                       "ms_per_launch": m_ms, "pairs_per_launch": m_pairs,
-                       "ops_per_pair": MATCH_OPS_PER_PAIR,
-                       "unique_descriptor_bytes": float(oc[:B].sum() + oc[B + 1:2 * B + 1].sum()) * 32}
+    roof["matcher"] = matcher_roofline(m_pairs, m_ms, trk.cap, "stereo, in the pipeline")
+    roof["matcher"]["unique_descriptor_bytes"] = float(oc[:B].sum() + oc[B + 1:2 * B + 1].sum()) * 32
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_assemble", "k_solve_blk",
                                                   "k_back_trial<true>"))
-    roof["matcher"]["traffic"] = pmc_bytes(pmc, ("knn2_kernel",))
+    roof["matcher"]["traffic"] = pmc_bytes(pmc, (roof["matcher"]["kernel"].split()[0],))
     units = {"orb": f"bytes per ORB launch ({n_img} images), HBM, from PMC",
              "local_ba": f"bytes per batched LM iteration ({n_launch} windows), HBM, from PMC",
-             "matcher": "bytes per knn2_kernel dispatch (mean of the stereo and temporal launches), HBM, from PMC"}
+             "matcher": "bytes per matcher dispatch (mean of the stereo and temporal launches), HBM, from PMC"}
     for name, r in roof.items():
         r["frac"] = r["achieved"] / r["peak"]
         if r["traffic"] is not None:
@@ -755,6 +772,10 @@ def run_matcher(args, world, rank):
     from slam355 import matcher
     from slam355.synthetic import descriptor_batch
 
+    if args.valu:
+        from slam355 import _lib
+
+        _lib.lib.slam_hamming_force_valu(1)
     q, nq, t, nt = descriptor_batch(args.batch, 2000, 2000, seed=rank)
     dev = torch.device("cuda")
     tq, tt = torch.from_numpy(q).to(dev), torch.from_numpy(t).to(dev)
@@ -776,7 +797,9 @@ def run_matcher(args, world, rank):
     dt, stages = timed_loop(step, args.steps, args.warmup, world)
     pairs = float((nq.astype(np.int64) * nt).sum())
     kms = stages["knn2"]
-    achieved = pairs * MATCH_OPS_PER_PAIR / (kms * 1e-3) / 1e12
+    roof = matcher_roofline(pairs, kms, t.shape[1], f"batch {args.batch}", args.valu)
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    roof["traffic"] = None
     return {
         "metric": "BF-Hamming kNN-2 match throughput @ C2 (2000x2000 x 32 B descriptors)",
         "value": reduce_scalar(pairs * args.steps, world, "sum") / dt / 1e9, "unit": "Gpairs/s",
@@ -785,9 +808,7 @@ def run_matcher(args, world, rank):
         "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (seeded random descriptors, 60% planted near-duplicates)",
         "config": {"workload": "C2 matcher", "batch_pairs_per_gpu": args.batch},
-        "roofline": {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TOPS, "unit": "Tops/s",
-                     "frac": achieved / VALU_PEAK_TOPS, "traffic": None, "kernel": "knn2_kernel",
-                     "ms_per_launch": kms},
+        "roofline": roof,
     }
 
 
@@ -968,6 +989,8 @@ def main():
     ap.add_argument("--solve-lds-floor", type=int, default=0,
                     help="LDS bytes the one-workgroup camera solve requests at least "
                          "(slam_ba_set_solve_lds_floor)")
+    ap.add_argument("--valu", action="store_true",
+                    help="matcher: force the integer-VALU kNN-2 kernel (default: fp4 matrix cores)")
     ap.add_argument("--no-tracked-ba", action="store_true",
                     help="tracking: skip the local BA of a window built from tracked frames")
     ap.add_argument("--ba-cus", type=int, default=0,

@@ -64,12 +64,19 @@ int slam_device_count(void);
  * (`10*d1 < 7*d2` == `d1 < 0.7*d2` for every integer d1, d2 in [0, 256].)
  * A train set with fewer than 2 rows yields no good matches, mirroring the
  * reference's ValueError truncation (keypoint.py:46-51).
- * t_cap must be <= 65535.
+ * t_cap must be <= 65535.  t_cap <= 16383 runs on the fp4 matrix cores
+ * (knn2_mx_kernel: exact integer keys in f32), larger train sets on the
+ * integer VALU (knn2_kernel); both give identical outputs.
  * ---------------------------------------------------------------------- */
 int slam_hamming_knn2(const uint8_t* d_q, const int32_t* d_nq, int q_cap,
                       const uint8_t* d_t, const int32_t* d_nt, int t_cap,
                       int batch, int32_t* d_idx2, int32_t* d_dist2,
                       uint8_t* d_good, void* stream);
+
+/* Kernel selection of slam_hamming_knn2 for A/B tests and benchmarks:
+ * valu != 0 forces the integer-VALU kernel, 0 (default) the matrix-core one
+ * where t_cap allows.  Process-wide; returns the previous setting. */
+int slam_hamming_force_valu(int valu);
 
 /* Order-preserving compaction of the good matches of slam_hamming_knn2:
  * d_pairs [batch][q_cap][2] i32 = (queryIdx, trainIdx) of the good rows in

@@ -24,6 +24,7 @@ constexpr int kWaves = kWG / kWave;     // 8: the train rows of a chunk are spli
 constexpr int kQPL = 2;                 // queries per lane
 constexpr int kQPerWG = kWave * kQPL;   // 128 queries per workgroup (every wave holds all of them)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
+int g_knn2_valu = 0;  // slam_hamming_force_valu
 
 // popcount-accumulate: v_bcnt_u32_b32 d, x, acc (one VALU op per dword; the
 // compiler would otherwise split the sum into v_add3 trees)
@@ -159,6 +160,241 @@ __global__ __launch_bounds__(kWG) void knn2_kernel(
   good[o] = (m2 != kNone && 10 * ds.x < 7 * ds.y) ? 1 : 0;
 }
 
+// ---------------------------------------------------------------- matrix-core matcher
+// The same kNN-2 on the fp4 matrix cores (v_mfma_scale_f32_16x16x128_f8f6f4,
+// e2m1 operands, K = 128 bits per instruction, two per 256-bit descriptor).
+// With query bits as +1.0 and train bits as -2.0 x 2^14 (E8M0 block scale
+// 141), and the accumulator of column j initialised to (pt_j + 256) 2^14 + j
+// (pt_j = popcount of train row j), one 16 x 16 tile of the product is
+//   key(i, j) = (pt_j - 2 popcount(q_i & t_j) + 256) 2^14 + j
+//             = (H(q_i, t_j) - pq_i + 256) 2^14 + j,
+// every term an integer below 2^24, so the f32 accumulation is exact and its
+// order immaterial.  For a fixed query the key orders train rows exactly as
+// the VALU kernel's dist << 16 | j (Hamming distance, ties to the lower
+// index); the running top-2 is v_min_f32 / v_med3_f32 on the keys.
+//   * one workgroup = 64 queries (4 blocks of 16) x the whole train set; its
+//     4 waves hold the same query fragments in registers and take every 4th
+//     step of 16 train rows (4 waves per SIMD at the C2 batch: the MFMA /
+//     load latency of one wave hides behind the others), each lane loading
+//     its column's whole 32-byte row 2 steps ahead (popcount in-lane); the
+//     wave partials are merged over the 16 column-lanes (shuffles), then over
+//     the 4 waves through LDS in wave order (keys are unique: the order is
+//     immaterial anyway);
+//   * byte -> 8 fp4 nibbles through two 1 KiB LDS tables (+1.0 / -2.0);
+//   * operand map (scripts/micro/mx_hamming.hip, exact on the GPU): lane l
+//     holds row / column l & 15 and bits [32 (l >> 4), +32) of each 128-bit
+//     half as 32 nibbles, low nibble first (any k order shared by A and B is
+//     harmless); C/D: row 4 (l >> 4) + r, column l & 15 -- each lane keeps a
+//     partial top-2 of 4 queries per block over the columns = l mod 16.
+// Train row index < 2^14 (t_cap <= 16383; larger sets take knn2_kernel).
+#ifndef SLAM_MX_WG
+#define SLAM_MX_WG 256
+#endif
+constexpr int kMxWG = SLAM_MX_WG;          // 4 waves: train steps dealt round-robin
+constexpr int kMxWaves = kMxWG / kWave;
+#ifndef SLAM_MX_QB
+#define SLAM_MX_QB 8
+#endif
+constexpr int kMxQB = SLAM_MX_QB;          // query blocks of 16 (8: 4 per step measured 10 % slower)
+constexpr int kMxQWG = 16 * kMxQB;         // queries per workgroup
+constexpr int kMxAhead = 2;                // train steps loaded ahead
+constexpr float kMxNone = 16777215.0f;     // > every valid key (< 2^23 + 2^14)
+typedef int mx_v8i __attribute__((ext_vector_type(8)));
+typedef float mx_v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t spread8(uint32_t b, uint32_t nib) {  // 8 bits -> 8 nibbles
+  uint32_t x = b & 0xFFu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  x = (x | (x << 3)) & 0x11111111u;
+  return x * nib;
+}
+
+__global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
+    const uint32_t* __restrict__ q, const int32_t* __restrict__ nq_arr, int q_cap,
+    const uint32_t* __restrict__ t, const int32_t* __restrict__ nt_arr, int t_cap,
+    int tiles_per_item, int2* __restrict__ idx2, int2* __restrict__ dist2,
+    uint8_t* __restrict__ good) {
+  __shared__ uint32_t lut[2][256];  // byte -> 8 fp4 nibbles: +1.0 (0x2), -2.0 (0xC)
+  __shared__ uint32_t part[kMxWaves][kMxQWG][2];
+  const int item = blockIdx.x / tiles_per_item;
+  const int tile = blockIdx.x - item * tiles_per_item;
+  const int nq = min(max(nq_arr[item], 0), q_cap);
+  const int nt = min(max(nt_arr[item], 0), t_cap);
+  const int q0 = tile * kMxQWG;
+  if (q0 >= nq) return;  // uniform over the workgroup
+  if (threadIdx.x < 256) {
+    lut[0][threadIdx.x] = spread8(threadIdx.x, 0x2u);
+    lut[1][threadIdx.x] = spread8(threadIdx.x, 0xCu);
+  }
+  __syncthreads();
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int l = threadIdx.x & (kWave - 1), r = l & 15, g = l >> 4;
+  const uint32_t* qb = q + (size_t)item * q_cap * 8;
+  const uint4* tb = reinterpret_cast<const uint4*>(t + (size_t)item * t_cap * 8);
+  // query fragments: block b, half h = dword 4 h + g of query q0 + 16 b + r
+  mx_v8i A[kMxQB][2];
+#pragma unroll
+  for (int b = 0; b < kMxQB; ++b) {
+    const int qi = q0 + 16 * b + r;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t w = qi < nq ? qb[(size_t)qi * 8 + 4 * h + g] : 0u;
+      A[b][h] = mx_v8i{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) A[b][h][d] = (int)lut[0][(w >> (8 * d)) & 255u];
+    }
+  }
+  uint32_t k1[kMxQB][4], k2[kMxQB][4];  // key bit patterns (non-negative floats)
+#pragma unroll
+  for (int b = 0; b < kMxQB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k1[b][i] = k2[b][i] = __float_as_uint(kMxNone);
+  // this wave's steps: train rows 16 (wid + 4 s) + r; whole rows, kMxAhead
+  // ahead.  Software pipeline: while the MFMAs of step s run, the operands of
+  // step s + 1 are formed (popcount, byte -> nibble tables) and the keys of
+  // step s - 1 are folded into the top-2 (the loop is unrolled twice so the
+  // two accumulator sets alternate by name).
+  const int nsteps = (nt + 15) >> 4;
+  const int nmine = nsteps > wid ? (nsteps - wid + kMxWaves - 1) / kMxWaves : 0;  // uniform
+  uint4 ra[kMxAhead][2];
+  auto ld = [&](int s, uint4 (&o)[2]) {
+    const int j = 16 * (wid + kMxWaves * s) + r;
+    const size_t row = (size_t)min(j, max(nt - 1, 0));
+    const bool ok = nt > 0 && s < nmine;
+    o[0] = ok ? tb[2 * row] : make_uint4(0, 0, 0, 0);
+    o[1] = ok ? tb[2 * row + 1] : make_uint4(0, 0, 0, 0);
+  };
+  // operands of step s from its row (ra[0]): B halves and the accumulator seed
+  struct Ops {
+    mx_v8i B0, B1;
+    float init;
+  };
+  auto form = [&](int s) {
+    const uint4 x = ra[0][0], y = ra[0][1];
+#pragma unroll
+    for (int a = 0; a + 1 < kMxAhead; ++a) {
+      ra[a][0] = ra[a + 1][0];
+      ra[a][1] = ra[a + 1][1];
+    }
+    ld(s + kMxAhead, ra[kMxAhead - 1]);
+    const int j = 16 * (wid + kMxWaves * s) + r;
+    const bool valid = j < nt && s < nmine;
+    const int pc = __builtin_popcount(x.x) + __builtin_popcount(x.y) + __builtin_popcount(x.z) +
+                   __builtin_popcount(x.w) + __builtin_popcount(y.x) + __builtin_popcount(y.y) +
+                   __builtin_popcount(y.z) + __builtin_popcount(y.w);
+    Ops o;
+    o.init = valid ? (float)((pc + 256) * 16384 + j) : kMxNone;
+    // dwords g and 4 + g of the row (zero past the train set: B = 0, the
+    // accumulator keeps kMxNone)
+    uint32_t w0 = g == 0 ? x.x : g == 1 ? x.y : g == 2 ? x.z : x.w;
+    uint32_t w1 = g == 0 ? y.x : g == 1 ? y.y : g == 2 ? y.z : y.w;
+    w0 = valid ? w0 : 0u;
+    w1 = valid ? w1 : 0u;
+    o.B0 = mx_v8i{0, 0, 0, 0, 0, 0, 0, 0};
+    o.B1 = o.B0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      o.B0[d] = (int)lut[1][(w0 >> (8 * d)) & 255u];
+      o.B1[d] = (int)lut[1][(w1 >> (8 * d)) & 255u];
+    }
+    return o;
+  };
+  // all first halves, then all second halves (independent accumulators
+  // between the dependent pairs)
+  auto issue = [&](const Ops& o, mx_v4f (&acc)[kMxQB]) {
+#pragma unroll
+    for (int b = 0; b < kMxQB; ++b) {
+      acc[b] = mx_v4f{o.init, o.init, o.init, o.init};
+      acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[b][0], o.B0, acc[b], 4, 4, 0, 127, 0, 141);
+    }
+#pragma unroll
+    for (int b = 0; b < kMxQB; ++b)
+      acc[b] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(A[b][1], o.B1, acc[b], 4, 4, 0, 127, 0, 141);
+  };
+  // the keys are non-negative floats: their bit patterns order as unsigned
+  // integers (v_min_u32 / v_med3_u32, no NaN canonicalisation)
+  auto fold = [&](const mx_v4f (&acc)[kMxQB]) {
+#pragma unroll
+    for (int b = 0; b < kMxQB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t key = __float_as_uint(acc[b][i]);
+        k2[b][i] = umed3(k1[b][i], k2[b][i], key);
+        k1[b][i] = min(k1[b][i], key);
+      }
+  };
+#pragma unroll
+  for (int a = 0; a < kMxAhead; ++a) ld(a, ra[a]);
+  mx_v4f accA[kMxQB], accB[kMxQB];
+  if (nmine > 0) {
+    Ops o = form(0);
+    issue(o, accA);
+    int s = 1;
+    for (; s + 1 < nmine; s += 2) {
+      o = form(s);
+      issue(o, accB);
+      fold(accA);
+      o = form(s + 1);
+      issue(o, accA);
+      fold(accB);
+    }
+    if (s < nmine) {
+      o = form(s);
+      issue(o, accB);
+      fold(accA);
+      fold(accB);
+    } else {
+      fold(accA);
+    }
+  }
+  // merge the 16 column-lanes of each query row (lanes 16 g .. 16 g + 15)
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int b = 0; b < kMxQB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        merge2(k1[b][i], k2[b][i], __shfl_xor(k1[b][i], off, kWave), __shfl_xor(k2[b][i], off, kWave));
+  // lane (g, r < 4) holds query 16 b + 4 g + r of this wave's partial
+  if (r < 4) {
+#pragma unroll
+    for (int b = 0; b < kMxQB; ++b) {
+      uint32_t m1 = k1[b][0], m2 = k2[b][0];
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {
+        m1 = r == i ? k1[b][i] : m1;
+        m2 = r == i ? k2[b][i] : m2;
+      }
+      part[wid][16 * b + 4 * g + r][0] = m1;
+      part[wid][16 * b + 4 * g + r][1] = m2;
+    }
+  }
+  __syncthreads();
+  const int ql = threadIdx.x;  // one thread per query of the workgroup
+  if (ql >= kMxQWG) return;
+  const int qi = q0 + ql;
+  if (qi >= nq) return;
+  uint32_t b1 = part[0][ql][0], b2 = part[0][ql][1];
+#pragma unroll
+  for (int w = 1; w < kMxWaves; ++w) merge2(b1, b2, part[w][ql][0], part[w][ql][1]);
+  const float m1 = __uint_as_float(b1), m2 = __uint_as_float(b2);
+  int pq = 0;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) pq += __builtin_popcount(qb[(size_t)qi * 8 + w]);
+  const bool h1 = m1 < kMxNone, h2 = m2 < kMxNone;
+  const uint32_t u1 = (uint32_t)m1, u2 = (uint32_t)m2;
+  int2 id, ds;
+  id.x = h1 ? (int)(u1 & 16383u) : -1;
+  ds.x = h1 ? (int)(u1 >> 14) - 256 + pq : -1;
+  id.y = h2 ? (int)(u2 & 16383u) : -1;
+  ds.y = h2 ? (int)(u2 >> 14) - 256 + pq : -1;
+  const size_t o = (size_t)item * q_cap + qi;
+  idx2[o] = id;
+  dist2[o] = ds;
+  good[o] = (h2 && 10 * ds.x < 7 * ds.y) ? 1 : 0;
+}
+
 // One workgroup per batch item: order-preserving compaction of good rows.
 constexpr int kCWG = 1024;
 
@@ -220,6 +456,17 @@ extern "C" int slam_hamming_knn2(const uint8_t* d_q, const int32_t* d_nq, int q_
                "slam_hamming_knn2: null pointer");
   SLAM_REQUIRE(((uintptr_t)d_q & 15) == 0 && ((uintptr_t)d_t & 15) == 0,
                "slam_hamming_knn2: descriptor buffers must be 16-byte aligned");
+  if (t_cap <= 16383 && !g_knn2_valu) {  // matrix-core form (train index in 14 bits)
+    const int tiles = (q_cap + kMxQWG - 1) / kMxQWG;
+    const long long grid = (long long)tiles * batch;
+    SLAM_REQUIRE(grid < (1ll << 31), "slam_hamming_knn2: grid too large");
+    knn2_mx_kernel<<<dim3((unsigned)grid), dim3(kMxWG), 0, slam::as_stream(stream)>>>(
+        reinterpret_cast<const uint32_t*>(d_q), d_nq, q_cap, reinterpret_cast<const uint32_t*>(d_t),
+        d_nt, t_cap, tiles, reinterpret_cast<int2*>(d_idx2), reinterpret_cast<int2*>(d_dist2),
+        d_good);
+    SLAM_LAUNCHED("knn2_mx_kernel");
+    return SLAM_OK;
+  }
   const int tiles = (q_cap + kQPerWG - 1) / kQPerWG;
   const long long grid = (long long)tiles * batch;
   SLAM_REQUIRE(grid < (1ll << 31), "slam_hamming_knn2: grid too large");
@@ -229,6 +476,12 @@ extern "C" int slam_hamming_knn2(const uint8_t* d_q, const int32_t* d_nq, int q_
       d_good);
   SLAM_LAUNCHED("knn2_kernel");
   return SLAM_OK;
+}
+
+extern "C" int slam_hamming_force_valu(int valu) {
+  const int prev = g_knn2_valu;
+  g_knn2_valu = valu != 0;
+  return prev;
 }
 
 extern "C" int slam_compact_matches(const int32_t* d_idx2, const uint8_t* d_good,

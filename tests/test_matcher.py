@@ -125,6 +125,38 @@ def test_gpu_knn2_max_train_and_chunk_boundaries():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("valu", [0, 1])
+def test_gpu_knn2_matrix_core_and_valu_kernels_bit_exact(valu):
+    """slam_hamming_knn2's fp4 matrix-core kernel (t_cap <= 16383) and the
+    integer-VALU kernel (forced) against the oracle: train sets at the 16-row
+    step boundaries, empty / single rows, the 14-bit index limit, duplicated
+    rows (distance ties broken by the lower train index) and all-equal sets."""
+    import torch
+    from slam355 import _lib, matcher
+
+    rng = np.random.default_rng(23)
+    prev = _lib.lib.slam_hamming_force_valu(valu)
+    try:
+        cases = [(70, 0), (70, 1), (65, 2), (64, 15), (64, 16), (63, 17), (257, 33),
+                 (129, 16383), (2087, 2087)]
+        for nq, nt in cases:
+            qq, tt = _sets(rng, nq, nt, dup=min(nt, 40))
+            if nt >= 8:
+                tt[nt // 2: nt // 2 + 4] = tt[1]  # exact duplicate rows: tied distances
+            i2, d2, g = matcher.knn2(qq, tt)
+            ei2, ed2, eg = oracle.hamming_knn2(qq, tt)
+            assert np.array_equal(i2, ei2) and np.array_equal(d2, ed2), (valu, nq, nt)
+            assert np.array_equal(g, eg), (valu, nq, nt)
+        same = np.full((33, 32), 0xA5, np.uint8)  # every distance 0 (or equal): all ties
+        i2, d2, g = matcher.knn2(same[:17], same)
+        ei2, ed2, eg = oracle.hamming_knn2(same[:17], same)
+        assert np.array_equal(i2, ei2) and np.array_equal(d2, ed2) and np.array_equal(g, eg)
+    finally:
+        _lib.lib.slam_hamming_force_valu(prev)
+        torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
 def test_gpu_compact_matches_order_and_gate():
     import torch
     from slam355 import matcher
