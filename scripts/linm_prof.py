@@ -1,5 +1,8 @@
-"""Phase split of k_lin_mfma per workgroup (library built by build_linm_prof.sh):
-staging loads, projections (A), points (B), W/Y (C), MFMA + U (D), write-out (E)."""
+"""Phase split of k_lin_mfma per workgroup (library built by build_linm_prof.sh),
+shader cycles summed over the workgroup's chunks: staging + load wait, projections
+(A), points (B), W/Y (C), MFMA + U (D), write-out (E).
+
+    python scripts/linm_prof.py N_WINDOWS CHUNKS_PER_WG"""
 import ctypes
 import os
 import sys
@@ -26,7 +29,7 @@ for _ in range(nb):
 bat = BABatch(probs)
 fn = _lib.lib.slam_linm_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-names = ["loads", "A proj", "B points", "C W/Y", "D mfma+U", "E write"]
+names = ["staging+wait", "A proj", "B points", "C W/Y", "D mfma+U", "E write"]
 for it in range(5):
     bat.iterate(1)
     torch.cuda.synchronize()
@@ -35,9 +38,9 @@ for it in range(5):
     fn(buf, 4096)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(4096, 8).astype(np.int64)
     rows = np.concatenate([a[1024 * y:1024 * y + n] for y in range(nb)])
-    d = np.diff(rows[:, :7], axis=1)
-    span = rows[:, 6].max() - rows[:, 0].min()
-    st = rows[:, 0] - rows[:, 0].min()
-    print(f"iter {it}: WGs {len(rows)} span {span} clk; start spread {st.max()} clk; per-WG total "
-          f"median {np.median(rows[:, 6] - rows[:, 0]):.0f}")
-    print("   " + "  ".join(f"{nm} {np.median(d[:, k]):.0f}/{d[:, k].max()}" for k, nm in enumerate(names)))
+    d = rows[:, 1:7]  # per-phase shader cycles summed over the workgroup's chunks
+    tot = d.sum(1)
+    print(f"iter {it}: WGs {len(rows)} ({cpw} chunks/WG); per-WG total median {np.median(tot):.0f} "
+          f"max {tot.max()} clk")
+    print("   " + "  ".join(f"{nm} {np.median(d[:, k]):.0f} ({100 * np.median(d[:, k]) / np.median(tot):.0f}%)"
+                            for k, nm in enumerate(names)))

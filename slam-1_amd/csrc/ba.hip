@@ -565,22 +565,38 @@ static_assert(sizeof(MLds) <= 80 * 1024, "k_lin_mfma: two workgroups per CU");
 static_assert(9 * kMCams <= kMRows, "k_lin_mfma: 9m rows in 4 tile rows");
 static_assert(2 * kMPts * 3 * kMRows >= kMRows * kMRows + kMCams * 256, "staging aliases yt/wt");
 
+// -DSLAM_LINM_PROFILE: shader cycles per phase, summed over the workgroup's
+// chunks (thread 0, s_memtime): 1 staging (incl. the wait for the prefetched
+// loads), 2 projections (A), 3 points (B), 4 W/Y (C), 5 MFMA + U (D),
+// 6 write-out (E); slam_linm_stamps reads them (scripts/linm_prof.py).
 #ifdef SLAM_LINM_PROFILE
 __device__ unsigned long long g_linm_stamp[4096][8];
-#define LINM_T(i)                                                                   \
-  do {                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x + 1024 * blockIdx.y < 4096)                  \
-      g_linm_stamp[blockIdx.x + 1024 * blockIdx.y][i] = __builtin_amdgcn_s_memtime(); \
+#define LINM_DECL() unsigned long long linm_prev = __builtin_amdgcn_s_memtime(), linm_acc[7] = {0, 0, 0, 0, 0, 0, 0}
+#define LINM_T(i)                                                  \
+  do {                                                             \
+    if (threadIdx.x == 0) {                                        \
+      const unsigned long long linm_now = __builtin_amdgcn_s_memtime(); \
+      linm_acc[i] += linm_now - linm_prev;                         \
+      linm_prev = linm_now;                                        \
+    }                                                              \
+  } while (0)
+#define LINM_END()                                                               \
+  do {                                                                           \
+    if (threadIdx.x == 0 && blockIdx.x + 1024 * blockIdx.y < 4096)               \
+      for (int linm_i = 0; linm_i < 7; ++linm_i)                                 \
+        g_linm_stamp[blockIdx.x + 1024 * blockIdx.y][linm_i] = linm_acc[linm_i]; \
   } while (0)
 #else
+#define LINM_DECL() (void)0
 #define LINM_T(i) (void)0
+#define LINM_END() (void)0
 #endif
 
 __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   BA_PROB(bat);
   const int sg = blockIdx.x;
   if (sg >= p.n_sgrps) return;  // batch: grid.x covers the largest problem
-  LINM_T(0);
+  LINM_DECL();
   lm_wave_priority();
   __shared__ MLds L;
   const int t = threadIdx.x, lane = t & 63;
@@ -872,11 +888,11 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     }
     p0 = np0; p1 = np1; o0 = no0; o1 = no1;
     np0 = nnp0; np1 = nnp1; no0 = nno0; no1 = nno1;
+    LINM_T(5);
   }
   // (E) T and the Z_a tiles -> LDS staging (aliases the operand planes), then
   //     the partial rows
   __syncthreads();
-  LINM_T(5);
   double* T = &L.yt[0][0][0];
   double* Z = T + kMRows * kMRows;  // [kMCams][16][16]
 #pragma unroll
@@ -921,6 +937,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     p.bpart[(size_t)L.brow[pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
   }
   LINM_T(6);
+  LINM_END();
 }
 
 // Column sums of the n-wide rows [rb, re) of part (row stride `stride`): the
