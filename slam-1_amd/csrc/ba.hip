@@ -647,7 +647,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   for (int s = 0; s < 3; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int s = 0; s < 2; ++s) zacc[s] = d4{0.0, 0.0, 0.0, 0.0};
-  const int mi = lane & 15, mk = lane >> 4, mkc = mk < 3 ? mk : 2;
+  const int mi = lane & 15, mk = lane >> 4;
 
   // chunk extents: the first from the record, the next loaded one chunk ahead;
   // a chunk's inputs are loaded one chunk ahead too (issued after the current
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     // a point is not seen by, rows >= 9m)
     for (int i = t; i < npts * 3 * 16 * nt; i += kMWG) {
       const int row = i % (16 * nt), pk = i / (16 * nt);
-      const int pos = (row + 16 * (pk % 3)) & (kMRows - 1);  // plane rotation, see (D)
+      const int pos = (row + 16 * (pk & 3)) & (kMRows - 1);  // plane rotation, see (D)
       (&L.yt[0][0][0])[pk * kMRows + pos] = 0.0;
       (&L.wt[0][0][0])[pk * kMRows + pos] = 0.0;
     }
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
           const int row = 9 * a + ib + i;
 #pragma unroll
           for (int c = 0; c < 3; ++c) {
-            const int pos = (row + 16 * c) & (kMRows - 1);
+            const int pos = (row + 16 * ((3 * lp + c) & 3)) & (kMRows - 1);  // see (D)
             L.wt[lp][c][pos] = W[i][c];
             L.yt[lp][c][pos] = W[i][0] * V[0][c] + W[i][1] * V[1][c] + W[i][2] * V[2][c];
           }
@@ -817,34 +817,42 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     }
     __syncthreads();
     LINM_T(4);
-    // (D) T += Y_p W_p^T, one MFMA per point and tile (operand plane k stores
-    //     row r at (r + 16k) mod 64, so the 16-lane groups k = 0, 1 of an
-    //     operand read fall on different LDS banks -- a 64-double k stride
-    //     would put them on the same ones):
-    //     A[i][k] = Y_p[16I + i][k], B[k][j] = W_p[16J + j][k], k = 3 -> 0.
-    //     Every wave issues 3 tile MFMAs per point (a wave with 2 tiles feeds
+    // (D) T += sum_p Y_p W_p^T as ONE product over the flat index kk = 3 lp + c
+    //     (point lp, coordinate c): K-step s of an MFMA takes kk = 4 s + k
+    //     (k = lane >> 4), so the 3 coordinates of consecutive points pack the
+    //     K = 4 steps densely -- ceil(3 npts / 4) MFMAs per tile instead of one
+    //     per point with K padded 3 -> 4 (-25 %).  Plane kk stores row r at
+    //     (r + 16 (kk & 3)) mod 64, so the lane groups k = 0, 1 of an operand
+    //     read fall on different LDS banks:
+    //     A[i][k] = Y[16I + i][kk], B[k][j] = W[16J + j][kk], kk >= 3 npts -> 0.
+    //     Every wave issues 3 tile MFMAs per K-step (a wave with 2 tiles feeds
     //     its third accumulator zeros), so the accumulators stay in their own
-    //     AGPRs with no control flow around the MFMAs; operands of 4 points are
-    //     loaded before their MFMAs are issued (points past npts: zeros).
-    for (int lp0 = 0; lp0 < npts; lp0 += 4) {
-      double av[4][3], bv[4][3];
+    //     AGPRs with no control flow around the MFMAs; operands of 4 K-steps
+    //     are loaded before their MFMAs are issued.
+    {
+      const double* Yf = &L.yt[0][0][0];
+      const double* Wf = &L.wt[0][0][0];
+      const int nk = 3 * npts;
+      for (int k0 = 0; k0 < nk; k0 += 16) {
+        double av[4][3], bv[4][3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int lp = min(lp0 + u, kMPts - 1);
+        for (int u = 0; u < 4; ++u) {
+          const int kk = min(k0 + 4 * u + mk, 3 * kMPts - 1);
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          av[u][s] = L.yt[lp][mkc][(tRow[s] + 16 * mkc) & (kMRows - 1)];
-          bv[u][s] = L.wt[lp][mkc][(tCol[s] + 16 * mkc) & (kMRows - 1)];
+          for (int s = 0; s < 3; ++s) {
+            av[u][s] = Yf[kk * kMRows + ((tRow[s] + 16 * mk) & (kMRows - 1))];
+            bv[u][s] = Wf[kk * kMRows + ((tCol[s] + 16 * mk) & (kMRows - 1))];
+          }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool on = mk < 3 && lp0 + u < npts;
+        for (int u = 0; u < 4; ++u) {
+          const bool on = k0 + 4 * u + mk < nk;
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          const bool o = on && s < ntl;
-          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(o ? av[u][s] : 0.0, o ? bv[u][s] : 0.0,
-                                                       acc[s], 0, 0, 0);
+          for (int s = 0; s < 3; ++s) {
+            const bool o = on && s < ntl;
+            acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(o ? av[u][s] : 0.0, o ? bv[u][s] : 0.0,
+                                                         acc[s], 0, 0, 0);
+          }
         }
       }
     }

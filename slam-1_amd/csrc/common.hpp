@@ -57,5 +57,5 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int M>
 __device__ __forceinline__ double bcast16(double v) {
   static_assert(M >= 0 && M < 16, "row lane");
-  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + M, 0xf, 0xf, false);
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + M, 0xf, 0xf, true);
 }
