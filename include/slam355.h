@@ -335,7 +335,6 @@ typedef struct slam_ba_problem {
   const int32_t* cslot_row;     /* [n_cslots] row of a camera slot in cpart (camera-major, group order) */
   const int32_t* blk_bslot_ptr; /* [n_blocks+1] block -> its rows of bpart (empty: no common point) */
   const int32_t* bslot_row;     /* [n_bslots] row of a block slot in bpart (block-major, group order) */
-  double* ptdata;               /* [P][16] e(3) g(3) diagV(3) V*^-1(6) -       */
   double* cpart;                /* [n_cslots][112] U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2 */
   double* bpart;                /* [n_bslots][81] sum Y W^T                    */
   double* sys;                  /* S (dense or packed blocks) b[9C] g[9C] diagU[9C] cost[C] */

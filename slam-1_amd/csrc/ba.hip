@@ -278,7 +278,41 @@ __host__ __device__ __forceinline__ long long sys_vec_off(int n_cams, int n_bloc
   return sys_packed(n_cams) ? 81ll * n_blocks : 81ll * n_cams * n_cams;
 }
 
-constexpr int kPtData = 16;  // per point: e(3) g(3) diagV(3) V*^-1(6) pad
+
+// Per point: V = sum Jp^T Jp and g = -sum Jp^T r over its observations, in
+// observation order (pt_acc per observation row), then V* = V + lam diag(V)
+// (diag clamped), V*^-1 by cofactors and e = V*^-1 g (pt_schur).  The
+// linearisers and k_back_trial run the same operations in the same order, so
+// the back substitution sees bit-identical V*^-1, e, g, diag.
+struct PtSchur {
+  double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+  double d[3], iv[6], e[3];
+  __device__ __forceinline__ void acc(double j0, double j1, double j2, double rr) {
+    V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
+    V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
+    g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
+  }
+  __device__ __forceinline__ void solve(double lam);
+};
+__device__ __forceinline__ void PtSchur::solve(double lam) {
+  d[0] = clampd(V00); d[1] = clampd(V11); d[2] = clampd(V22);
+  const double a00 = V00 + lam * d[0], a11 = V11 + lam * d[1], a22 = V22 + lam * d[2];
+  const double a01 = V01, a02 = V02, a12 = V12;
+  const double c00 = a11 * a22 - a12 * a12;
+  const double c01 = a02 * a12 - a01 * a22;
+  const double c02 = a01 * a12 - a02 * a11;
+  const double c11 = a00 * a22 - a02 * a02;
+  const double c12 = a01 * a02 - a00 * a12;
+  const double c22 = a00 * a11 - a01 * a01;
+  const double det = a00 * c00 + a01 * c01 + a02 * c02;
+  const double id = det != 0.0 ? 1.0 / det : 0.0;
+  iv[0] = c00 * id; iv[1] = c01 * id; iv[2] = c02 * id;
+  iv[3] = c11 * id; iv[4] = c12 * id; iv[5] = c22 * id;
+  e[0] = iv[0] * g0 + iv[1] * g1 + iv[2] * g2;
+  e[1] = iv[1] * g0 + iv[3] * g1 + iv[4] * g2;
+  e[2] = iv[2] * g0 + iv[4] * g1 + iv[5] * g2;
+}
+
 constexpr int kCPart = 112;  // per camera slot: U - sum Y W^T (81), Jc^T r, Jc^T u, diag U (9 each), |r|^2, pad
 // Point groups: a workgroup owns the contiguous observation range of a group
 // of whole points (observations are sorted by point), at most kGrp of them.
@@ -445,42 +479,16 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
   const double lam = p.state[SLAM_BA_ST_LAMBDA];
   if (t < p1 - p0) {
     const int pt = p0 + t;
-    double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+    PtSchur ps;
     for (int k = p.pt_ptr[pt] - o0; k < p.pt_ptr[pt + 1] - o0; ++k) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const double j0 = L.w[k][3 * a], j1 = L.w[k][3 * a + 1], j2 = L.w[k][3 * a + 2];
-        const double rr = L.w[k][6 + a];
-        V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
-        V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
-        g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
-      }
+      for (int a = 0; a < 2; ++a) ps.acc(L.w[k][3 * a], L.w[k][3 * a + 1], L.w[k][3 * a + 2], L.w[k][6 + a]);
     }
-    const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
-    const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
-    const double a01 = V01, a02 = V02, a12 = V12;
-    const double c00 = a11 * a22 - a12 * a12;
-    const double c01 = a02 * a12 - a01 * a22;
-    const double c02 = a01 * a12 - a02 * a11;
-    const double c11 = a00 * a22 - a02 * a02;
-    const double c12 = a01 * a02 - a00 * a12;
-    const double c22 = a00 * a11 - a01 * a01;
-    const double det = a00 * c00 + a01 * c01 + a02 * c02;
-    const double id = det != 0.0 ? 1.0 / det : 0.0;
-    const double iv[6] = {c00 * id, c01 * id, c02 * id, c11 * id, c12 * id, c22 * id};
-    const double e0 = iv[0] * g0 + iv[1] * g1 + iv[2] * g2;
-    const double e1 = iv[1] * g0 + iv[3] * g1 + iv[4] * g2;
-    const double e2 = iv[2] * g0 + iv[4] * g1 + iv[5] * g2;
-    double* pd = p.ptdata + (size_t)pt * kPtData;
-    pd[0] = e0; pd[1] = e1; pd[2] = e2;
-    pd[3] = g0; pd[4] = g1; pd[5] = g2;
-    pd[6] = d0; pd[7] = d1; pd[8] = d2;
-    L.pt[t][0] = e0; L.pt[t][1] = e1; L.pt[t][2] = e2;
+    ps.solve(lam);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      pd[9 + k] = iv[k];
-      L.pt[t][3 + k] = iv[k];
-    }
+    for (int k = 0; k < 3; ++k) L.pt[t][k] = ps.e[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) L.pt[t][3 + k] = ps.iv[k];
   }
   __syncthreads();
   if (has) {
@@ -533,7 +541,7 @@ __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
 // accumulated in registers across the supergroup's chunks and written once:
 // per camera a one cpart row (U_a - T_aa, Jc^T r, Jc^T u, diag U, |r|^2), per
 // co-observed camera pair a < b one bpart row (T_ab) -- the rows k_assemble
-// sums.  Per point: V, g, V*, V*^-1, e as k_linearize (ptdata).
+// sums.  Per point: V, g, V*, V*^-1, e (PtSchur, as k_linearize; LDS only).
 constexpr int kMObs = 120, kMPts = 16, kMCams = 7, kMRows = 64;
 constexpr int kMWG = 256;
 constexpr int kSgMeta = 24;  // sg_meta record: ch0 ch1 cs0 m bs0 nb p0 p1 o0 o1 cams[8] pad
@@ -730,43 +738,16 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     LINM_T(2);
     // (B) per point: V, g, V* = V + lam diag(V), V*^-1 (cofactors), e = V*^-1 g
     if (t < npts) {
-      const int pt = p0 + t;
-      double V00 = 0, V01 = 0, V02 = 0, V11 = 0, V12 = 0, V22 = 0, g0 = 0, g1 = 0, g2 = 0;
+      PtSchur ps;
       for (int k = L.optr[t]; k < L.optr[t + 1]; ++k) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const double j0 = L.jp[3 * a][k], j1 = L.jp[3 * a + 1][k], j2 = L.jp[3 * a + 2][k];
-          const double rr = L.ru[a][k];
-          V00 += j0 * j0; V01 += j0 * j1; V02 += j0 * j2;
-          V11 += j1 * j1; V12 += j1 * j2; V22 += j2 * j2;
-          g0 -= j0 * rr; g1 -= j1 * rr; g2 -= j2 * rr;
-        }
+        for (int a = 0; a < 2; ++a) ps.acc(L.jp[3 * a][k], L.jp[3 * a + 1][k], L.jp[3 * a + 2][k], L.ru[a][k]);
       }
-      const double d0 = clampd(V00), d1 = clampd(V11), d2 = clampd(V22);
-      const double a00 = V00 + lam * d0, a11 = V11 + lam * d1, a22 = V22 + lam * d2;
-      const double a01 = V01, a02 = V02, a12 = V12;
-      const double c00 = a11 * a22 - a12 * a12;
-      const double c01 = a02 * a12 - a01 * a22;
-      const double c02 = a01 * a12 - a02 * a11;
-      const double c11 = a00 * a22 - a02 * a02;
-      const double c12 = a01 * a02 - a00 * a12;
-      const double c22 = a00 * a11 - a01 * a01;
-      const double det = a00 * c00 + a01 * c01 + a02 * c02;
-      const double id = det != 0.0 ? 1.0 / det : 0.0;
-      const double iv[6] = {c00 * id, c01 * id, c02 * id, c11 * id, c12 * id, c22 * id};
-      const double e0 = iv[0] * g0 + iv[1] * g1 + iv[2] * g2;
-      const double e1 = iv[1] * g0 + iv[3] * g1 + iv[4] * g2;
-      const double e2 = iv[2] * g0 + iv[4] * g1 + iv[5] * g2;
-      double* pd = p.ptdata + (size_t)pt * kPtData;
-      pd[0] = e0; pd[1] = e1; pd[2] = e2;
-      pd[3] = g0; pd[4] = g1; pd[5] = g2;
-      pd[6] = d0; pd[7] = d1; pd[8] = d2;
-      L.e[t][0] = e0; L.e[t][1] = e1; L.e[t][2] = e2;
+      ps.solve(lam);
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        pd[9 + k] = iv[k];
-        L.vi[t][k] = iv[k];
-      }
+      for (int k = 0; k < 3; ++k) L.e[t][k] = ps.e[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) L.vi[t][k] = ps.iv[k];
     }
     __syncthreads();
     LINM_T(3);
@@ -2445,8 +2426,12 @@ static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
 __device__ void lm_decide(double* __restrict__ state, const double* __restrict__ small);
 
 // Back substitution + trial cost, one workgroup per point group:
-//   per observation: dy_o = Y_o^T dc_cam(o) = V*^-1 W_o^T dc         (-> LDS)
-//   per point: dp = e - sum_o dy_o, trial point x + dp, predicted-reduction term
+//   per observation: Jacobian at the live parameters (the one the lineariser
+//     used), Jp and r -> LDS, w_o = W_o^T dc = Jp^T (Jc dc_cam(o))   (-> LDS)
+//   per point: V, g, diag, V*^-1, e re-derived in the lineariser's operation
+//     order (PtSchur: bit-identical to what it used -- no per-point record
+//     written by the lineariser and read back here), dp = e - sum_o V*^-1 w_o,
+//     trial point x + dp, predicted-reduction term
 //   per observation: trial residual at (cams[next], trial point)   (-> |r|^2)
 // Workgroup partial sums go to part[g] (cost) and part[G + g] (pred) as sc1
 // stores; the last workgroup to finish (agent-scope ticket) sums them in a
@@ -2459,7 +2444,7 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
   if (g >= G) return;  // batch: grid.x covers the largest problem (not in the ticket count)
   double* __restrict__ part = p.red_part;
   lm_wave_priority();
-  __shared__ double sdy[kGrp][3];
+  __shared__ double sjp[6][kGrp + 1], sr[2][kGrp + 1], sw[3][kGrp + 1];  // [value][obs]
   __shared__ double snp[kGrp][3];
   __shared__ double red[kGrp / 64];
   __shared__ int last;
@@ -2473,20 +2458,15 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
   const bool fail = p.state[SLAM_BA_ST_CHOL_FAIL] != 0.0;
   // the point lanes' inputs, loaded before the observation phase
   const bool ptl = t < p1 - p0;
-  double pdv[9], xv[3];
+  double xv[3];
   int kb = 0, ke = 0;
   if (ptl) {
-    const double* pd = p.ptdata + (size_t)(p0 + t) * kPtData;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) pdv[k] = pd[k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) xv[k] = p.pts[cur][3 * (p0 + t) + k];
     kb = p.pt_ptr[p0 + t] - o0;
     ke = p.pt_ptr[p0 + t + 1] - o0;
   }
   if (has) {
-    // dy_o = Y_o^T dc = V*^-1 (W_o^T dc), W_o = Jc^T Jp re-derived from the
-    // Jacobian at the live parameters (the one k_linearize used)
     double r[2], J[2][12];
     const int pt = p.obs_pt[o];
     reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
@@ -2501,30 +2481,42 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
       w1 += (J[0][i] * J[0][10] + J[1][i] * J[1][10]) * c;
       w2 += (J[0][i] * J[0][11] + J[1][i] * J[1][11]) * c;
     }
-    const double* vi = p.ptdata + (size_t)pt * kPtData + 9;
-    sdy[t][0] = vi[0] * w0 + vi[1] * w1 + vi[2] * w2;
-    sdy[t][1] = vi[1] * w0 + vi[3] * w1 + vi[4] * w2;
-    sdy[t][2] = vi[2] * w0 + vi[4] * w1 + vi[5] * w2;
+    sw[0][t] = w0;
+    sw[1][t] = w1;
+    sw[2][t] = w2;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) sjp[3 * a + c][t] = J[a][9 + c];
+      sr[a][t] = r[a];
+    }
   }
   __syncthreads();
   double pred = 0.0;
   if (ptl) {
     const int pt = p0 + t;
     const double lam = p.state[SLAM_BA_ST_LAMBDA];
-    const double* pd = pdv;
-    double d0 = pd[0], d1 = pd[1], d2 = pd[2];
+    PtSchur ps;
     for (int k = kb; k < ke; ++k) {
-      d0 -= sdy[k][0];
-      d1 -= sdy[k][1];
-      d2 -= sdy[k][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) ps.acc(sjp[3 * a][k], sjp[3 * a + 1][k], sjp[3 * a + 2][k], sr[a][k]);
+    }
+    ps.solve(lam);
+    const double* iv = ps.iv;
+    double d0 = ps.e[0], d1 = ps.e[1], d2 = ps.e[2];
+    for (int k = kb; k < ke; ++k) {
+      const double w0 = sw[0][k], w1 = sw[1][k], w2 = sw[2][k];
+      d0 -= iv[0] * w0 + iv[1] * w1 + iv[2] * w2;
+      d1 -= iv[1] * w0 + iv[3] * w1 + iv[4] * w2;
+      d2 -= iv[2] * w0 + iv[4] * w1 + iv[5] * w2;
     }
     const double* x = xv;
     double* xn = p.pts[1 - cur] + 3 * pt;
     snp[t][0] = xn[0] = x[0] + d0;
     snp[t][1] = xn[1] = x[1] + d1;
     snp[t][2] = xn[2] = x[2] + d2;
-    pred = d0 * (lam * pd[6] * d0 + pd[3]) + d1 * (lam * pd[7] * d1 + pd[4]) +
-           d2 * (lam * pd[8] * d2 + pd[5]);
+    pred = d0 * (lam * ps.d[0] * d0 + ps.g0) + d1 * (lam * ps.d[1] * d1 + ps.g1) +
+           d2 * (lam * ps.d[2] * d2 + ps.g2);
     if (fail) pred = 0.0;
   }
   __syncthreads();
@@ -2612,7 +2604,7 @@ inline int nblk(int n, int bs) { return (n + bs - 1) / bs; }
 int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(p != nullptr, "slam_ba: null problem");
   SLAM_REQUIRE(p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "slam_ba: bad sizes");
-  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->camrec[0] && p->camrec[1] && p->ptdata &&
+  SLAM_REQUIRE(p->cams[0] && p->cams[1] && p->camrec[0] && p->camrec[1] &&
                    p->cpart && p->bpart && p->grp_ptr && p->grp_cslot && p->grp_bslot &&
                    p->cslot_obs_ptr && p->bslot_pair_ptr && p->cam_cslot_ptr && p->cslot_row && p->bslot_row &&
                    p->blk_bslot_ptr && p->blocks && p->ticket && p->sys && p->state &&

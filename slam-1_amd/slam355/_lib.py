@@ -35,7 +35,7 @@ class BAProblemStruct(ctypes.Structure):
         ("grp_cslot", c_p), ("cslot_cam", c_p), ("cslot_obs_ptr", c_p), ("cslot_obs", c_p),
         ("grp_bslot", c_p), ("bslot_blk", c_p), ("bslot_pair_ptr", c_p), ("bslot_pairs", c_p),
         ("blocks", c_p), ("cam_cslot_ptr", c_p), ("cslot_row", c_p), ("blk_bslot_ptr", c_p),
-        ("bslot_row", c_p), ("ptdata", c_p), ("cpart", c_p), ("bpart", c_p),
+        ("bslot_row", c_p), ("cpart", c_p), ("bpart", c_p),
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
         ("state", c_p), ("ticket", c_p),
         ("sg_ptr", c_p), ("sg_meta", c_p), ("obs_meta", c_p), ("chk_optr", c_p), ("chk_cptr", c_p),

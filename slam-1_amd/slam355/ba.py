@@ -681,7 +681,6 @@ class BAProblem:
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
         C9 = 9 * C
         n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])
-        t["ptdata"] = z(P * 16)
         t["cpart"] = z(n_cs * 112)
         t["bpart"] = z(n_bs * 81)
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
@@ -706,7 +705,7 @@ class BAProblem:
         s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
         s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
         s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
-        for k in _INDEX_TABLES + ("obs_q", "ptdata", "cpart", "bpart", "sys", "chol", "delta_c",
+        for k in _INDEX_TABLES + ("obs_q", "cpart", "bpart", "sys", "chol", "delta_c",
                                   "red_part", "small", "state", "ticket") + \
                 (_MFMA_TABLES if pl["mode"] == 1 else ()):
             setattr(s, k, t[k].data_ptr())
