@@ -11,7 +11,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "slam-1_amd")]
-os.environ["SLAM355_LIB"] = os.path.join(ROOT, "slam-1_amd", "prof", "libslam355_linm.so")
+os.environ.setdefault("SLAM355_LIB", os.path.join(ROOT, "slam-1_amd", "prof", "libslam355_linm.so"))
 
 import torch  # noqa: E402
 from slam355 import _lib  # noqa: E402
