@@ -221,6 +221,99 @@ __device__ __forceinline__ void clamp_rows(double r[2], double J[2][12]) {
   }
 }
 
+// reproject_pre<true> + clamp_rows<true> split over two lanes by Jacobian
+// columns: H = 0 the rotation / translation columns 0..5, H = 1 the f, k1, k2
+// and point columns 6..11 (Jh[a][k] = J[a][6 H + k]).  Both halves run the
+// forward projection; every value is computed with the same operations in
+// the same order as the one-lane form (the clamp's chain rule is per column).
+template <int H>
+__device__ __forceinline__ void reproject_half(const double* __restrict__ cr,
+                                               const double* __restrict__ X,
+                                               const double* __restrict__ q, double r[2],
+                                               double Jh[2][6]) {
+  const double c = cr[0], s = cr[1], omc = cr[2];
+  const double v0 = cr[3], v1 = cr[4], v2 = cr[5];
+  const double X0 = X[0], X1 = X[1], X2 = X[2];
+  const double dot = X0 * v0 + X1 * v1 + X2 * v2;
+  const double cx0 = v1 * X2 - v2 * X1;
+  const double cx1 = v2 * X0 - v0 * X2;
+  const double cx2 = v0 * X1 - v1 * X0;
+  const double dk = dot * omc;
+  const double RX0 = c * X0 + s * cx0 + dk * v0;
+  const double RX1 = c * X1 + s * cx1 + dk * v1;
+  const double RX2 = c * X2 + s * cx2 + dk * v2;
+  const double P0 = RX0 + cr[26], P1 = RX1 + cr[27], P2 = RX2 + cr[28];
+  const double p0 = -P0 / P2, p1 = -P1 / P2;
+  const double f = cr[29], k1 = cr[30], k2 = cr[31];
+  const double n = p0 * p0 + p1 * p1;
+  const double rad = 1.0 + k1 * n + k2 * (n * n);
+  const double sc = rad * f;
+  r[0] = p0 * sc - q[0];
+  r[1] = p1 * sc - q[1];
+  const double iz = 1.0 / P2;
+  const double dpP[2][3] = {{-iz, 0.0, P0 * iz * iz}, {0.0, -iz, P1 * iz * iz}};
+  const double g2 = 2.0 * f * (k1 + 2.0 * k2 * n);
+  const double Dp[2][2] = {{sc + g2 * p0 * p0, g2 * p0 * p1}, {g2 * p1 * p0, sc + g2 * p1 * p1}};
+  double D[2][3];
+  for (int a = 0; a < 2; ++a)
+    for (int k = 0; k < 3; ++k) D[a][k] = Dp[a][0] * dpP[0][k] + Dp[a][1] * dpP[1][k];
+  if constexpr (H == 0) {
+    double dR[3][3];
+    if (cr[25] != 0.0) {
+      dR[0][0] = 0.0;  dR[0][1] = RX2;  dR[0][2] = -RX1;
+      dR[1][0] = -RX2; dR[1][1] = 0.0;  dR[1][2] = RX0;
+      dR[2][0] = RX1;  dR[2][1] = -RX0; dR[2][2] = 0.0;
+    } else {
+      double R[3][3], A[3][3];
+      for (int i = 0; i < 9; ++i) {
+        R[i / 3][i % 3] = cr[6 + i];
+        A[i / 3][i % 3] = cr[15 + i];
+      }
+      const double Xs[3][3] = {{0.0, -X2, X1}, {X2, 0.0, -X0}, {-X1, X0, 0.0}};
+      double B[3][3];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          B[i][k] = Xs[i][0] * A[0][k] + Xs[i][1] * A[1][k] + Xs[i][2] * A[2][k];
+      const double inv = cr[24];
+      for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k)
+          dR[i][k] = (R[i][0] * B[0][k] + R[i][1] * B[1][k] + R[i][2] * B[2][k]) * inv;
+    }
+    for (int a = 0; a < 2; ++a)
+      for (int k = 0; k < 3; ++k) {
+        Jh[a][k] = D[a][0] * dR[0][k] + D[a][1] * dR[1][k] + D[a][2] * dR[2][k];
+        Jh[a][3 + k] = D[a][k];
+      }
+  } else {
+    double R[3][3];
+    for (int i = 0; i < 9; ++i) R[i / 3][i % 3] = cr[6 + i];
+    const double pp[2] = {p0, p1};
+    for (int a = 0; a < 2; ++a) {
+      Jh[a][0] = pp[a] * rad;
+      Jh[a][1] = pp[a] * (f * n);
+      Jh[a][2] = pp[a] * (f * n * n);
+      for (int k = 0; k < 3; ++k) Jh[a][3 + k] = D[a][0] * R[0][k] + D[a][1] * R[1][k] + D[a][2] * R[2][k];
+    }
+  }
+#pragma unroll
+  for (int comp = 0; comp < 2; ++comp) {  // clamp_rows<true> on this lane's columns
+    const double rc = r[comp];
+    if (fabs(rc) > kClamp) {
+      const double arc = fabs(rc);
+      const double half = comp == 0 ? 613.0 : 185.0;
+      const double a = (half * 2.0) / arc;
+      double Jc[6];
+      for (int k = 0; k < 6; ++k) Jc[k] = Jh[comp][k];
+      for (int row = 0; row < 2; ++row) {
+        const double ratio = r[row] / rc;
+        for (int k = 0; k < 6; ++k) Jh[row][k] = a * (Jh[row][k] - ratio * Jc[k]);
+      }
+      r[0] = r[0] / arc * half * 2.0;
+      r[1] = r[1] / arc * half * 2.0;
+    }
+  }
+}
+
 __device__ __forceinline__ double block_sum(double v, double* lds) {
   // deterministic: fixed shuffle tree then fixed LDS order
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
@@ -667,11 +760,12 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   auto load_in = [&](int ch, int p0, int p1, int o0, int o1) {
     ChunkIn in{0.0, 0.0, 0.0, 0, 0, 0};
     const int nobs = o1 - o0, npts = p1 - p0;
-    if (t < nobs) {
-      in.q0 = p.obs_q[2 * (o0 + t)];
-      in.q1 = p.obs_q[2 * (o0 + t) + 1];
-      in.meta = p.obs_meta[o0 + t];
+    const int ko = t & 127;  // (A) splits an observation over lanes t and t + 128
+    if (ko < nobs) {
+      in.q0 = p.obs_q[2 * (o0 + ko)];
+      in.q1 = p.obs_q[2 * (o0 + ko) + 1];
     }
+    if (t < nobs) in.meta = p.obs_meta[o0 + t];
     if (t < 3 * npts) in.xv = p.pts[cur][3 * p0 + t];
     if (t >= 128 && t - 128 <= npts) in.pp = p.pt_ptr[p0 + t - 128] - o0;
     if (t < 8) in.cp = p.chk_cptr[8 * ch + t];
@@ -725,19 +819,32 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
       }
     }
     LINM_T(1);
-    // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350)
-    if (t < nobs) {
-      const double q[2] = {q0, q1};
-      double r[2], J[2][12];
-      reproject_pre<true>(L.cam[L.la[t]], L.X[L.lpt[t]], q, r, J);
-      clamp_rows<true>(r, J);
+    // (A) per observation: residual + Jacobian (BundleAdjustment.py:317-350),
+    //     split by Jacobian columns over lanes k and k + 128 (all 4 waves busy;
+    //     was lanes 0..119 only)
+    {
+      const int k = t & 127;
+      if (k < nobs) {
+        const double q[2] = {q0, q1};
+        double r[2], Jh[2][6];
+        if (t < 128) {
+          reproject_half<0>(L.cam[L.la[k]], L.X[L.lpt[k]], q, r, Jh);
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
+          for (int a = 0; a < 2; ++a) {
 #pragma unroll
-        for (int i = 0; i < 9; ++i) L.jc[9 * a + i][t] = J[a][i];
+            for (int i = 0; i < 6; ++i) L.jc[9 * a + i][k] = Jh[a][i];
+            L.ru[a][k] = r[a];
+          }
+        } else {
+          reproject_half<1>(L.cam[L.la[k]], L.X[L.lpt[k]], q, r, Jh);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) L.jp[3 * a + c][t] = J[a][9 + c];
-        L.ru[a][t] = r[a];
+          for (int a = 0; a < 2; ++a) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) L.jc[9 * a + 6 + i][k] = Jh[a][i];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) L.jp[3 * a + c][k] = Jh[a][3 + c];
+          }
+        }
       }
     }
     __syncthreads();
