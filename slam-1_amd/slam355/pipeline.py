@@ -87,6 +87,9 @@ class Tracker:
         self.imgs = torch.zeros((2 * B + 1, H, W), **u8)
         # device pose chain (main.py:120-124): (pose, T) carried across batches
         self.chain_state = torch.zeros((32,), **f64)
+        # identity pose + identity stale transform, device-resident: reset_chain
+        # restarts the chain with an async device copy (no host synchronisation)
+        self._chain_eye = torch.from_numpy(np.concatenate([np.eye(4), np.eye(4)]).ravel()).to(d)
         self.reset_chain()
         self.poses = torch.zeros((B, 4, 4), **f64)
         # running minimum of the ORB counts since the last check(): k_orb_compact
@@ -193,9 +196,16 @@ class Tracker:
     def reset_chain(self, pose0=None, T0=None):
         """Start the device pose chain at pose0 (default identity) with T0 as the
         stale transform (default identity)."""
-        st = np.concatenate([np.eye(4) if pose0 is None else np.asarray(pose0, float),
-                             np.eye(4) if T0 is None else np.asarray(T0, float)]).ravel()
-        self.chain_state.copy_(torch.from_numpy(st))
+        if pose0 is None and T0 is None:
+            src = self._chain_eye
+        else:  # a host-built start state (a synchronous upload; not on the bench path)
+            st = np.concatenate([np.eye(4) if pose0 is None else np.asarray(pose0, float),
+                                 np.eye(4) if T0 is None else np.asarray(T0, float)]).ravel()
+            src = torch.from_numpy(st).to(self.chain_state.device)
+        # on the tracking stream, ordered after the previous batch's pose chain
+        with torch.cuda.stream(self.stream if self.stream is not None
+                               else torch.cuda.current_stream()):
+            self.chain_state.copy_(src, non_blocking=True)
 
     def check(self):
         """Synchronises: raise if any ORB count since the last check was negative
