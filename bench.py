@@ -293,6 +293,10 @@ def run_tracking(args, world, rank):
         from slam355 import _lib as slib
 
         slib.call("slam_ba_set_solve_lds_floor", int(args.solve_lds_floor))
+    if args.orb_lds_floor:
+        from slam355 import _lib as slib
+
+        slib.call("slam_orb_set_lds_floor", int(args.orb_lds_floor))
     trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
                   stream=trk_stream, orb_stream=orb_stream)
     rng = np.random.default_rng(2000 + rank)
@@ -993,6 +997,8 @@ def main():
     ap.add_argument("--solve-lds-floor", type=int, default=0,
                     help="LDS bytes the one-workgroup camera solve requests at least "
                          "(slam_ba_set_solve_lds_floor)")
+    ap.add_argument("--orb-lds-floor", type=int, default=0,
+                    help="LDS bytes k_orb_tile requests at least (slam_orb_set_lds_floor)")
     ap.add_argument("--valu", action="store_true",
                     help="matcher: force the integer-VALU kNN-2 kernel (default: fp4 matrix cores)")
     ap.add_argument("--no-tracked-ba", action="store_true",

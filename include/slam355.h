@@ -412,6 +412,12 @@ int slam_ba_iterate_batch(const slam_ba_problem* probs, int n_probs, int n_iter,
  * workgroup) keeps its latency-bound pivot chain on CUs of its own.  Process-wide;
  * takes effect at the next launch (and is baked into graphs captured after). */
 int slam_ba_set_solve_lds_floor(int bytes);
+
+/* Minimum dynamic LDS (bytes, <= 160 KiB) k_orb_tile requests; 0 (default) =
+ * what the patch needs (~79 KiB at C2: two workgroups per CU).  Between 80 and
+ * ~80.6 KiB one ORB workgroup per CU leaves room for one local-BA
+ * linearisation workgroup beside it.  Process-wide (A/B experiments). */
+int slam_orb_set_lds_floor(int bytes);
 int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0, void* stream);
 
 /* ------------------------------------------------------------------ pose chain

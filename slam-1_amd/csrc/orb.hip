@@ -1076,6 +1076,7 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
 }
 
 bool g_pattern_uploaded[64] = {false};
+int g_orb_lds_floor = 0;  // slam_orb_set_lds_floor
 
 }  // namespace
 
@@ -1091,6 +1092,12 @@ extern "C" int slam_orb_profile_read(unsigned long long* out16) {
   return SLAM_OK;
 }
 #endif
+
+extern "C" int slam_orb_set_lds_floor(int bytes) {
+  SLAM_REQUIRE(bytes >= 0 && bytes <= 160 * 1024, "slam_orb_set_lds_floor: %d B", bytes);
+  g_orb_lds_floor = bytes;
+  return SLAM_OK;
+}
 
 extern "C" int slam_orb_workspace_bytes(int batch, int H, int W, int max_kp, int overlap_div,
                                         int height_div, int width_div, size_t* bytes) {
@@ -1142,7 +1149,7 @@ extern "C" int slam_orb_tiles(const uint8_t* d_img, int batch, int H, int W, int
       ~(uintptr_t)255);
   SLAM_REQUIRE(((uintptr_t)ws_cnt & 3) == 0, "slam_orb_tiles: workspace misaligned");
   auto kern = g.glob ? k_orb_tile<true> : k_orb_tile<false>;
-  kern<<<dim3(g.n_tiles, batch), kOrbWG, g.lds_total, s>>>(d_img, g, ws_kp, ws_oct,
+  kern<<<dim3(g.n_tiles, batch), kOrbWG, max(g.lds_total, g_orb_lds_floor), s>>>(d_img, g, ws_kp, ws_oct,
                                                                   ws_desc, ws_cnt, ws_cand,
                                                                   ws_lvl);
   SLAM_LAUNCHED("k_orb_tile");
