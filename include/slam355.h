@@ -418,6 +418,11 @@ int slam_ba_set_solve_lds_floor(int bytes);
  * ~80.6 KiB one ORB workgroup per CU leaves room for one local-BA
  * linearisation workgroup beside it.  Process-wide (A/B experiments). */
 int slam_orb_set_lds_floor(int bytes);
+
+/* *d_min = min(*d_min, d_count[0..n)) on the device (the Tracker's running
+ * minimum of slam_orb_tiles' counts: a negative count flags an overflow), with
+ * no host round trip. */
+int slam_count_min(const int32_t* d_count, int n, int32_t* d_min, void* stream);
 int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0, void* stream);
 
 /* ------------------------------------------------------------------ pose chain

@@ -1078,6 +1078,14 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
 bool g_pattern_uploaded[64] = {false};
 int g_orb_lds_floor = 0;  // slam_orb_set_lds_floor
 
+// running minimum of the per-image keypoint counts (a negative count flags a
+// workspace overflow): one lane per count, integer atomicMin (order-free)
+__global__ __launch_bounds__(256) void k_count_min(const int32_t* __restrict__ count, int n,
+                                                   int32_t* __restrict__ dmin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicMin(dmin, count[i]);
+}
+
 }  // namespace
 
 #ifdef SLAM_ORB_PROFILE
@@ -1092,6 +1100,15 @@ extern "C" int slam_orb_profile_read(unsigned long long* out16) {
   return SLAM_OK;
 }
 #endif
+
+extern "C" int slam_count_min(const int32_t* d_count, int n, int32_t* d_min, void* stream) {
+  SLAM_REQUIRE(n >= 0, "slam_count_min: n < 0");
+  if (n == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_count && d_min, "slam_count_min: null pointer");
+  k_count_min<<<dim3((n + 255) / 256), dim3(256), 0, slam::as_stream(stream)>>>(d_count, n, d_min);
+  SLAM_LAUNCHED("k_count_min");
+  return SLAM_OK;
+}
 
 extern "C" int slam_orb_set_lds_floor(int bytes) {
   SLAM_REQUIRE(bytes >= 0 && bytes <= 160 * 1024, "slam_orb_set_lds_floor: %d B", bytes);

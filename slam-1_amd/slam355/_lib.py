@@ -89,6 +89,7 @@ SIGNATURES = {
     "slam_ba_iterate_batch": [_PROB, c_int, c_int, c_p],
     "slam_ba_set_solve_lds_floor": [c_int],
     "slam_orb_set_lds_floor": [c_int],
+    "slam_count_min": [c_p, c_int, c_p, c_p],
     "slam_hamming_force_valu": [c_int],
     "slam_ba_reset_batch": [_PROB, c_int, c_double, c_p],
     "slam_pose_chain_objective": [c_p, c_int, c_int, c_int, c_p, c_p],
