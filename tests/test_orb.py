@@ -402,3 +402,22 @@ def test_gpu_orb_reference_api_shapes():
     ek, eo, ed = oracle.orb_tiles(L[0], 14)
     assert des.shape == (len(kps), 32) and des.dtype == np.uint8
     assert [k.pt for k in kps] == [(float(a), float(b)) for a, b in ek[:, :2]]
+
+
+@pytest.mark.gpu
+def test_gpu_count_min_running_minimum():
+    """slam_count_min (the Tracker's device-side overflow flag): the running
+    minimum over successive count arrays, negative counts included."""
+    import torch
+    from slam355 import _lib
+    from slam355.device import ptr
+
+    dmin = torch.full((1,), 1 << 30, dtype=torch.int32, device="cuda")
+    seen = 1 << 30
+    rng = np.random.default_rng(3)
+    for n in (1, 65, 300, 0):
+        c = rng.integers(-5, 3000, n).astype(np.int32)
+        _lib.call("slam_count_min", ptr(torch.from_numpy(c).cuda()) if n else None, n, ptr(dmin), None)
+        seen = min([seen] + c.tolist())
+        torch.cuda.synchronize()
+        assert int(dmin.item()) == seen, n
