@@ -2585,19 +2585,15 @@ __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
     reproject_pre<true>(p.camrec[cur] + kCamRec * p.obs_cam[o], p.pts[cur] + 3 * pt,
                         p.obs_q + 2 * o, r, J);
     clamp_rows<true>(r, J);
-    // w = W_o^T dc with W_o = Jc^T Jp, as Jp^T (Jc dc): 24 FMAs instead of
-    // the 9 x 15 of forming W_o's rows (the same sum, reassociated)
     const double* dc = p.delta_c + 9 * p.obs_cam[o];
-    double t0 = 0.0, t1 = 0.0;
+    double w0 = 0.0, w1 = 0.0, w2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const double c = dc[i];
-      t0 += J[0][i] * c;
-      t1 += J[1][i] * c;
+      w0 += (J[0][i] * J[0][9] + J[1][i] * J[1][9]) * c;
+      w1 += (J[0][i] * J[0][10] + J[1][i] * J[1][10]) * c;
+      w2 += (J[0][i] * J[0][11] + J[1][i] * J[1][11]) * c;
     }
-    const double w0 = J[0][9] * t0 + J[1][9] * t1;
-    const double w1 = J[0][10] * t0 + J[1][10] * t1;
-    const double w2 = J[0][11] * t0 + J[1][11] * t1;
     sw[0][t] = w0;
     sw[1][t] = w1;
     sw[2][t] = w2;
