@@ -1,4 +1,4 @@
-"""Phase timing of k_solve_reg (needs a library built with -DSLAM_SOLVE_PROFILE:
+"""Phase timing of k_solve_blk (needs a library built with -DSLAM_SOLVE_PROFILE:
 `make -C slam-1_amd clean all HIPFLAGS_EXTRA=-DSLAM_SOLVE_PROFILE`)."""
 import os
 import sys
