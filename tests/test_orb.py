@@ -421,3 +421,25 @@ def test_gpu_count_min_running_minimum():
         seen = min([seen] + c.tolist())
         torch.cuda.synchronize()
         assert int(dmin.item()) == seen, n
+
+
+@pytest.mark.gpu
+def test_gpu_orb_lds_floor_keeps_results():
+    """slam_orb_set_lds_floor (placement knob: one ORB workgroup per CU) changes
+    where the workgroups run, never what they compute: bit-identical outputs."""
+    import torch
+    from slam355 import _lib, orb
+
+    L, R = _frames(1, 1280, 720, seed=4)
+    t = torch.from_numpy(np.ascontiguousarray(np.concatenate([L, R]))).cuda()
+    ref = [x.cpu().numpy().copy() for x in orb.orb_batch(t, 64)]
+    try:
+        _lib.call("slam_orb_set_lds_floor", 82432)
+        got = [x.cpu().numpy().copy() for x in orb.orb_batch(t, 64)]
+    finally:
+        _lib.call("slam_orb_set_lds_floor", 0)
+    n = ref[3]
+    assert np.array_equal(got[3], n)
+    for b in range(len(n)):
+        for a, e in zip(got[:3], ref[:3]):
+            assert np.array_equal(a[b, :n[b]], e[b, :n[b]]), b
