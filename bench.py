@@ -946,12 +946,16 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="tracking", choices=["tracking", "ba", "matcher", "vo"])
-    ap.add_argument("--batch", type=int, default=32, help="frame pairs per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frame pairs per GPU per step (default: 64 for the tracking workload -- "
+                         "in alternating runs 17.6-17.9k frames/s against 16.5-16.7k at 32 and "
+                         "15.3k at 128, profiles/r3_sweeps/batch_ab_v1/ -- 32 elsewhere)")
     ap.add_argument("--kp-per-tile", type=int, default=64,
                     help="ORB max_number_of_kp per tile: 64 -> ~2090 kp/frame (levels 6-7 of a "
                          "216x192 patch cannot hold keypoints, so 56 gives only ~1780)")
-    ap.add_argument("--windows", type=int, default=8,
-                    help="distinct tracking batches in the streamed sequence")
+    ap.add_argument("--windows", type=int, default=None,
+                    help="distinct tracking batches in the streamed sequence (default: 256 / "
+                         "batch, at least 2: a 257-frame sequence at batch 32 or 64)")
     ap.add_argument("--keep-poses", action="store_true")
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
@@ -963,8 +967,10 @@ def main():
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
-    ap.add_argument("--ba-group", type=int, default=2,
-                    help="tracking: the local-BA windows of G consecutive steps advance as one launch set")
+    ap.add_argument("--ba-group", type=int, default=None,
+                    help="tracking: the local-BA windows of G consecutive steps advance as one "
+                         "launch set (default: the fewest steps whose windows fill a set of 8 -- "
+                         "2 at batch 32, 1 at batch 64)")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")
@@ -1006,6 +1012,12 @@ def main():
     ap.add_argument("--ba-cus", type=int, default=0,
                     help="disjoint CU partition: local BA on the last N CUs, tracking on the rest")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 64 if args.workload == "tracking" else 32
+    if args.windows is None:
+        args.windows = max(2, 256 // args.batch)
+    if args.ba_group is None:
+        args.ba_group = max(1, -(-8 // max(1, args.batch // args.ba_every)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
