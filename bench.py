@@ -330,11 +330,13 @@ def run_tracking(args, world, rank):
     bas = []
     for i, s in enumerate(ba_subs):
         with torch.cuda.stream(s):
-            # 8 chunks per workgroup unless set: the launch set batches 8 windows,
-            # so fewer, fuller workgroups still cover the chip and write 3/8 of
-            # the partial rows of the single-window auto choice (3); measured
-            # 13.5k (3) / 13.7k (5) / 13.8k (8) frames/s
-            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 8
+            # 5 chunks per workgroup unless set: the launch set batches 8 windows,
+            # so fewer, fuller workgroups than the single-window auto choice (3)
+            # still cover the chip and write 3/5 of its partial rows; at 64 pairs
+            # per step, alternating runs: 3 / 4 / 5 / 6 / 8 -> 17.7k / 17.8k /
+            # 18.1-18.3k / 18.1-18.3k / 17.6-17.9k frames/s
+            # (profiles/r3_sweeps/b64_knobs_v1/; 8 was best at 32 pairs per step)
+            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 5
             bas.append(BABatch([BAProblem(*w, stream=s, chunks_per_wg=cpw)
                                 for w in windows[i::ns]], stream=s))
     ba = bas[0]
@@ -962,7 +964,7 @@ def main():
     ap.add_argument("--lin-mode", default="auto", choices=["auto", "mfma", "slot"],
                     help="BA linearisation: camera-union MFMA kernel or the slot kernel")
     ap.add_argument("--chunks-per-wg", type=int, default=None,
-                    help="camera-union linearisation: chunks per workgroup (default: 8 for the "
+                    help="camera-union linearisation: chunks per workgroup (default: 5 for the "
                          "tracking workload's batched windows, auto elsewhere)")
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Batch-64 default bench against one-knob variants (ORB CU mask, linearisation
+# chunks per workgroup), alternating in separate processes:
+#   gpu_r3_b64_knobs.sh TAG [ROUNDS] [SET]
+# SET "mask" (default): ORB CU mask 200 / 232 / all and 5 chunks per WG;
+# SET "cpw": 3 / 4 / 5 / 6 chunks per linearisation WG against the default.
+set -o pipefail
+ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+TAG="${1:-r3}"
+N="${2:-2}"
+SET="${3:-mask}"
+if [ "$SET" = cpw ]; then
+  KNOBS=("default::" "cpw3::--chunks-per-wg 3" "cpw4::--chunks-per-wg 4" "cpw5::--chunks-per-wg 5" "cpw6::--chunks-per-wg 6")
+else
+  KNOBS=("default::" "orb200::--orb-cus 200" "orb232::--orb-cus 232" "orball::--orb-cus 0" "cpw5::--chunks-per-wg 5")
+fi
+OUT="$ROOT/gpurun_out/b64knobs_$TAG"
+mkdir -p "$OUT"
+cd "$ROOT"
+V=("${KNOBS[@]}")
+for i in $(seq 1 $N); do
+  for v in "${V[@]}"; do
+    name="${v%%::*}"; flags="${v#*::}"
+    timeout -k 10 200 python bench.py --no-cpu-baseline --no-ba-scale --no-tracked-ba $flags > "$OUT/${name}_$i.json" 2> "$OUT/${name}_$i.err" || exit 1
+  done
+done
+echo done
