@@ -4,13 +4,16 @@
 #   gpu_r3_b64_knobs.sh TAG [ROUNDS] [SET]
 # SET "mask" (default): ORB CU mask 200 / 232 / all and 5 chunks per WG;
 # SET "cpw": 3 / 4 / 5 / 6 chunks per linearisation WG against the default;
-# SET "misc": stream priority, BA windows over two streams, ORB mask 208.
+# SET "misc": stream priority, BA windows over two streams, ORB mask 208;
+# SET "trk": tracking-tail CU mask 240 / 248 (the last CUs left to local BA).
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-r3}"
 N="${2:-2}"
 SET="${3:-mask}"
-if [ "$SET" = misc ]; then
+if [ "$SET" = trk ]; then
+  KNOBS=("default::" "trk248::--track-cus 248" "trk240::--track-cus 240")
+elif [ "$SET" = misc ]; then
   KNOBS=("default::" "prio_equal::--priority equal" "prio_track::--priority track" "bastreams2::--ba-streams 2" "orb208::--orb-cus 208")
 elif [ "$SET" = cpw ]; then
   KNOBS=("default::" "cpw3::--chunks-per-wg 3" "cpw4::--chunks-per-wg 4" "cpw5::--chunks-per-wg 5" "cpw6::--chunks-per-wg 6")
