@@ -971,8 +971,8 @@ def main():
                          "--workload ba --ba-batch N)")
     ap.add_argument("--ba-group", type=int, default=None,
                     help="tracking: the local-BA windows of G consecutive steps advance as one "
-                         "launch set (default: the fewest steps whose windows fill a set of 8 -- "
-                         "2 at batch 32, 1 at batch 64)")
+                         "launch set (default: the fewest steps whose windows fill one batched "
+                         "launch of SLAM_BA_MAX_BATCH = 16 -- 2 at batch 64, 4 at batch 32)")
     ap.add_argument("--ba-batch", type=int, default=1,
                     help="--workload ba: advance this many C3 windows together")
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")
@@ -1018,8 +1018,8 @@ def main():
         args.batch = 64 if args.workload == "tracking" else 32
     if args.windows is None:
         args.windows = max(2, 256 // args.batch)
-    if args.ba_group is None:
-        args.ba_group = max(1, -(-8 // max(1, args.batch // args.ba_every)))
+    if args.ba_group is None:  # the fewest steps whose windows fill one batched launch
+        args.ba_group = max(1, -(-16 // max(1, args.batch // args.ba_every)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:

@@ -372,8 +372,11 @@ typedef struct slam_ba_problem {
  * one persistent workgroup per tile column, all resident at once (<= 1 per CU). */
 #define SLAM_TL_FLOW_MAX_T 128
 
-/* Problems per batched launch (slam_ba_iterate_batch splits larger batches). */
-#define SLAM_BA_MAX_BATCH 8
+/* Problems per batched launch (slam_ba_iterate_batch splits larger batches).
+ * The descriptors travel by value in the kernel arguments: 16 x 296 B. */
+#ifndef SLAM_BA_MAX_BATCH
+#define SLAM_BA_MAX_BATCH 16
+#endif
 
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);

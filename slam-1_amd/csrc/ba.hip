@@ -54,7 +54,7 @@ constexpr int kBS = 256;   // block size of the element-wise kernels
 // Batched LM: independent problems (local-BA windows) advance through one set
 // of launches, one problem per blockIdx.y; each keeps its own buffers and LM
 // state, so the iterates of a batched problem equal its solo iterates.  The
-// problem descriptors travel by value in the kernel arguments (8 x 296 B).
+// problem descriptors travel by value in the kernel arguments (16 x 296 B).
 constexpr int kBaMaxBatch = SLAM_BA_MAX_BATCH;
 struct BaBatch {
   slam_ba_problem p[kBaMaxBatch];

@@ -864,7 +864,7 @@ class BABatch:
     latency instead of B.  Every problem keeps its own device buffers and LM
     state; its iterates equal the ones BAProblem.iterate gives it alone."""
 
-    MAX_BATCH = 8  # SLAM_BA_MAX_BATCH
+    MAX_BATCH = 16  # SLAM_BA_MAX_BATCH
 
     def __init__(self, problems, stream=None):
         self.problems = list(problems)

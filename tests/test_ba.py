@@ -374,6 +374,28 @@ def test_gpu_batched_windows_equal_solo_iterates():
 
 
 @pytest.mark.gpu
+def test_gpu_batched_windows_full_launch_and_split():
+    """More windows than one batched launch takes (SLAM_BA_MAX_BATCH = 16: the
+    descriptors travel by value in the kernel arguments): 16 windows in one
+    launch, the 2 left over in a second; every window's iterates equal its solo
+    iterates bit for bit."""
+    from slam355 import ba
+
+    assert ba.BABatch.MAX_BATCH == 16
+    shapes = [(60 + i, 6 + (i % 3), 300 + 40 * i, 3 + (i % 2)) for i in range(18)]
+    wins = [_window(*w) for w in shapes]
+    solo = [ba.BAProblem(*w) for w in wins]
+    for p in solo:
+        p.iterate(3)
+    batch = ba.BABatch([ba.BAProblem(*w) for w in wins])
+    batch.iterate(3)
+    for a, b in zip(solo, batch.problems):
+        assert a.state() == b.state()
+        for x, y in zip(a.params(), b.params()):
+            assert np.array_equal(x, y)
+
+
+@pytest.mark.gpu
 def test_gpu_batched_windows_match_oracle_schur_lm():
     """Per window of a batch, 3 LM iterations (C3 included) equal the oracle's
     Schur LM (oracle.ba.lm_iteration_schur): accept flags, costs 1e-9, lambda,
