@@ -998,10 +998,11 @@ def main():
                     help="tracking: ORB on the tracking stream (default: ORB on its own stream "
                          "into double-buffered outputs, so the next batch's ORB overlaps this "
                          "batch's matching / PnP tail)")
-    ap.add_argument("--orb-cus", type=int, default=216,
+    ap.add_argument("--orb-cus", type=int, default=224,
                     help="ORB pipeline: ORB's stream may use only the first N CUs (0: all); the "
                          "rest are left to the latency-bound local-BA and tracking-tail kernels "
-                         "(r2 sweep: 224 -> 10.6k, 208 -> 10.7k, 192 -> 10.5k, all -> 10.0k frames/s)")
+                         "(at the 64-pair / 16-window default, alternating runs: 216 -> 18.8-19.0k, "
+                         "224 -> 19.2-19.3k, 232 -> 18.9-19.1k, 240 -> 18.8-19.0k frames/s)")
     ap.add_argument("--solve-lds-floor", type=int, default=0,
                     help="LDS bytes the one-workgroup camera solve requests at least "
                          "(slam_ba_set_solve_lds_floor)")
