@@ -297,6 +297,10 @@ def run_tracking(args, world, rank):
         from slam355 import _lib as slib
 
         slib.call("slam_orb_set_lds_floor", int(args.orb_lds_floor))
+    if args.valu:  # the integer-VALU kNN-2 kernel in the pipeline (A/B)
+        from slam355 import _lib as slib
+
+        slib.lib.slam_hamming_force_valu(1)
     trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
                   stream=trk_stream, orb_stream=orb_stream)
     rng = np.random.default_rng(2000 + rank)
@@ -444,7 +448,7 @@ def run_tracking(args, world, rank):
     oc = cnt["orb"].astype(np.int64)
     m_pairs = float((oc[:B] * oc[B + 1:2 * B + 1]).sum())
     m_ms = stages.get("stereo_knn2", float("nan"))
-    roof["matcher"] = matcher_roofline(m_pairs, m_ms, trk.cap, "stereo, in the pipeline")
+    roof["matcher"] = matcher_roofline(m_pairs, m_ms, trk.cap, "stereo, in the pipeline", args.valu)
     roof["matcher"]["unique_descriptor_bytes"] = float(oc[:B].sum() + oc[B + 1:2 * B + 1].sum()) * 32
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
@@ -1009,7 +1013,8 @@ def main():
     ap.add_argument("--orb-lds-floor", type=int, default=0,
                     help="LDS bytes k_orb_tile requests at least (slam_orb_set_lds_floor)")
     ap.add_argument("--valu", action="store_true",
-                    help="matcher: force the integer-VALU kNN-2 kernel (default: fp4 matrix cores)")
+                    help="matcher and tracking: force the integer-VALU kNN-2 kernel (default: fp4 "
+                         "matrix cores)")
     ap.add_argument("--no-tracked-ba", action="store_true",
                     help="tracking: skip the local BA of a window built from tracked frames")
     ap.add_argument("--ba-cus", type=int, default=0,

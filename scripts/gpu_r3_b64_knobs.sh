@@ -7,13 +7,16 @@
 # SET "misc": stream priority, BA windows over two streams, ORB mask 208;
 # SET "trk": tracking-tail CU mask 240 / 248 (the last CUs left to local BA);
 # SET "mb16": chunks per WG 6 / 8 and ORB mask 208 / 224 with 16-window launches;
-# SET "orbmask": ORB mask 224 / 232 / 240 with 16-window launches.
+# SET "orbmask": ORB mask 224 / 232 / 240 with 16-window launches;
+# SET "valu": the integer-VALU kNN-2 kernel in the pipeline.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-r3}"
 N="${2:-2}"
 SET="${3:-mask}"
-if [ "$SET" = orbmask ]; then
+if [ "$SET" = valu ]; then
+  KNOBS=("default::" "valu::--valu")
+elif [ "$SET" = orbmask ]; then
   KNOBS=("default::" "orb224::--orb-cus 224" "orb232::--orb-cus 232" "orb240::--orb-cus 240")
 elif [ "$SET" = mb16 ]; then
   KNOBS=("default::" "cpw6::--chunks-per-wg 6" "cpw8::--chunks-per-wg 8" "orb208::--orb-cus 208" "orb224::--orb-cus 224")
