@@ -8,13 +8,16 @@
 # SET "trk": tracking-tail CU mask 240 / 248 (the last CUs left to local BA);
 # SET "mb16": chunks per WG 6 / 8 and ORB mask 208 / 224 with 16-window launches;
 # SET "orbmask": ORB mask 224 / 232 / 240 with 16-window launches;
-# SET "valu": the integer-VALU kNN-2 kernel in the pipeline.
+# SET "valu": the integer-VALU kNN-2 kernel in the pipeline;
+# SET "prio": stream priorities equal / tracking-high at the final default.
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="${1:-r3}"
 N="${2:-2}"
 SET="${3:-mask}"
-if [ "$SET" = valu ]; then
+if [ "$SET" = prio ]; then
+  KNOBS=("default::" "prio_equal::--priority equal" "cpw4::--chunks-per-wg 4")
+elif [ "$SET" = valu ]; then
   KNOBS=("default::" "valu::--valu")
 elif [ "$SET" = orbmask ]; then
   KNOBS=("default::" "orb224::--orb-cus 224" "orb232::--orb-cus 232" "orb240::--orb-cus 240")
