@@ -192,10 +192,15 @@ __global__ __launch_bounds__(kWG) void knn2_kernel(
 #endif
 constexpr int kMxWG = SLAM_MX_WG;          // 4 waves: train steps dealt round-robin
 constexpr int kMxWaves = kMxWG / kWave;
+// Query blocks of 16 per workgroup: 8 is the fastest alone (C2 micro-bench
+// 2897 vs 2429 Gpairs/s at batch 32), 6 inside the tracking pipeline (192
+// instead of 248 VGPRs, so its waves find room beside the local-BA and tail
+// kernels on the CUs ORB leaves: 19.4-19.7k vs 19.0-19.1k frames/s in
+// alternating runs, profiles/r3_sweeps/mxqb_pipe_v1/) -- the pipeline wins.
 #ifndef SLAM_MX_QB
-#define SLAM_MX_QB 8
+#define SLAM_MX_QB 6
 #endif
-constexpr int kMxQB = SLAM_MX_QB;          // query blocks of 16 (8: 4 per step measured 10 % slower)
+constexpr int kMxQB = SLAM_MX_QB;          // (4 per step measured 10 % slower than 8 alone)
 constexpr int kMxQWG = 16 * kMxQB;         // queries per workgroup
 constexpr int kMxAhead = 2;                // train steps loaded ahead
 constexpr float kMxNone = 16777215.0f;     // > every valid key (< 2^23 + 2^14)
