@@ -3,8 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload tracking|ba|matcher]
 
 Default workload ("tracking", BASELINE.json metric "frames/sec tracking+local-BA
-@1280x720"): one step = B synthetic 1280x720 stereo frame pairs, streamed from
-pinned host memory inside the timed region, through the whole tracking hot
+@1280x720"): one step = B synthetic 1280x720 stereo frame pairs, resident in
+HBM before the timed region (the PCIe-inclusive rate, frames streamed from
+pinned host memory, is reported beside it), through the whole tracking hot
 path (ORB on 2B+1 images with 64 kp/tile ~ 2075 kp/frame, on its own CU-masked
 stream pipelined against the previous batch's tail; stereo kNN-2 + ratio,
 F-LMedS, triangulation, temporal kNN-2 + gate, PnP-RANSAC, device pose chain)
@@ -116,14 +117,18 @@ def timed_loop(step, steps, warmup, world, marks_every=True, dict_marks=False):
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_s = []
     for _ in range(steps):
+        ts = time.perf_counter()
         marks = ({} if dict_marks else []) if marks_every else None
         step(marks)
         if marks is not None:
             all_marks.append(marks)
+        step_s.append(time.perf_counter() - ts)
     # host time to issue the K steps (no synchronisation inside the loop): when
     # it approaches dt, the launches, not the GPU, set the pace
     timed_loop.host_s = time.perf_counter() - t0
+    timed_loop.step_s = step_s
     torch.cuda.synchronize()
     barrier(world)
     dt = time.perf_counter() - t0
@@ -188,28 +193,37 @@ def masked_stream(n_cus, first=0):
 
 
 class FrameFeed:
-    """Host-resident synthetic stereo sequence streamed to the GPU inside the
-    timed region: the sequence lives in pinned host memory, pre-packed per
-    tracking batch as [left_0..left_B, right_0..right_{B-1}] (2B+1 images, so
-    one H2D copy per step), and step k's batch is uploaded on a copy stream
-    into one of two device slots while step k-1 is tracked (double buffering:
-    the copy into a slot waits until the tracking that read it has finished)."""
+    """The synthetic stereo sequence, pre-packed per tracking batch as
+    [left_0..left_B, right_0..right_{B-1}] (2B+1 images per step).
 
-    def __init__(self, L, R, B, n_windows):
-        self.B, self.n_windows = B, n_windows
+    resident=True (the headline, the contract's "inputs already resident in
+    HBM"): every batch lives in HBM before the timed region; step k reads
+    batch k mod n_windows in place.
+    resident=False (`pcie_inclusive` beside the headline): the sequence lives in
+    pinned host memory and step k's batch is uploaded on a copy stream into one
+    of two device slots while step k-1 is tracked (double buffering: the copy
+    into a slot waits until the tracking that read it has finished)."""
+
+    def __init__(self, L, R, B, n_windows, resident=True):
+        self.B, self.n_windows, self.resident = B, n_windows, resident
         H, W = L.shape[1:]
-        packs = torch.empty((n_windows, 2 * B + 1, H, W), dtype=torch.uint8).pin_memory()
+        packs = torch.empty((n_windows, 2 * B + 1, H, W), dtype=torch.uint8,
+                            device="cuda" if resident else "cpu")
+        if not resident:
+            packs = packs.pin_memory()
         for w in range(n_windows):
             f0 = w * B
-            packs[w, :B + 1] = L[f0:f0 + B + 1].cpu()
-            packs[w, B + 1:] = R[f0:f0 + B].cpu()
+            packs[w, :B + 1] = L[f0:f0 + B + 1].to(packs.device)
+            packs[w, B + 1:] = R[f0:f0 + B].to(packs.device)
         self.packs = packs
+        self.k = 0
+        if resident:
+            return
         self.slots = [torch.empty((2 * B + 1, H, W), dtype=torch.uint8, device="cuda")
                       for _ in range(2)]
         self.copy_stream = torch.cuda.Stream()
         self.ready = [torch.cuda.Event() for _ in range(2)]
         self.free = [torch.cuda.Event() for _ in range(2)]
-        self.k = 0
 
     def upload(self, k):
         slot = k % 2
@@ -220,21 +234,27 @@ class FrameFeed:
         self.ready[slot].record(cs)
 
     def prime(self):
+        self.k = 0
+        if self.resident:
+            return
         for e in self.free:
             e.record(torch.cuda.current_stream())
         self.upload(0)
 
     def next(self, stream):
-        """-> (slot tensor of step k, window index); issues the upload of step
-        k+1; `stream` waits for step k's upload.  Call release(stream) after
-        the launches that read the slot."""
+        """-> (images of step k, window index).  Streamed: issues the upload of
+        step k+1 and makes `stream` wait for step k's upload.  Call
+        release(stream) after the launches that read the images."""
         k = self.k
+        if self.resident:
+            return self.packs[k % self.n_windows], k % self.n_windows
         self.upload(k + 1)
         stream.wait_event(self.ready[k % 2])
         return self.slots[k % 2], k % self.n_windows
 
     def release(self, stream):
-        self.free[self.k % 2].record(stream)
+        if not self.resident:
+            self.free[self.k % 2].record(stream)
         self.k += 1
 
 
@@ -267,7 +287,11 @@ def run_tracking(args, world, rank):
     # once (untimed), then held in pinned host memory and streamed back
     L, R, poses, rig = corridor_sequence(n_win * B + 1, W_IMG, H_IMG, seed=1000 + rank,
                                          device="cuda", as_numpy=False)
-    feed = FrameFeed(L, R, B, n_win)
+    feed = FrameFeed(L, R, B, n_win, resident=True)
+    # the PCIe-inclusive variant (reported beside `value`, never as it): the same
+    # sequence streamed from pinned host memory inside its own timed region
+    feed_h2d = None if args.no_pcie_leg else FrameFeed(L, R, B, n_win, resident=False)
+    feeds = [feed]
     CPU_PAIRS = 16  # cpu_baseline sample: 16 frame pairs + 16 LM iterations (~10 s of host work)
     L_np, R_np = L[:CPU_PAIRS + 1].cpu().numpy(), R[:CPU_PAIRS].cpu().numpy()
     del L, R
@@ -356,6 +380,7 @@ def run_tracking(args, world, rank):
 
     ba_done = [None]
     step_no, pending = [0], [0]
+    flush_at = {args.warmup, args.warmup + args.steps}  # step numbers that flush a launch set
 
     def step(marks):
         with torch.cuda.stream(tstream):
@@ -363,14 +388,21 @@ def run_tracking(args, world, rank):
 
     def tracked_step(marks):
         tmarks = [] if marks is not None else None
+        if marks is not None and trk.host_times is None:
+            trk.host_times = {}  # host issue time per call site, timed steps only
+        h0 = time.perf_counter()
         ist = orb_stream if orb_stream is not None else tstream  # the stream that reads imgs
-        imgs, win = feed.next(ist)
+        fd = feeds[0]
+        imgs, win = fd.next(ist)
+        h0 = trk._ht("upload_issue", h0)
         if win == 0:  # a new pass over the sequence starts at frame 0
             trk.reset_chain()
+            h0 = trk._ht("reset_chain", h0)
         if args.ba_overlap == "after-orb" and ba_done[0] is not None:
             ist.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
         trk.track(win * B, imgs=imgs, marks=tmarks)
-        feed.release(ist)
+        h0 = time.perf_counter()
+        fd.release(ist)
         if tmarks is not None and orb_stream is not None:
             marks["orb"] = trk.orb_marks  # ORB's own stream: start -> done there
         if marks is None and args.keep_poses:
@@ -378,9 +410,10 @@ def run_tracking(args, world, rank):
         step_no[0] += 1
         pending[0] += 1
         k = step_no[0]
-        if pending[0] < G and k != args.warmup and k != args.warmup + args.steps:
+        if pending[0] < G and k not in flush_at:
             if marks is not None:
                 marks["track"] = tmarks
+            trk._ht("release_marks", h0)
             return  # this step's windows join the next step's launch set
         # (a set flushed early -- end of warmup, or a timed region of K not a
         # multiple of G -- still advances all G steps' windows: extra work, never less)
@@ -388,6 +421,7 @@ def run_tracking(args, world, rank):
         pending[0] = 0
         if args.ba_overlap == "after-orb":
             ba_stream.wait_event(trk.orb_event)
+        h0 = trk._ht("release_marks", h0)
         bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None and full else None
         for bt, s in zip(bas, ba_subs):
             if s is not ba_stream:
@@ -410,8 +444,30 @@ def run_tracking(args, world, rank):
             marks["ba"] = bmarks
         if marks is not None:
             marks["track"] = tmarks
+        trk._ht("ba_graph_launch", h0)
 
     dt, stages = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
+    # host issue time per call site over the timed steps: sum per step and the
+    # slowest single call (a call that blocks on the device shows up as a max)
+    host_sites = host_site_summary(trk, args.steps)
+    main_step_s, main_host_s = timed_loop.step_s, timed_loop.host_s
+    pcie = None
+    if feed_h2d is not None:
+        # the same steps with the frames uploaded from pinned host memory inside
+        # the timed region (two device slots, copy stream): the PCIe-inclusive rate
+        feeds[0] = feed_h2d
+        feed_h2d.prime()
+        flush_at.clear()
+        flush_at.update({step_no[0] + args.warmup, step_no[0] + args.warmup + args.steps})
+        dt_p, st_p = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
+        pcie = {"frames_per_s": reduce_scalar(float(B * args.steps), world, "sum") / dt_p,
+                "ms_per_step": dt_p / args.steps * 1e3,
+                "host_issue_ms_per_step": timed_loop.host_s / args.steps * 1e3,
+                "host_issue_sites": host_site_summary(trk, args.steps),
+                "upload_bytes_per_step": float(feed_h2d.packs[0].numel()),
+                "note": "frames streamed from pinned host memory inside the timed region "
+                        "(copy stream, two device slots); not the headline"}
+        feeds[0] = feed
     frames = reduce_scalar(float(B * args.steps), world, "sum")
     cnt = trk.counters()  # raises on any ORB workspace overflow since the start
     # accuracy of the tracked trajectory (the last tracked window; the device
@@ -476,20 +532,23 @@ def run_tracking(args, world, rank):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
-        "host_issue_ms_per_step": timed_loop.host_s / args.steps * 1e3,
+        "host_issue_ms_per_step": main_host_s / args.steps * 1e3,
+        "host_issue_sites": host_sites,
+        "host_issue_ms_per_step_list": [round(x * 1e3, 3) for x in main_step_s],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8+f32+f64",
         "data": (f"synthetic (seeded textured-corridor stereo sequence, {n_win * B + 1} frames "
-                 "1280x720 in pinned host memory, uploaded inside the timed region; GT poses)"),
+                 "1280x720 resident in HBM; GT poses)"),
         "config": {"workload": f"C2 tracking (1280x720, {args.kp_per_tile} ORB kp/tile) + "
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
                                f"x {args.ba_iters} LM iters ({n_solves} windows per step, batched" +
                                (f" over {G} steps per launch set)" if G > 1 else ")"),
                    "orb_kp_mean": kp_mean,
                    "frames_per_gpu_per_step": B, "parallelism": f"frame-pair shards x{world}",
-                   "h2d_upload": "in timed region (pinned, copy stream, double-buffered)",
+                   "inputs": "resident in HBM before the timed region (the PCIe-inclusive "
+                             "rate with the frames streamed from pinned host memory: pcie_inclusive)",
                    "local_ba_stream": "serial" if args.ba_serial else "concurrent",
                    "high_priority_stream": args.priority,
                    "ba_overlap": args.ba_overlap,
@@ -517,6 +576,8 @@ def run_tracking(args, world, rank):
                      "trajectory_t_err_m_max_in_window": float(t_err_win.max()),
                      "frames_chained": int(f0 + B)},
     }
+    if pcie is not None:
+        rec["pcie_inclusive"] = pcie
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, windows[0],
                                                     pairs=CPU_PAIRS, lm_iters=CPU_PAIRS)
@@ -535,6 +596,16 @@ def run_tracking(args, world, rank):
         # of the reduced camera system per iteration) -- strong scaling in N
         rec["local_ba_sharded"] = c4_sharded_iters(world, rank, steps=20, warmup=3)
     return rec
+
+
+def host_site_summary(trk, steps):
+    """Host issue time per call site over the timed steps (Tracker.host_times):
+    sum per step and the slowest single call (a call that blocks on the device
+    shows up as a large max); resets the record."""
+    out = {k: {"ms_per_step": float(np.sum(v)) / steps * 1e3, "max_ms": float(np.max(v)) * 1e3,
+               "calls": len(v)} for k, v in (trk.host_times or {}).items()}
+    trk.host_times = None
+    return out
 
 
 def tracked_window_ba(feed, B, rig, args, n_pairs=8):
@@ -694,6 +765,8 @@ def run_ba(args, world, rank):
         else:  # one LM iteration = one HIP-graph replay (3T + 5 launches for the tiled solver)
             step_fn = lambda: prob.iterate_graphed(1)  # noqa: E731
 
+    pose_graph = pose_graph_solve(C) if name == "C5" and rank == 0 else None
+
     def step(marks):
         step_fn()
 
@@ -717,7 +790,37 @@ def run_ba(args, world, rank):
                      "unit": "TFLOP/s", "frac": achieved / F64_PEAK_TFLOPS, "traffic": None,
                      "kernel": "LM iteration", "flops_per_iter": flops},
         "final_cost": prob.state()["COST"],
-    }
+    } | ({"pose_graph": pose_graph,
+          "c5_pose_graph_plus_ba_ms": pose_graph["ms_per_solve"] + args.ba_iters * dt / args.steps * 1e3,
+          "c5_sequence": f"pose-graph TRF solve to convergence, then {args.ba_iters} full-BA LM "
+                         "iterations (BundleAdjustment.py:179-182, then :397-402)"}
+         if pose_graph is not None else {})
+
+
+def pose_graph_solve(m):
+    """The pose-graph half of BASELINE config 5 (BundleAdjustment.py:107-183,
+    loop_closure.py:39-52): scipy-TRF semantics on the m relative poses of a
+    drifted closed loop (k_chain_trf, one workgroup), run to its ftol test;
+    wall time per solve, including the host's status checks between chunks of
+    64 iterations."""
+    from slam355.posegraph import PoseChain
+    from slam355.synthetic import pose_chain_loop
+
+    x0 = pose_chain_loop(np.random.default_rng(11), m)
+    PoseChain(x0).solve(ftol=1e-8)  # warm (module load, first launch)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(3):
+        pc = PoseChain(x0)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = pc.solve(ftol=1e-8)
+        times.append(time.perf_counter() - t0)
+    ms = float(np.median(times)) * 1e3
+    return {"frames": m, "params": 6 * m, "residuals": m + 2, "ms_per_solve": ms,
+            "nfev": st["nfev"], "njev": st["njev"], "iterations": st["iterations"],
+            "ms_per_iteration": ms / max(1, st["iterations"]), "status": st["message"],
+            "cost0": st["cost0"], "cost": st["cost"]}
 
 
 def run_ba_batch(args, world, rank):
@@ -1015,6 +1118,9 @@ def main():
     ap.add_argument("--valu", action="store_true",
                     help="matcher and tracking: force the integer-VALU kNN-2 kernel (default: fp4 "
                          "matrix cores)")
+    ap.add_argument("--no-pcie-leg", action="store_true",
+                    help="tracking: skip the PCIe-inclusive run (frames streamed from pinned host "
+                         "memory inside the timed region) reported beside the headline")
     ap.add_argument("--no-tracked-ba", action="store_true",
                     help="tracking: skip the local BA of a window built from tracked frames")
     ap.add_argument("--ba-cus", type=int, default=0,

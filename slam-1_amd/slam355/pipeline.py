@@ -14,6 +14,8 @@ the host for the sequential 4x4 pose chain.
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 
@@ -98,6 +100,15 @@ class Tracker:
         # degrade into "no matches" + a stale pose
         self.orb_min = torch.full((1,), 1 << 30, **i32)
         self.orb_event = torch.cuda.Event()
+        # optional host-side issue time per call site (bench.py): {site: [seconds per call]}
+        self.host_times = None
+
+    def _ht(self, site, t0):
+        """Record the host time since t0 against `site`; returns the new t0."""
+        t1 = time.perf_counter()
+        if self.host_times is not None:
+            self.host_times.setdefault(site, []).append(t1 - t0)
+        return t1
 
     # ------------------------------------------------------------------ device step
     def track(self, frame0: int, imgs: torch.Tensor | None = None, marks=None, chain=True):
@@ -119,6 +130,7 @@ class Tracker:
 
         main = st if st is not None else torch.cuda.current_stream()
         ost = self.orb_stream
+        h0 = time.perf_counter()
         if ost is None:
             mark("start")
             kp, octv, desc, cnt = self.ows.run(im, st)
@@ -147,6 +159,7 @@ class Tracker:
             self.orb_done[slot].record(ost)
             main.wait_event(self.orb_done[slot])
             mark("orb_wait")
+        h0 = self._ht("orb_launch", h0)
         kpL, kpR = kp[0:B], kp[B + 1:2 * B + 1]
         dL, dR = desc[0:B], desc[B + 1:2 * B + 1]
         nL, nR = cnt[0:B], cnt[B + 1:2 * B + 1]
@@ -159,6 +172,7 @@ class Tracker:
         geometry.gather_matches(kpL, kpR, self.s_pairs, self.s_cnt,
                                 out=(self.s_ptl, self.s_ptr, None, None), stream=st)
         mark("stereo_match")
+        h0 = self._ht("stereo_launch", h0)
         # F-LMedS mask (keypoint.py:59-66), then the surviving pairs with descriptors
         geometry.fundamental_lmeds(self.s_ptl, self.s_ptr, self.s_cnt, seed=self.seed,
                                    item0=frame0, out=(self.f_mask, self.f_F, self.f_ninl),
@@ -181,29 +195,34 @@ class Tracker:
         if ost is not None:  # the last read of this slot's ORB outputs
             self.slot_free[slot].record(main)
         mark("triangulate_temporal")
+        h0 = self._ht("flmeds_tri_temporal_launch", h0)
         # PnP-RANSAC (transformation.py:11-13)
         geometry.pnp_ransac(self.Q1, self.q2, self.t_cnt, self.tK, seed=self.seed, item0=frame0,
                             out=(self.rvec, self.tvec, self.p_ninl, self.p_mask), stream=st,
                             ws=self.p_ws)
         mark("pnp")
+        h0 = self._ht("pnp_launch", h0)
         if chain:
             _lib.call("slam_pose_chain", ptr(self.rvec), ptr(self.tvec), ptr(self.p_ninl), B,
                       ptr(self.chain_state), ptr(self.poses), stream_ptr(st))
             mark("pose_chain")
+            self._ht("pose_chain_launch", h0)
         return self.rvec, self.tvec, self.p_ninl
 
     def reset_chain(self, pose0=None, T0=None):
         """Start the device pose chain at pose0 (default identity) with T0 as the
         stale transform (default identity)."""
-        if pose0 is None and T0 is None:
-            src = self._chain_eye
-        else:  # a host-built start state (a synchronous upload; not on the bench path)
-            st = np.concatenate([np.eye(4) if pose0 is None else np.asarray(pose0, float),
-                                 np.eye(4) if T0 is None else np.asarray(T0, float)]).ravel()
-            src = torch.from_numpy(st).to(self.chain_state.device)
-        # on the tracking stream, ordered after the previous batch's pose chain
+        # on the tracking stream, ordered after the previous batch's pose chain; a
+        # host-built start state is allocated on that same stream, so the caching
+        # allocator cannot hand its memory out before the copy has run (ADVICE r3)
         with torch.cuda.stream(self.stream if self.stream is not None
                                else torch.cuda.current_stream()):
+            if pose0 is None and T0 is None:
+                src = self._chain_eye
+            else:  # a host-built start state (a synchronous upload; not on the bench path)
+                st = np.concatenate([np.eye(4) if pose0 is None else np.asarray(pose0, float),
+                                     np.eye(4) if T0 is None else np.asarray(T0, float)]).ravel()
+                src = torch.from_numpy(st).to(self.chain_state.device)
             self.chain_state.copy_(src, non_blocking=True)
 
     def check(self):

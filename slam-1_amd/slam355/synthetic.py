@@ -125,6 +125,23 @@ def ba_problem_loop(rng, n_cams, n_pts, obs_per_pt, f=716.8, noise=0.5, step=1.0
     return cams, X, cam_idx.astype(np.int64), pt_idx.astype(np.int64), qs
 
 
+def pose_chain_loop(rng, m, step=1.0, rot_s=1e-3, t_s=1e-2):
+    """car_params [6m] of the reference's live pose chain (BundleAdjustment.py:
+    107-145: m relative poses [r0 r1 r2 t0 t1 t2], t2 the forward motion) for a
+    closed planar loop of m keyframes (BASELINE config 5: 500 keyframes) --
+    every relative pose turns 2 pi / m about y and moves `step` forward, so the
+    exact chain closes (a planar rigid motion is a rotation about a point; its
+    m-th power is the identity) -- plus the drift of tracking: Gaussian noise
+    rot_s on the rotation vectors and t_s on the translations, which opens the
+    loop for the loop-closure rows to pull shut."""
+    p = np.zeros((m, 6))
+    p[:, 1] = 2.0 * np.pi / m
+    p[:, 5] = step
+    p[:, :3] += rng.normal(0, rot_s, (m, 3))
+    p[:, 3:] += rng.normal(0, t_s, (m, 3))
+    return p.ravel()
+
+
 def perturb(rng, cams, pts, rot_s=1e-3, t_s=1e-2, p_s=0.05):
     """Initialisation noise of SURVEY.md §8d (rotvec 1e-3, t 1e-2 m, points 5 cm)."""
     c = cams.copy()
@@ -319,10 +336,11 @@ def render_corridor(T_cw, rig: StereoRig, gen, x_offset=0.0, ss=2, noise=2.0, de
     return torch.clamp(torch.round(img), 0, 255).to(torch.uint8)
 
 
-def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=True):
+def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=True, **geo):
     """(left [F,H,W] u8, right [F,H,W] u8, poses [F,4,4] camera-to-world, rig) of
     the textured corridor; the trajectory is trajectory() (1 m/frame, yaw
-    jitter 0.2 deg).  torch tensors on `device` unless as_numpy."""
+    jitter 0.2 deg).  torch tensors on `device` unless as_numpy.  `geo`
+    overrides CORRIDOR entries (e.g. a coarser `cell` at 640x480)."""
     import torch
 
     rng = np.random.default_rng(seed)
@@ -332,8 +350,8 @@ def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=Tr
     left = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
     right = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
     for i in range(n_frames):
-        left[i] = render_corridor(poses[i], rig, gen, 0.0, device=device)
-        right[i] = render_corridor(poses[i], rig, gen, rig.baseline, device=device)
+        left[i] = render_corridor(poses[i], rig, gen, 0.0, device=device, **geo)
+        right[i] = render_corridor(poses[i], rig, gen, rig.baseline, device=device, **geo)
     if as_numpy:
         return left.cpu().numpy(), right.cpu().numpy(), poses, rig
     return left, right, poses, rig

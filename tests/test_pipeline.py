@@ -311,3 +311,73 @@ def test_gpu_orb_pipelined_tracker_equals_serial():
             assert torch.equal(a, b), k
     ref.check()
     pip.check()
+
+
+# ----------------------------------------------------------------------------- BASELINE C1
+C1_CAP = 25  # ORB max_number_of_kp per tile giving C1's 500 kp/frame at 640x480
+@pytest.fixture(scope="module")
+def c1_seq():
+    """BASELINE config 1: synthetic 640x480 grayscale, 500 ORB kp/frame, a
+    2-keyframe window.  At 640x480 a tile's patch is 144x96, so only pyramid
+    levels 0-2 can hold keypoints (border 31): cap 14 per tile gives 3 + 3 + 2
+    per tile = 288 kp/frame; cap 25 gives 5 + 5 + 4 = 14 per tile = 504, i.e.
+    the config's 500 kp/frame."""
+    from slam355.synthetic import corridor_sequence
+
+    # 0.45 m texture cells (0.3 at 1280x720): at half the resolution the finer
+    # cells alias and leave too few temporal matches for PnP
+    return corridor_sequence(3, 640, 480, seed=41, cell=0.45)
+
+
+def test_oracle_c1_chain_is_c1_shaped(c1_seq):
+    """The C1 sequence gives ~500 kp per frame at cap 14 and a tracked pose."""
+    import oracle
+
+    L, R, poses, rig = c1_seq
+    _, _, _, cnt = oracle.orb_tiles_batch(np.concatenate([L[:2], R[:1]]), C1_CAP, 1 << 13)
+    assert 450 <= cnt.min() and cnt.max() <= 520, cnt
+    for i in range(2):  # both pairs reach PnP (>= 5 temporal matches)
+        out = op.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, max_kp=C1_CAP, seed=4, frame=i)
+        assert out["n_stereo"] >= 50 and out["n_pnp"] >= 5, (out["n_stereo"], out["n_pnp"])
+        rel = np.linalg.inv(poses[i + 1]) @ poses[i]
+        assert np.allclose(out["tvec"], rel[:3, 3], atol=0.25)
+
+
+@pytest.mark.gpu
+def test_gpu_tracker_c1_640x480_matches_oracle_chain(c1_seq):
+    """VERDICT r3 #1 (C1 = main.py:76-132 at 640x480, cap 14, a 2-keyframe
+    window; cap 25 per tile = 500 kp/frame): the batched Tracker against oracle.pipeline.track_pair per pair --
+    ORB counts, stereo / F-LMedS counts and mask, X at 1e-9, temporal count,
+    PnP inliers and pose at 1e-8, and the device-chained poses against the host
+    chain of the oracle's PnP results (the stale-T rule included)."""
+    import torch
+    from slam355.pipeline import Tracker, chain_poses
+
+    L, R, poses, rig = c1_seq
+    B = 2
+    trk = Tracker(B, 480, 640, rig.P_l, rig.P_r, max_kp_per_tile=C1_CAP, seed=4)
+    trk.imgs.copy_(torch.from_numpy(np.concatenate([L[:B + 1], R[:B]])))
+    rv, tv, n = trk.track(0)
+    P = trk.poses.cpu().numpy()
+    c = trk.counters()
+    assert 450 <= c["orb"].min() and c["orb"].max() <= 520, c["orb"]
+    cache = {}
+    erv, etv, en = [], [], []
+    for i in range(B):
+        e = op.track_pair(L[i], R[i], L[i + 1], rig.P_l, rig.P_r, max_kp=C1_CAP, seed=4, frame=i,
+                          orb_cache=cache)
+        assert c["orb"][i] == len(cache[("L", i)][0]), i
+        assert c["orb"][B + 1 + i] == len(cache[("R", i)][0]), i
+        assert c["stereo"][i] == e["n_stereo"] and c["f_inliers"][i] == e["n_f"], i
+        assert np.array_equal(trk.f_mask[i, :e["n_stereo"]].cpu().numpy().astype(bool), e["f_mask"])
+        X = trk.X[i, :e["n_f"]].cpu().numpy()
+        assert np.all(np.abs(X - e["X"]) <= 1e-9 * np.maximum(1, np.abs(e["X"])))
+        assert c["temporal"][i] == e["n_temporal"], i
+        assert int(n[i]) == e["n_pnp"], i
+        assert np.allclose(rv[i].cpu().numpy(), e["rvec"], rtol=0, atol=1e-8)
+        assert np.allclose(tv[i].cpu().numpy(), e["tvec"], rtol=0, atol=1e-8)
+        erv.append(e["rvec"]), etv.append(e["tvec"]), en.append(e["n_pnp"])
+    Ph, _ = chain_poses(np.eye(4), np.array(erv), np.array(etv), np.array(en))
+    assert np.allclose(P, Ph, rtol=0, atol=1e-8)
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[i + 1] for i in range(B)])
+    assert np.abs(P[:, :3, 3] - gt[:, :3, 3]).max() < 0.5

@@ -143,3 +143,49 @@ def test_gpu_solver_never_worse_than_reference(g):
     assert np.allclose(rf, op.objective(x), rtol=1e-10, atol=1e-9)
     ref = _scipy_trf(x0, 1e-1)
     assert cost <= 10.0 * ref.cost + 1e-6
+
+
+# ----------------------------------------------------------------------------- BASELINE C5 loop
+@pytest.fixture(scope="module")
+def loop500():
+    """BASELINE config 5's pose-graph half: a 500-keyframe loop (3000 params,
+    502 residuals) with tracking drift (slam355.synthetic.pose_chain_loop)."""
+    from slam355.synthetic import pose_chain_loop
+
+    return pose_chain_loop(np.random.default_rng(5), 500)
+
+
+def test_oracle_loop500_closes_without_drift_and_jacobian(loop500):
+    from slam355.synthetic import pose_chain_loop
+
+    exact = pose_chain_loop(np.random.default_rng(0), 500, rot_s=0.0, t_s=0.0)
+    r = op.objective(exact)
+    assert r[-2] < 1e-6 and r[-1] < 1e-6  # the drift-free loop closes
+    r = op.objective(loop500)
+    assert r[-2] > 10.0 and r[-1] > 10.0  # the drifted one does not
+    J = op.jacobian(loop500)
+    eps = 1e-7
+    for k in (0, 4, 1501, 2998):  # a few columns against central differences
+        e = np.zeros_like(loop500)
+        e[k] = eps
+        Jn = (op.objective(loop500 + e) - op.objective(loop500 - e)) / (2 * eps)
+        assert np.abs(J[:, k] - Jn).max() <= 1e-6 * max(1.0, np.abs(Jn).max()), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nfev", [5, 12, 20])  # first step accepted at nfev 9; cost 1.8e7 -> 6.6e3
+def test_gpu_trf_500_keyframe_loop_follows_scipy(loop500, nfev):
+    """VERDICT r3 #1 (C5 pose-graph half at 500 keyframes): k_chain_trf on the
+    3000-parameter loop against scipy's TRF (x_scale='jac', exact subproblem,
+    the oracle's analytic Jacobian) after the same number of function
+    evaluations: nfev, parameters and cost."""
+    from slam355.posegraph import PoseChain
+
+    ref = _scipy_trf(loop500, 1e-8, max_nfev=nfev)
+    pc = PoseChain(loop500)
+    s = pc.solve(ftol=1e-8, max_nfev=nfev)
+    assert s["nfev"] == ref.nfev
+    assert abs(s["cost"] - ref.cost) <= 1e-7 * ref.cost
+    assert np.allclose(pc.params(), ref.x, rtol=1e-7, atol=1e-8)
+    if nfev >= 12:
+        assert s["cost"] < 0.1 * float(op.objective(loop500) @ op.objective(loop500))
