@@ -22,6 +22,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -211,8 +212,8 @@ class FrameFeed:
                             device="cuda" if resident else "cpu")
         if not resident:
             packs = packs.pin_memory()
-        for w in range(n_windows):
-            f0 = w * B
+        for w in range(n_windows):  # L, R: window w's B + 1 frames at rows w * (B + 1) ..
+            f0 = w * (B + 1)
             packs[w, :B + 1] = L[f0:f0 + B + 1].to(packs.device)
             packs[w, B + 1:] = R[f0:f0 + B].to(packs.device)
         self.packs = packs
@@ -283,10 +284,16 @@ def run_tracking(args, world, rank):
 
     B = args.batch
     n_win = args.windows
-    # the sequence: n_win distinct batches of B frame pairs, rendered on the GPU
-    # once (untimed), then held in pinned host memory and streamed back
-    L, R, poses, rig = corridor_sequence(n_win * B + 1, W_IMG, H_IMG, seed=1000 + rank,
-                                         device="cuda", as_numpy=False)
+    # ONE sequence over all ranks: n_win global steps of world * B consecutive
+    # frame pairs; rank r tracks pairs r*B .. r*B + B - 1 of every global step
+    # (frame-pair shards, main.py:79-97), so its window w starts at frame
+    # (w * world + r) * B.  Each rank renders only its own frames on the GPU
+    # (untimed; per-frame seeded noise, so the images do not depend on the world
+    # size) and keeps them resident in HBM.
+    f0s = [(w * world + rank) * B for w in range(n_win)]
+    ids = [f0 + i for f0 in f0s for i in range(B + 1)]
+    L, R, poses, rig = corridor_sequence(n_win * world * B + 1, W_IMG, H_IMG, seed=1000,
+                                         device="cuda", as_numpy=False, frames=ids)
     feed = FrameFeed(L, R, B, n_win, resident=True)
     # the PCIe-inclusive variant (reported beside `value`, never as it): the same
     # sequence streamed from pinned host memory inside its own timed region
@@ -295,6 +302,14 @@ def run_tracking(args, world, rank):
     CPU_PAIRS = 16  # cpu_baseline sample: 16 frame pairs + 16 LM iterations (~10 s of host work)
     L_np, R_np = L[:CPU_PAIRS + 1].cpu().numpy(), R[:CPU_PAIRS].cpu().numpy()
     del L, R
+    # the global trajectory of the shards (world > 1): one all-gather of the
+    # step's PnP results + the device pose chain over all world * B pairs, every
+    # step, inside the timed region (slam355.dist.GlobalChain)
+    gchain = None
+    if world > 1:
+        from slam355.dist import GlobalChain
+
+        gchain = GlobalChain(B, world, torch.device("cuda", torch.cuda.current_device()))
     n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     if args.ba_cus:  # disjoint CU sets: tracking on [0, n - ba_cus), local BA on the rest
         args.track_cus = n_cu - args.ba_cus
@@ -325,7 +340,9 @@ def run_tracking(args, world, rank):
         from slam355 import _lib as slib
 
         slib.lib.slam_hamming_force_valu(1)
-    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=rank,
+    # the same RANSAC seed on every rank: each pair's draws follow its global
+    # frame index (item0), so a pair tracks alike whichever rank holds it
+    trk = Tracker(B, H_IMG, W_IMG, rig.P_l, rig.P_r, max_kp_per_tile=args.kp_per_tile, seed=0,
                   stream=trk_stream, orb_stream=orb_stream)
     rng = np.random.default_rng(2000 + rank)
     C3 = (10, 5000, 6)
@@ -396,12 +413,18 @@ def run_tracking(args, world, rank):
         imgs, win = fd.next(ist)
         h0 = trk._ht("upload_issue", h0)
         if win == 0:  # a new pass over the sequence starts at frame 0
-            trk.reset_chain()
+            if gchain is None:
+                trk.reset_chain()
+            else:
+                gchain.reset(tstream)
             h0 = trk._ht("reset_chain", h0)
         if args.ba_overlap == "after-orb" and ba_done[0] is not None:
             ist.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
-        trk.track(win * B, imgs=imgs, marks=tmarks)
+        trk.track(f0s[win], imgs=imgs, marks=tmarks, chain=gchain is None)
         h0 = time.perf_counter()
+        if gchain is not None:
+            gchain.step(trk.rvec, trk.tvec, trk.p_ninl, tstream)
+            h0 = trk._ht("global_chain", h0)
         fd.release(ist)
         if tmarks is not None and orb_stream is not None:
             marks["orb"] = trk.orb_marks  # ORB's own stream: start -> done there
@@ -473,9 +496,10 @@ def run_tracking(args, world, rank):
     # accuracy of the tracked trajectory (the last tracked window; the device
     # chain restarts at frame 0 of the sequence with window 0) against ground truth
     last_win = (args.warmup + args.steps - 1) % n_win
-    est = trk.poses.cpu().numpy()
-    f0 = last_win * B
-    gt = np.stack([np.linalg.inv(poses[0]) @ poses[f0 + i + 1] for i in range(B)])
+    # the chain of the last global step: world * B poses from frame last_win*world*B
+    est = (trk.poses if gchain is None else gchain.poses).cpu().numpy()
+    f0 = last_win * world * B
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[f0 + i + 1] for i in range(world * B)])
     t_err = np.linalg.norm(est[:, :3, 3] - gt[:, :3, 3], axis=1)
     # drift inside the window, relative to its first tracked frame
     rel_e = np.stack([np.linalg.inv(est[0]) @ e for e in est])
@@ -539,8 +563,8 @@ def run_tracking(args, world, rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8+f32+f64",
-        "data": (f"synthetic (seeded textured-corridor stereo sequence, {n_win * B + 1} frames "
-                 "1280x720 resident in HBM; GT poses)"),
+        "data": (f"synthetic (seeded textured-corridor stereo sequence, {n_win * world * B + 1} "
+                 f"frames 1280x720, each rank's {n_win} windows resident in its HBM; GT poses)"),
         "config": {"workload": f"C2 tracking (1280x720, {args.kp_per_tile} ORB kp/tile) + "
                                f"C3 local BA (10 KF x 5k pts x 30k obs) every {args.ba_every} frames "
                                f"x {args.ba_iters} LM iters ({n_solves} windows per step, batched" +
@@ -574,7 +598,13 @@ def run_tracking(args, world, rank):
                      "pnp_inliers_mean": float(np.mean(cnt["pnp_inliers"])),
                      "trajectory_t_err_m_max_from_frame0": float(t_err.max()),
                      "trajectory_t_err_m_max_in_window": float(t_err_win.max()),
-                     "frames_chained": int(f0 + B)},
+                     "frames_chained": int(f0 + world * B),
+                     "trajectory": ("one sequence, frame-pair shards, gathered and chained on "
+                                    "every rank each step (slam355.dist.GlobalChain)"
+                                    if world > 1 else "one sequence, device pose chain"),
+                     # bytes of the last global step's chained poses: equal across world
+                     # sizes with equal world * batch (the same pairs per global step)
+                     "trajectory_sha1": hashlib.sha1(np.ascontiguousarray(est).tobytes()).hexdigest()},
     }
     if pcie is not None:
         rec["pcie_inclusive"] = pcie
@@ -1063,8 +1093,8 @@ def main():
                     help="ORB max_number_of_kp per tile: 64 -> ~2090 kp/frame (levels 6-7 of a "
                          "216x192 patch cannot hold keypoints, so 56 gives only ~1780)")
     ap.add_argument("--windows", type=int, default=None,
-                    help="distinct tracking batches in the streamed sequence (default: 256 / "
-                         "batch, at least 2: a 257-frame sequence at batch 32 or 64)")
+                    help="global steps in the sequence, each gpus x batch frame pairs (default: "
+                         "256 / (gpus x batch), at least 2: a 257-frame sequence at 1 GPU, batch 64)")
     ap.add_argument("--keep-poses", action="store_true")
     ap.add_argument("--ba-every", type=int, default=8, help="frames per local-BA solve")
     ap.add_argument("--ba-iters", type=int, default=10, help="LM iterations per local-BA solve")
@@ -1128,8 +1158,8 @@ def main():
     args = ap.parse_args()
     if args.batch is None:
         args.batch = 64 if args.workload == "tracking" else 32
-    if args.windows is None:
-        args.windows = max(2, 256 // args.batch)
+    if args.windows is None:  # global steps in the sequence (each world * batch pairs)
+        args.windows = max(2, 256 // (args.batch * args.gpus))
     if args.ba_group is None:  # the fewest steps whose windows fill one batched launch
         args.ba_group = max(1, -(-16 // max(1, args.batch // args.ba_every)))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:

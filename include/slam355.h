@@ -428,6 +428,33 @@ int slam_orb_set_lds_floor(int bytes);
 int slam_count_min(const int32_t* d_count, int n, int32_t* d_min, void* stream);
 int slam_ba_reset_batch(const slam_ba_problem* probs, int n_probs, double lambda0, void* stream);
 
+/* ------------------------------------------------------------------ collectives
+ * The sharded local BA (replaces the one serial least_squares
+ * call of BundleAdjustment.py:397-402 at C4 / C5 scale): each rank holds the
+ * observations of its landmark shard and all cameras; per LM iteration the
+ * packed reduced camera system and the 4-double trial buffer are summed over
+ * the ranks.  RCCL (over xGMI) is loaded at the first slam_comm_* call
+ * (dlopen "librccl.so.1", or SLAM_RCCL_LIB, or an RCCL already exporting the
+ * nccl* symbols globally).  One rank per GPU; the communicator is used from
+ * one host thread at a time. */
+#define SLAM_COMM_ID_BYTES 128
+typedef struct slam_comm_opaque* slam_comm_t;
+/* Rank 0 creates the id (h_id: SLAM_COMM_ID_BYTES host bytes) and sends it to
+ * the other ranks out of band (torch.distributed broadcast, MPI, a file). */
+int slam_comm_unique_id(void* h_id);
+/* Collective over the nranks processes (ncclCommInitRank); the current HIP
+ * device is this rank's GPU. */
+int slam_comm_init(int nranks, int rank, const void* h_id, slam_comm_t* comm);
+int slam_comm_destroy(slam_comm_t comm);
+/* In-place sum over the ranks of d_buf[0..n) (f64), async on stream. */
+int slam_comm_allreduce_f64(slam_comm_t comm, double* d_buf, long long n, void* stream);
+/* One LM iteration of a landmark-sharded problem (every rank calls it on its
+ * shard; prob built with the GLOBAL problem's packed block list): phase 1,
+ * all-reduce of prob->sys (slam_ba_sys_len doubles), phase 2, all-reduce of
+ * prob->small (4 doubles), phase 3 -- all on `stream`, no host sync.  With
+ * nranks = 1 it equals slam_ba_iterate(prob, 1, stream). */
+int slam_ba_step_distributed(const slam_ba_problem* prob, slam_comm_t comm, void* stream);
+
 /* ------------------------------------------------------------------ pose chain
  * The live pose-chain optimisation of BundleAdjustment.py:79-183 (loop
  * closure): m relative poses [r0 r1 r2 t0 t1 t2] (cv2.Rodrigues rotation

@@ -1595,8 +1595,9 @@ struct TlLayout {  // doubles inside p.chol
     fail = nz + ((long long)T * T + 7) / 8;
     xo = fail + 8;                       // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
     fc = xo + N;                         // k_tl3_flow: x in camera order; [T][T][64] L_Ik y_k
-    flow = fc + (long long)T * T * kTB;  // (forward-substitution terms), then int flags:
-    total = flow + ((long long)T * T + 2 * T + 8 + 1) / 2;  // tile[T][T], y[T], x[T], ticket, epoch
+    flow = fc + (long long)T * T * kTB;  // (forward-substitution terms), then ints: flags
+    // tile[T][T], y[T], x[T]; ticket, epoch, start ticket (+5 spare); retired parents cnt[T]
+    total = flow + ((long long)T * T + 3 * T + 8 + 1) / 2;
   }
 };
 
@@ -1884,12 +1885,17 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p) {
     p.chol[L.b + I * kTB + threadIdx.x] =
         r < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
   }
-  if (idx == 0 && threadIdx.x == 0) {
-    *reinterpret_cast<int*>(p.chol + L.fail) = 0;
-    // k_tl3_flow: a new solve epoch (its flags compare against it), ticket re-armed
+  if (idx == 0) {
+    // k_tl3_flow: a new solve epoch (its flags compare against it); the retire
+    // ticket, the start ticket and the per-column parent counters re-armed
     int* fl = reinterpret_cast<int*>(p.chol + L.flow) + L.T * L.T + 2 * L.T;
-    fl[0] = 0;
-    fl[1] = fl[1] + 1;
+    for (int i = threadIdx.x; i < L.T; i += blockDim.x) fl[8 + i] = 0;
+    if (threadIdx.x == 0) {
+      *reinterpret_cast<int*>(p.chol + L.fail) = 0;
+      fl[0] = 0;
+      fl[1] = fl[1] + 1;
+      fl[2] = 0;
+    }
   }
 }
 
@@ -2096,15 +2102,24 @@ __global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
 //   (5) the last column to finish (ticket) runs the solve epilogue.
 // Launch boundaries become device flags: a column starts as soon as the tiles
 // it needs exist, so the factor advances along the elimination tree with no
-// per-level launch gaps.  Data crossing workgroups (L tiles, y, x) is written
-// with sc1 (write-through) stores and read with sc1 loads; a flag is raised
-// after the writer's stores have drained (s_waitcnt + barrier) and equals the
-// solve's epoch (bumped by k_tl2_load), so flags never need clearing.  Steps
-// (1)-(3) wait only on earlier columns; (4) waits on later ones, which is safe
-// because all T <= SLAM_TL_FLOW_MAX_T workgroups are resident together (one per
-// CU; the host checks T against the CU count).  Every wait gives up when the
-// solve failed (non-SPD tile) or after kFlowSpinMax polls (then it marks the
-// solve failed), so every workgroup reaches the ticket and exits.
+// per-level launch gaps.  Data crossing workgroups (L tiles, L_JJ^-1, y, x) is
+// written with sc1 (write-through) stores and read with sc1 loads; a flag is
+// raised after the writer's stores have drained (s_waitcnt + barrier) and
+// equals the solve's epoch (bumped by k_tl2_load), so flags never need clearing.
+// No residency assumption: a workgroup takes its column from a start
+// ticket, so the columns are handed out in the order the workgroups actually
+// start, and steps (1)-(3) wait only on lower columns -- workgroups that have
+// already started and cannot be descheduled.  The back substitution (4) never
+// waits on a later column: x_J is computed by the workgroup that retires the
+// LAST of J's row tiles' x (a per-column counter; the roots by their own
+// workgroup), so a column whose workgroup finished its forward part long ago,
+// or a workgroup that has not started yet, holds nothing up.  The solve is
+// therefore correct with any number of its workgroups resident (a CU-masked
+// stream, other streams' kernels holding the CUs), and bit-identical whichever
+// workgroup computes a column.  Every wait still gives up when the solve failed
+// (non-SPD tile) or after kFlowSpinMax polls (a safety net that then marks the
+// solve failed: SOLVE_FAULT), and every column is retired exactly once, so the
+// retire ticket always reaches T and its last adder runs the epilogue.
 constexpr int kFlowSpinMax = 1 << 22;  // ~0.2 s of 128-cycle polls
 
 #ifdef SLAM_FLOW_PROFILE
@@ -2120,7 +2135,7 @@ __device__ unsigned long long g_flow_stamp[SLAM_TL_FLOW_MAX_T][8];
 #endif
 
 struct FlowPtrs {
-  int *tile, *yf, *xf, *ticket, *epoch;
+  int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt;
   __device__ FlowPtrs(const slam_ba_problem& p, const TlLayout& L) {
     int* base = reinterpret_cast<int*>(p.chol + L.flow);
     tile = base;
@@ -2128,6 +2143,8 @@ struct FlowPtrs {
     xf = yf + L.T;
     ticket = xf + L.T;
     epoch = ticket + 1;
+    start = ticket + 2;
+    cnt = ticket + 8;
   }
 };
 
@@ -2195,6 +2212,40 @@ __device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int
   return ok;
 }
 
+// Before x_k is formed from bytes other workgroups published: wave 0 polls
+// y_k's flag, the x flag of every row tile I of column k and the flags of the
+// tiles L_Ik (all up in a good solve: one round trip).  krc <= 31 (host-checked).
+__device__ bool flow_wait_back(const FlowPtrs& F, const int32_t* rows, int krc, int k, int T,
+                               int epoch, int* fail, int* sh) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int* f = nullptr;
+    if (lane < krc) f = F.xf + rows[lane];
+    else if (lane >= 32 && lane - 32 < krc) f = F.tile + rows[lane - 32] * T + k;
+    else if (lane == 31) f = F.yf + k;
+    int ok = 1;
+    for (int spins = 0;; ++spins) {
+      const bool up = f == nullptr || ld_flag(f) == epoch;
+      if (__all(up)) break;
+      if (ld_flag(fail) != 0) {
+        ok = 0;
+        break;
+      }
+      if (spins > kFlowSpinMax) {
+        if (lane == 0) st_flag(fail, 2);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) *sh = ok;
+  }
+  __syncthreads();
+  const bool ok = *sh != 0;
+  __syncthreads();
+  return ok;
+}
+
 // every thread's (sc1) stores drained, then thread 0 raises the flag
 __device__ __forceinline__ void flow_publish(int* flag, int epoch) {
   __builtin_amdgcn_s_waitcnt(0);
@@ -2234,18 +2285,24 @@ void k_tl3_flow(slam_ba_problem p) {
   const int n = 9 * p.n_cams;
   const TlLayout L(n);
   const int32_t* S = p.tl_sched;
-  const int T = L.T, J = blockIdx.x;
-  const int32_t* rec = S + S[5] + 5 * J;
-  const int ro = rec[0], rc = rec[1], so = rec[2], sc = rec[3], uo = rec[4];
+  const int T = L.T;
   const FlowPtrs F(p, L);
-  int* fail = reinterpret_cast<int*>(p.chol + L.fail);
-  const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
   __shared__ double VX[2 * kTB * kTB];  // factor scratch; then L_JJ^-1 (fragments) | operand Y
   __shared__ double Xf[kTB * kTB];      // operand X
   __shared__ double part[4][kTB];
   __shared__ double yv[kTB];
   __shared__ double rv[kTB];
-  __shared__ int shf, okf;
+  __shared__ int shf, okf, col_sh;
+  __shared__ int stk[SLAM_TL_FLOW_MAX_T], sp_sh, cur_sh, last_sh;
+  // the column: the start ticket hands them out in the order the workgroups start
+  if (threadIdx.x == 0)
+    col_sh = (int)ticket_add(reinterpret_cast<uint32_t*>(F.start));
+  __syncthreads();
+  const int J = col_sh;
+  const int32_t* rec = S + S[5] + 5 * J;
+  const int ro = rec[0], rc = rec[1], so = rec[2], sc = rec[3], uo = rec[4];
+  int* fail = reinterpret_cast<int*>(p.chol + L.fail);
+  const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
   double* A = p.chol + L.a;
   double* Vf = VX;
   double* Yf = VX + kTB * kTB;
@@ -2319,10 +2376,10 @@ void k_tl3_flow(slam_ba_problem p) {
     if (!ok) {
       if (t == 0) st_flag(fail, 1);
     } else if (w == 1) {
-      double* V = p.chol + L.dinv + (size_t)J * kTB * kTB;
+      double* V = p.chol + L.dinv + (size_t)J * kTB * kTB;  // read back by (3) and by (4)'s
 #pragma unroll
-      for (int m = 0; m < kTB; ++m) {
-        V[m * kTB + lane] = x[m];
+      for (int m = 0; m < kTB; ++m) {                        // workgroup, maybe another one
+        st_sc1(V + m * kTB + lane, x[m]);
         Vf[frag_idx(m, lane)] = x[m];
       }
     }
@@ -2390,10 +2447,13 @@ void k_tl3_flow(slam_ba_problem p) {
     __syncthreads();
     // y_J[m] = sum_c L_JJ^-1[m][c] r[c]: thread (w, m) sums c in [16w, 16w + 16)
     double s3 = 0.0;
-    for (int c = 16 * w; c < 16 * w + 16; ++c) s3 = __builtin_fma(Vkk[lane * kTB + c], rv[c], s3);
+    for (int c = 16 * w; c < 16 * w + 16; ++c) s3 = __builtin_fma(ld_sc1(Vkk + lane * kTB + c), rv[c], s3);
     part[w][lane] = s3;
     __syncthreads();
-    if (t < kTB) yv[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+    if (t < kTB) {
+      yv[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+      st_sc1(p.chol + L.y + J * kTB + t, yv[t]);  // for the workgroup that forms x_J
+    }
     __syncthreads();
     for (int q = 0; q < rc; ++q) {
       const int I = S[ro + q];
@@ -2414,50 +2474,76 @@ void k_tl3_flow(slam_ba_problem p) {
     flow_publish(F.yf + J, epoch);
   }
   FLOW_T(4);
-  // (4) back substitution: thread (w, c = lane) sums rows [16w, 16w + 16)
-  if (ok) {
-    double s2 = 0.0;
-    for (int q = 0; q < rc && ok; ++q) {
-      const int I = S[ro + q];
-      ok = flow_wait(F.xf + I, epoch, fail, &shf);
-      if (!ok) break;
-      const double* LIJ = A + (size_t)(I * kTB + 16 * w) * L.N + J * kTB + lane;
-      const double* xI = p.chol + L.x + I * kTB + 16 * w;
-      double la[16], xa[16];
+  // (4) back substitution, last-arriver form: x_k = L_kk^-T (y_k - sum_I L_Ik^T
+  // x_I) over the row tiles I of column k.  Column k is pushed onto this
+  // workgroup's stack when it is a root (its own column) or when this workgroup
+  // retired the last of k's row tiles (cnt[k] reaches rows(k)); thread (w, c =
+  // lane) sums rows [16w, 16w + 16) of every I in row order -- the operations
+  // and their order do not depend on which workgroup forms x_k.
+  if (t == 0) {
+    sp_sh = 0;
+    last_sh = 0;
+    if (rc == 0) stk[sp_sh++] = J;
+  }
+  __syncthreads();
+  for (;;) {
+    if (t == 0) cur_sh = sp_sh > 0 ? stk[--sp_sh] : -1;
+    __syncthreads();
+    const int k = cur_sh;
+    if (k < 0) break;
+    const int32_t* rk = S + S[5] + 5 * k;
+    const int kro = rk[0], krc = rk[1], kso = rk[2], ksc = rk[3];
+    const bool okk = flow_wait_back(F, S + kro, krc, k, T, epoch, fail, &shf);
+    if (okk) {
+      if (t < kTB) yv[t] = ld_sc1(p.chol + L.y + k * kTB + t);
+      double s2 = 0.0;
+      for (int q = 0; q < krc; ++q) {
+        const int I = S[kro + q];
+        const double* LIk = A + (size_t)(I * kTB + 16 * w) * L.N + k * kTB + lane;
+        const double* xI = p.chol + L.x + I * kTB + 16 * w;
+        double la[16], xa[16];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        la[m] = ld_sc1(LIJ + (size_t)m * L.N);
-        xa[m] = ld_sc1(xI + m);
+        for (int m = 0; m < 16; ++m) {
+          la[m] = ld_sc1(LIk + (size_t)m * L.N);
+          xa[m] = ld_sc1(xI + m);
+        }
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s2 = __builtin_fma(la[m], xa[m], s2);
       }
-#pragma unroll
-      for (int m = 0; m < 16; ++m) s2 = __builtin_fma(la[m], xa[m], s2);
-    }
-    FLOW_T(5);
-    if (ok) {
+      FLOW_T(5);
       part[w][lane] = s2;
       __syncthreads();
       if (t < kTB) rv[t] = yv[t] - (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
       __syncthreads();
-      double s3 = 0.0;  // x_J[c] = sum_m L_JJ^-1[m][c] r[m]
-      for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(Vkk[m * kTB + lane], rv[m], s3);
+      const double* Vk = p.chol + L.dinv + (size_t)k * kTB * kTB;
+      double s3 = 0.0;  // x_k[c] = sum_m L_kk^-1[m][c] r[m]
+      for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(ld_sc1(Vk + m * kTB + lane), rv[m], s3);
+      __syncthreads();  // rv / part reads done before part is rewritten
       part[w][lane] = s3;
       __syncthreads();
       if (t < kTB) {
         const double xv = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-        st_sc1(p.chol + L.x + J * kTB + t, xv);
-        const int orow = S[S[3] + J] * kTB + t;  // camera order (padded rows dropped)
+        st_sc1(p.chol + L.x + k * kTB + t, xv);
+        const int orow = S[S[3] + k] * kTB + t;  // camera order (padded rows dropped)
         if (orow < n) st_sc1(p.chol + L.xo + orow, xv);
       }
-      flow_publish(F.xf + J, epoch);
     }
+    // retire column k even when the solve failed (every column is retired once:
+    // the counters and the ticket still complete, the epilogue sees the fail code)
+    flow_publish(F.xf + k, epoch);
+    if (t == 0) {
+      for (int u = 0; u < ksc; ++u) {
+        const int c = S[kso + u];  // k is a row tile of column c
+        const int rcc = S[S[5] + 5 * c + 1];
+        if ((int)ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c)) == rcc - 1) stk[sp_sh++] = c;
+      }
+      if (ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1)) last_sh = 1;
+    }
+    __syncthreads();
   }
   FLOW_T(6);
-  // (5) ticket: the last column runs the epilogue
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (t == 0) okf = ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1);
-  __syncthreads();
-  if (!okf) return;
+  // (5) the workgroup that retired the last column runs the epilogue
+  if (!last_sh) return;
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
   const bool good = fcode == 0;
   double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
@@ -2470,35 +2556,19 @@ void k_tl3_flow(slam_ba_problem p) {
   FLOW_T(7);
 }
 
-static int g_cu_count = 0;
-
-// The dataflow solve needs its T workgroups resident together (one per CU):
-// T must not exceed the CUs the stream may use (a CU-masked stream counts only
-// its mask).  Otherwise the level-scheduled launches run instead.  (Kernels of
-// other streams can still hold CUs for a while; a wait that outlasts
-// kFlowSpinMax marks the solve failed with code 2, which the Python layer
-// turns into an error: SLAM_BA_ST_SOLVE_FAULT.)
-static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t s) {
+// The dataflow solve makes no residency assumption (k_tl3_flow's comment), so it
+// runs on any stream, CU-masked or not, beside any other work.  It needs the
+// column count within its LDS stack (SLAM_TL_FLOW_MAX_T), at most 31 row tiles
+// per column (flow_wait_back polls them in one wave) and the camera-order x of
+// the epilogue in its LDS scratch; otherwise (or with tl_mode "levels") the
+// level-scheduled launches run.
+static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t) {
   if (p.tl_mode != 0 || p.tl_sched_host == nullptr || p.tl_sched_host[5] <= 0) return false;
-  if (g_cu_count == 0) {
-    int dev = 0, cu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      cu = -1;
-    g_cu_count = cu;
-  }
   const TlLayout L(9 * p.n_cams);
-  if (!(L.T <= SLAM_TL_FLOW_MAX_T && L.T <= g_cu_count && 9 * p.n_cams <= 2 * kTB * kTB))
-    return false;
-  if (s != nullptr) {
-    uint32_t mask[16] = {};
-    const int words = min(16, (g_cu_count + 31) / 32);
-    if (hipExtStreamGetCUMask(s, (uint32_t)words, mask) == hipSuccess) {
-      int n = 0;
-      for (int w = 0; w < words; ++w) n += __builtin_popcount(mask[w]);
-      if (n > 0 && L.T > n) return false;
-    }
-  }
+  if (!(L.T <= SLAM_TL_FLOW_MAX_T && 9 * p.n_cams <= 2 * kTB * kTB)) return false;
+  const int32_t* h = p.tl_sched_host;
+  for (int J = 0; J < L.T; ++J)
+    if (h[h[5] + 5 * J + 1] > 31) return false;
   return true;
 }
 

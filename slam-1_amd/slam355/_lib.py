@@ -118,6 +118,11 @@ SIGNATURES = {
     "slam_triangulate_f32": [c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p],
     "slam_pose_chain_trf": [c_p, c_int, c_int, c_int, c_int, c_double, c_double, c_double, c_int,
                             c_p, c_p],
+    "slam_comm_unique_id": [c_p],
+    "slam_comm_init": [c_int, c_int, c_p, ctypes.POINTER(c_p)],
+    "slam_comm_destroy": [c_p],
+    "slam_comm_allreduce_f64": [c_p, c_p, ctypes.c_longlong, c_p],
+    "slam_ba_step_distributed": [_PROB, c_p, c_p],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
             "slam_ba_chol_len": ctypes.c_longlong, "slam_pnp_workspace_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}

@@ -782,7 +782,7 @@ class BAProblem:
             graphs[name] = g
         return graphs[name]
 
-    def step_distributed(self, group=None, graphed=True):
+    def step_distributed(self, group=None, graphed=True, comm=None):
         """One LM iteration with RCCL all-reduce of the camera system (multi-rank).
 
         The kernels and the collectives are ordered on one stream: the body runs
@@ -791,6 +791,9 @@ class BAProblem:
         and the solve (tiled factor + k_back_trial) are each one HIP-graph
         replay, so an iteration is 2 graph launches + k_decide + 2 collectives
         instead of ~8 kernel launches."""
+        if comm is not None:  # slam355.dist.CapiComm: the whole iteration is one C call
+            _lib.call("slam_ba_step_distributed", ctypes.byref(self._s), comm.handle, self._sp())
+            return
         import torch.distributed as dist
 
         with torch.cuda.stream(self.stream if self.stream is not None

@@ -76,3 +76,109 @@ def gather_pose_chain(rvec, tvec, ninl, pose0=None, T0=None, group=None):
     a = allb.numpy()
     poses, _ = chain_poses(p0, a[:, 0:3], a[:, 3:6], np.rint(a[:, 6]).astype(np.int64), t0)
     return torch.from_numpy(poses)
+
+
+class GlobalChain:
+    """The global trajectory of frame-pair shards, advanced every tracking step
+    (main.py:120-124 over all ranks' pairs): rank r of `world` tracked pairs
+    r*B .. r*B + B - 1 of the step's world*B consecutive pairs; the ranks
+    all-gather each pair's PnP result (rvec, tvec, n_inliers: 7 doubles) and
+    every rank chains the world*B results in frame order on the device
+    (k_pose_chain, the stale-T rule across shard boundaries included),
+    continuing a device-resident (pose, T) state from the previous step -- the
+    trajectory one Tracker over all pairs gives, bit for bit.  Asynchronous on
+    `stream` with the nccl (RCCL) backend; buffers are preallocated."""
+
+    def __init__(self, B, world, device, group=None):
+        import torch
+
+        self.B, self.world, self.group = B, world, group
+        f64 = dict(dtype=torch.float64, device=device)
+        self.buf = torch.empty((B, 7), **f64)
+        self.all = torch.empty((world * B, 7), **f64)
+        self.parts = [self.all[i * B:(i + 1) * B] for i in range(world)]
+        self.rv = torch.empty((world * B, 3), **f64)
+        self.tv = torch.empty((world * B, 3), **f64)
+        self.ni = torch.empty((world * B,), dtype=torch.int32, device=device)
+        self.state = torch.empty((32,), **f64)
+        self._eye = torch.as_tensor(np.concatenate([np.eye(4), np.eye(4)]).ravel(), **f64)
+        self.poses = torch.empty((world * B, 4, 4), **f64)
+
+    def reset(self, stream=None):
+        """Restart the chain at the identity (an async device copy on `stream`)."""
+        import torch
+
+        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+            self.state.copy_(self._eye, non_blocking=True)
+
+    def step(self, rvec, tvec, ninl, stream=None):
+        """Gather this step's shard results and chain the world*B pairs into
+        self.poses [world*B, 4, 4] (absolute poses of the step's frames 1..)."""
+        import torch
+        import torch.distributed as dist
+
+        from . import _lib
+        from .device import ptr, stream_ptr
+
+        st = stream if stream is not None else torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            self.buf[:, 0:3].copy_(rvec)
+            self.buf[:, 3:6].copy_(tvec)
+            self.buf[:, 6].copy_(ninl)
+            dist.all_gather(self.parts, self.buf, group=self.group)
+            self.rv.copy_(self.all[:, 0:3])
+            self.tv.copy_(self.all[:, 3:6])
+            self.ni.copy_(self.all[:, 6].round())
+            _lib.call("slam_pose_chain", ptr(self.rv), ptr(self.tv), ptr(self.ni),
+                      self.world * self.B, ptr(self.state), ptr(self.poses), stream_ptr(st))
+        return self.poses
+
+
+class CapiComm:
+    """An RCCL communicator of the C ABI (slam_comm_*; include/slam355.h) over
+    the ranks of a torch.distributed group: rank 0 creates the unique id, the
+    group broadcasts it (128 bytes), every rank joins.  BAProblem.
+    step_distributed(comm=...) then runs the sharded LM iteration as ONE C call
+    (slam_ba_step_distributed: build, all-reduce, solve, all-reduce, decide)."""
+
+    def __init__(self, group=None, single=False):
+        """single=True: a one-rank communicator with no torch.distributed group
+        (tests; a C caller's nranks = 1)."""
+        import ctypes
+
+        import torch
+
+        from . import _lib
+
+        idb = (ctypes.c_uint8 * 128)()
+        if single:
+            self.rank, self.world = 0, 1
+            _lib.call("slam_comm_unique_id", ctypes.cast(idb, ctypes.c_void_p))
+        else:
+            import torch.distributed as dist
+
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+            if self.rank == 0:
+                _lib.call("slam_comm_unique_id", ctypes.cast(idb, ctypes.c_void_p))
+            t = torch.tensor(list(bytes(idb)), dtype=torch.uint8)
+            if dist.get_backend(group) == "nccl":
+                t = t.cuda()
+            dist.broadcast(t, src=0, group=group)
+            idb = (ctypes.c_uint8 * 128)(*t.cpu().tolist())
+        self.handle = ctypes.c_void_p()
+        _lib.call("slam_comm_init", self.world, self.rank, ctypes.cast(idb, ctypes.c_void_p),
+                  ctypes.byref(self.handle))
+
+    def allreduce_(self, t, stream=None):
+        """In-place f64 sum of a contiguous device tensor over the ranks."""
+        from . import _lib
+        from .device import ptr, stream_ptr
+
+        _lib.call("slam_comm_allreduce_f64", self.handle, ptr(t), t.numel(), stream_ptr(stream))
+
+    def close(self):
+        from . import _lib
+
+        if self.handle:
+            _lib.call("slam_comm_destroy", self.handle)
+            self.handle = type(self.handle)()

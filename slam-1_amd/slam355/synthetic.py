@@ -336,22 +336,32 @@ def render_corridor(T_cw, rig: StereoRig, gen, x_offset=0.0, ss=2, noise=2.0, de
     return torch.clamp(torch.round(img), 0, 255).to(torch.uint8)
 
 
-def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=True, **geo):
+def corridor_sequence(n_frames, W=1280, H=720, seed=0, device="cpu", as_numpy=True, frames=None,
+                      **geo):
     """(left [F,H,W] u8, right [F,H,W] u8, poses [F,4,4] camera-to-world, rig) of
     the textured corridor; the trajectory is trajectory() (1 m/frame, yaw
     jitter 0.2 deg).  torch tensors on `device` unless as_numpy.  `geo`
-    overrides CORRIDOR entries (e.g. a coarser `cell` at 640x480)."""
+    overrides CORRIDOR entries (e.g. a coarser `cell` at 640x480).
+
+    frames: render only these frame indices (left/right hold them in that
+    order; poses stay the whole sequence's), each view's noise drawn from a
+    generator seeded by (seed, frame), so every subset of one sequence holds
+    the same images -- the ranks of a sharded run render only their own
+    frames.  (frames=None keeps the one sequential generator.)"""
     import torch
 
     rng = np.random.default_rng(seed)
     rig = StereoRig(W, H)
     poses = trajectory(rng, n_frames)
+    ids = list(range(n_frames)) if frames is None else [int(f) for f in frames]
     gen = torch.Generator(device=device).manual_seed(seed)
-    left = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
-    right = torch.empty((n_frames, H, W), dtype=torch.uint8, device=device)
-    for i in range(n_frames):
-        left[i] = render_corridor(poses[i], rig, gen, 0.0, device=device, **geo)
-        right[i] = render_corridor(poses[i], rig, gen, rig.baseline, device=device, **geo)
+    left = torch.empty((len(ids), H, W), dtype=torch.uint8, device=device)
+    right = torch.empty((len(ids), H, W), dtype=torch.uint8, device=device)
+    for k, i in enumerate(ids):
+        if frames is not None:
+            gen.manual_seed(seed * 1_000_003 + i)
+        left[k] = render_corridor(poses[i], rig, gen, 0.0, device=device, **geo)
+        right[k] = render_corridor(poses[i], rig, gen, rig.baseline, device=device, **geo)
     if as_numpy:
         return left.cpu().numpy(), right.cpu().numpy(), poses, rig
     return left, right, poses, rig

@@ -228,3 +228,109 @@ def test_gpu_gather_pose_chain_equals_device_chain(tmp_path):
     _lib.call("slam_pose_chain", ptr(trv), ptr(ttv), ptr(tni), n, ptr(state), ptr(poses),
               stream_ptr(None))
     assert np.array_equal(np.load(out), poses.cpu().numpy())
+
+
+# ---------------------------------------------------------------- one sequence over tracking shards
+def _track_shard_worker(rank, world, port, out, B, steps):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "slam-1_amd")]
+    import torch
+    import torch.distributed as dist
+    from slam355.dist import GlobalChain
+    from slam355.pipeline import Tracker
+    from slam355.synthetic import corridor_sequence
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    n = steps * world * B + 1
+    f0s = [(s * world + rank) * B for s in range(steps)]
+    ids = [f0 + i for f0 in f0s for i in range(B + 1)]
+    L, R, _, rig = corridor_sequence(n, 1280, 720, seed=77, device="cuda", as_numpy=False, frames=ids)
+    trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=0)
+    gc = GlobalChain(B, world, torch.device("cuda", 0))
+    gc.reset()
+    chains = []
+    for s in range(steps):
+        o = s * (B + 1)
+        imgs = torch.cat([L[o:o + B + 1], R[o:o + B]]).contiguous()
+        trk.track(f0s[s], imgs=imgs, chain=False)
+        chains.append(gc.step(trk.rvec, trk.tvec, trk.p_ninl).clone())
+    torch.cuda.synchronize()
+    if rank == 0:
+        np.save(out, torch.cat(chains).cpu().numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_tracking_shards_gather_one_trajectory(tmp_path):
+    """`--gpus N` tracking shards ONE sequence -- rank r tracks
+    pairs r*B.. of every global step, GlobalChain all-gathers the PnP results
+    and chains them on every rank each step.  Two ranks of B = 3 pairs (gloo on
+    one GPU) over two global steps give, bit for bit, the trajectory of one
+    Tracker of B = 6 pairs over the same frames (main.py:79-98, 120-124)."""
+    import torch
+    from slam355.pipeline import Tracker
+    from slam355.synthetic import corridor_sequence
+
+    B, world, steps = 3, 2, 2
+    out = str(tmp_path / "chain.npy")
+    mp.spawn(_track_shard_worker, args=(world, _free_port(), out, B, steps), nprocs=world, join=True)
+    got = np.load(out)
+    G = world * B
+    n = steps * G + 1
+    ids = [s * G + i for s in range(steps) for i in range(G + 1)]
+    L, R, poses, rig = corridor_sequence(n, 1280, 720, seed=77, device="cuda", as_numpy=False,
+                                         frames=ids)
+    trk = Tracker(G, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=0)
+    want = []
+    for s in range(steps):
+        o = s * (G + 1)
+        trk.track(s * G, imgs=torch.cat([L[o:o + G + 1], R[o:o + G]]).contiguous())
+        want.append(trk.poses.clone())
+    want = torch.cat(want).cpu().numpy()
+    assert np.array_equal(got, want)
+    gt = np.stack([np.linalg.inv(poses[0]) @ poses[i + 1] for i in range(steps * G)])
+    assert np.abs(want[:, :3, 3] - gt[:, :3, 3]).max() < 0.5
+
+
+# ---------------------------------------------------------------- C-ABI communicator (RCCL)
+def test_comm_unique_id_loads_rccl_lazily():
+    """slam_comm_unique_id resolves RCCL at run time (dlopen; no GPU needed for
+    the id) and fills SLAM_COMM_ID_BYTES bytes."""
+    import ctypes
+
+    from slam355 import _lib
+
+    b = (ctypes.c_uint8 * 128)()
+    _lib.call("slam_comm_unique_id", ctypes.cast(b, ctypes.c_void_p))
+    assert any(bytes(b))
+    with pytest.raises(_lib.SlamError):  # argument checks before any RCCL call
+        _lib.call("slam_comm_init", 2, 5, ctypes.cast(b, ctypes.c_void_p),
+                  ctypes.byref(ctypes.c_void_p()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,P,k", [(8, 600, 4), (30, 1500, 4)])
+def test_gpu_capi_comm_step_distributed_single_rank_equals_iterate(C, P, k):
+    """slam_ba_step_distributed (build, RCCL all-reduce of prob->sys, solve,
+    all-reduce of prob->small, decide: one C call) on a one-rank RCCL
+    communicator gives the single-process iterates bit for bit (dense and
+    packed / tiled systems)."""
+    from slam355.ba import BAProblem
+    from slam355.dist import CapiComm
+
+    c0, p0, ci, pi, qs = _problem(C, P, k)
+    a, b = BAProblem(c0, p0, ci, pi, qs), BAProblem(c0, p0, ci, pi, qs)
+    comm = CapiComm(single=True)
+    try:
+        for _ in range(4):
+            a.iterate(1)
+            b.step_distributed(comm=comm)
+            sa, sb = a.state(), b.state()
+            assert sa["COST_NEW"] == sb["COST_NEW"] and sa["LAMBDA"] == sb["LAMBDA"]
+        assert np.array_equal(a.params()[0], b.params()[0])
+    finally:
+        comm.close()
