@@ -1596,8 +1596,9 @@ struct TlLayout {  // doubles inside p.chol
     xo = fail + 8;                       // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
     fc = xo + N;                         // k_tl3_flow: x in camera order; [T][T][64] L_Ik y_k
     flow = fc + (long long)T * T * kTB;  // (forward-substitution terms), then ints: flags
-    // tile[T][T], y[T], x[T]; ticket, epoch, start ticket (+5 spare); retired parents cnt[T]
-    total = flow + ((long long)T * T + 3 * T + 8 + 1) / 2;
+    // tile[T][T], y[T], x[T]; ticket, epoch, start ticket (+5 spare); retired row
+    // tiles + waiter mark cnt[T]; L_JJ^-1 / y_J published dv[T]
+    total = flow + ((long long)T * T + 4 * T + 8 + 1) / 2;
   }
 };
 
@@ -1659,6 +1660,7 @@ __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayo
 // LDS [3][16][17] scratch.  Every wave must call it; returns false (uniform)
 // on a non-positive or non-finite pivot.
 constexpr int kMS = 65;   // row stride of M (odd: MFMA operand reads spread over banks)
+constexpr int kVR = 65;   // row stride of k_tl3_flow's row-major L_JJ^-1
 constexpr int kBS17 = 17; // row stride of a 16x16 block
 __device__ __forceinline__ int blk_id(int i, int j) { return i * (i + 1) / 2 + j; }
 
@@ -2135,7 +2137,7 @@ __device__ unsigned long long g_flow_stamp[SLAM_TL_FLOW_MAX_T][8];
 #endif
 
 struct FlowPtrs {
-  int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt;
+  int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt, *dv;
   __device__ FlowPtrs(const slam_ba_problem& p, const TlLayout& L) {
     int* base = reinterpret_cast<int*>(p.chol + L.flow);
     tile = base;
@@ -2145,6 +2147,7 @@ struct FlowPtrs {
     epoch = ticket + 1;
     start = ticket + 2;
     cnt = ticket + 8;
+    dv = cnt + L.T;
   }
 };
 
@@ -2212,38 +2215,37 @@ __device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int
   return ok;
 }
 
-// Before x_k is formed from bytes other workgroups published: wave 0 polls
-// y_k's flag, the x flag of every row tile I of column k and the flags of the
-// tiles L_Ik (all up in a good solve: one round trip).  krc <= 31 (host-checked).
-__device__ bool flow_wait_back(const FlowPtrs& F, const int32_t* rows, int krc, int k, int T,
-                               int epoch, int* fail, int* sh) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int* f = nullptr;
-    if (lane < krc) f = F.xf + rows[lane];
-    else if (lane >= 32 && lane - 32 < krc) f = F.tile + rows[lane - 32] * T + k;
-    else if (lane == 31) f = F.yf + k;
+// Thread 0 polls the parent counter of column J until its low half (retired row
+// tiles) reaches rc -- the retirers' x stores drained before their adds (the
+// counter is the acquire for those bytes); false (uniform) when the solve failed
+// or the wait timed out.
+__device__ bool flow_wait_count(const int* cnt, int rc, int* fail, int* sh) {
+  if (threadIdx.x == 0) {
     int ok = 1;
-    for (int spins = 0;; ++spins) {
-      const bool up = f == nullptr || ld_flag(f) == epoch;
-      if (__all(up)) break;
+    for (int spins = 0; (ld_flag(cnt) & 0xffff) < rc; ++spins) {
       if (ld_flag(fail) != 0) {
         ok = 0;
         break;
       }
       if (spins > kFlowSpinMax) {
-        if (lane == 0) st_flag(fail, 2);
+        st_flag(fail, 2);
         ok = 0;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
     }
-    if (lane == 0) *sh = ok;
+    *sh = ok;
   }
   __syncthreads();
   const bool ok = *sh != 0;
   __syncthreads();
   return ok;
+}
+
+// one flag, the same contract as flow_wait (its definition follows below)
+__device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh);
+__device__ __forceinline__ bool flow_wait_one(const int* flag, int epoch, int* fail, int* sh) {
+  return flow_wait(flag, epoch, fail, sh);
 }
 
 // every thread's (sc1) stores drained, then thread 0 raises the flag
@@ -2293,7 +2295,8 @@ void k_tl3_flow(slam_ba_problem p) {
   __shared__ double yv[kTB];
   __shared__ double rv[kTB];
   __shared__ int shf, okf, col_sh;
-  __shared__ int stk[SLAM_TL_FLOW_MAX_T], sp_sh, cur_sh, last_sh;
+  __shared__ double VR[kTB * kVR];        // L_JJ^-1 row-major (stride 65): (3), this column's x
+  __shared__ int stk[SLAM_TL_FLOW_MAX_T], sp_sh, cur_sh, last_sh, own_sh;
   // the column: the start ticket hands them out in the order the workgroups start
   if (threadIdx.x == 0)
     col_sh = (int)ticket_add(reinterpret_cast<uint32_t*>(F.start));
@@ -2306,7 +2309,6 @@ void k_tl3_flow(slam_ba_problem p) {
   double* A = p.chol + L.a;
   double* Vf = VX;
   double* Yf = VX + kTB * kTB;
-  const double* Vkk = p.chol + L.dinv + (size_t)J * kTB * kTB;  // L_JJ^-1, this column's own
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   bool ok = true;
   FLOW_T(0);
@@ -2376,11 +2378,10 @@ void k_tl3_flow(slam_ba_problem p) {
     if (!ok) {
       if (t == 0) st_flag(fail, 1);
     } else if (w == 1) {
-      double* V = p.chol + L.dinv + (size_t)J * kTB * kTB;  // read back by (3) and by (4)'s
 #pragma unroll
-      for (int m = 0; m < kTB; ++m) {                        // workgroup, maybe another one
-        st_sc1(V + m * kTB + lane, x[m]);
+      for (int m = 0; m < kTB; ++m) {
         Vf[frag_idx(m, lane)] = x[m];
+        VR[m * kVR + lane] = x[m];
       }
     }
     __syncthreads();
@@ -2447,13 +2448,10 @@ void k_tl3_flow(slam_ba_problem p) {
     __syncthreads();
     // y_J[m] = sum_c L_JJ^-1[m][c] r[c]: thread (w, m) sums c in [16w, 16w + 16)
     double s3 = 0.0;
-    for (int c = 16 * w; c < 16 * w + 16; ++c) s3 = __builtin_fma(ld_sc1(Vkk + lane * kTB + c), rv[c], s3);
+    for (int c = 16 * w; c < 16 * w + 16; ++c) s3 = __builtin_fma(VR[lane * kVR + c], rv[c], s3);
     part[w][lane] = s3;
     __syncthreads();
-    if (t < kTB) {
-      yv[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-      st_sc1(p.chol + L.y + J * kTB + t, yv[t]);  // for the workgroup that forms x_J
-    }
+    if (t < kTB) yv[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
     __syncthreads();
     for (int q = 0; q < rc; ++q) {
       const int I = S[ro + q];
@@ -2474,28 +2472,59 @@ void k_tl3_flow(slam_ba_problem p) {
     flow_publish(F.yf + J, epoch);
   }
   FLOW_T(4);
-  // (4) back substitution, last-arriver form: x_k = L_kk^-T (y_k - sum_I L_Ik^T
-  // x_I) over the row tiles I of column k.  Column k is pushed onto this
-  // workgroup's stack when it is a root (its own column) or when this workgroup
-  // retired the last of k's row tiles (cnt[k] reaches rows(k)); thread (w, c =
-  // lane) sums rows [16w, 16w + 16) of every I in row order -- the operations
-  // and their order do not depend on which workgroup forms x_k.
+  // (4) back substitution: x_k = L_kk^-T (y_k - sum_I L_Ik^T x_I) over the row
+  // tiles I of column k (thread (w, c = lane) sums rows [16w, 16w + 16) of every
+  // I in row order; the operations and their order do not depend on which
+  // workgroup forms x_k).  Who forms x_J:
+  //   a root (no row tiles): this workgroup, right away;
+  //   otherwise, once every workgroup of the grid has started (the start ticket
+  //   reached T: waiting can then hold up no one), this workgroup registers as
+  //   the waiter on cnt[J] (+2^16) and forms x_J when its row tiles' x are all
+  //   retired -- unless the last of them was retired before it registered;
+  //   else the workgroup that retires the last row tile of J (cnt[J] reaches
+  //   rows(J) with no waiter registered) pushes J on its own stack.
+  // So the columns run in parallel when the grid is resident, and a column whose
+  // workgroup cannot wait is still formed.  Every column is retired once: x
+  // flag, its children's counters, the retire ticket.
   if (t == 0) {
     sp_sh = 0;
     last_sh = 0;
-    if (rc == 0) stk[sp_sh++] = J;
+    own_sh = 0;
+    if (rc == 0) {
+      own_sh = 1;
+    } else if (ld_flag(F.start) >= T) {
+      const unsigned old = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(F.cnt + J), 1u << 16,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      own_sh = (int)(old & 0xffffu) < rc ? 2 : 0;
+    }
   }
   __syncthreads();
-  for (;;) {
-    if (t == 0) cur_sh = sp_sh > 0 ? stk[--sp_sh] : -1;
-    __syncthreads();
-    const int k = cur_sh;
-    if (k < 0) break;
+  if (!own_sh) {
+    // another workgroup forms x_J: L_JJ^-1 and y_J for it, published by dv[J]
+    double* V = p.chol + L.dinv + (size_t)J * kTB * kTB;
+    for (int e = t; e < kTB * kTB; e += kTlWG) st_sc1(V + e, VR[(e >> 6) * kVR + (e & 63)]);
+    if (t < kTB) st_sc1(p.chol + L.y + J * kTB + t, yv[t]);
+    flow_publish(F.dv + J, epoch);
+  }
+  for (int it = 0;; ++it) {
+    int k;
+    bool okk;
+    if (it == 0) {  // this workgroup's own column, when it forms it
+      if (!own_sh) continue;
+      k = J;
+      okk = ok && (own_sh == 1 || flow_wait_count(F.cnt + J, rc, fail, &shf));
+    } else {
+      if (t == 0) cur_sh = sp_sh > 0 ? stk[--sp_sh] : -1;
+      __syncthreads();
+      k = cur_sh;
+      if (k < 0) break;
+      okk = flow_wait_one(F.dv + k, epoch, fail, &shf);
+    }
+    const bool own = k == J;
     const int32_t* rk = S + S[5] + 5 * k;
     const int kro = rk[0], krc = rk[1], kso = rk[2], ksc = rk[3];
-    const bool okk = flow_wait_back(F, S + kro, krc, k, T, epoch, fail, &shf);
     if (okk) {
-      if (t < kTB) yv[t] = ld_sc1(p.chol + L.y + k * kTB + t);
+      if (!own && t < kTB) yv[t] = ld_sc1(p.chol + L.y + k * kTB + t);
       double s2 = 0.0;
       for (int q = 0; q < krc; ++q) {
         const int I = S[kro + q];
@@ -2515,9 +2544,13 @@ void k_tl3_flow(slam_ba_problem p) {
       __syncthreads();
       if (t < kTB) rv[t] = yv[t] - (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
       __syncthreads();
-      const double* Vk = p.chol + L.dinv + (size_t)k * kTB * kTB;
       double s3 = 0.0;  // x_k[c] = sum_m L_kk^-1[m][c] r[m]
-      for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(ld_sc1(Vk + m * kTB + lane), rv[m], s3);
+      if (own) {
+        for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(VR[m * kVR + lane], rv[m], s3);
+      } else {
+        const double* Vk = p.chol + L.dinv + (size_t)k * kTB * kTB;
+        for (int m = 16 * w; m < 16 * w + 16; ++m) s3 = __builtin_fma(ld_sc1(Vk + m * kTB + lane), rv[m], s3);
+      }
       __syncthreads();  // rv / part reads done before part is rewritten
       part[w][lane] = s3;
       __syncthreads();
@@ -2528,14 +2561,15 @@ void k_tl3_flow(slam_ba_problem p) {
         if (orow < n) st_sc1(p.chol + L.xo + orow, xv);
       }
     }
-    // retire column k even when the solve failed (every column is retired once:
-    // the counters and the ticket still complete, the epilogue sees the fail code)
+    // retire column k even when the solve failed (the counters and the ticket
+    // still complete; the epilogue sees the fail code)
     flow_publish(F.xf + k, epoch);
     if (t == 0) {
       for (int u = 0; u < ksc; ++u) {
         const int c = S[kso + u];  // k is a row tile of column c
         const int rcc = S[S[5] + 5 * c + 1];
-        if ((int)ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c)) == rcc - 1) stk[sp_sh++] = c;
+        const unsigned old = ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c));
+        if ((int)(old & 0xffffu) == rcc - 1 && (old >> 16) == 0) stk[sp_sh++] = c;
       }
       if (ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1)) last_sh = 1;
     }
@@ -2558,18 +2592,13 @@ void k_tl3_flow(slam_ba_problem p) {
 
 // The dataflow solve makes no residency assumption (k_tl3_flow's comment), so it
 // runs on any stream, CU-masked or not, beside any other work.  It needs the
-// column count within its LDS stack (SLAM_TL_FLOW_MAX_T), at most 31 row tiles
-// per column (flow_wait_back polls them in one wave) and the camera-order x of
-// the epilogue in its LDS scratch; otherwise (or with tl_mode "levels") the
-// level-scheduled launches run.
+// column count within its LDS stack (SLAM_TL_FLOW_MAX_T, < 2^16 for the parent
+// counters) and the camera-order x of the epilogue in its LDS scratch;
+// otherwise (or with tl_mode "levels") the level-scheduled launches run.
 static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t) {
   if (p.tl_mode != 0 || p.tl_sched_host == nullptr || p.tl_sched_host[5] <= 0) return false;
   const TlLayout L(9 * p.n_cams);
-  if (!(L.T <= SLAM_TL_FLOW_MAX_T && 9 * p.n_cams <= 2 * kTB * kTB)) return false;
-  const int32_t* h = p.tl_sched_host;
-  for (int J = 0; J < L.T; ++J)
-    if (h[h[5] + 5 * J + 1] > 31) return false;
-  return true;
+  return L.T <= SLAM_TL_FLOW_MAX_T && 9 * p.n_cams <= 2 * kTB * kTB;
 }
 
 static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
