@@ -289,7 +289,9 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
 #define SLAM_BA_ST_NACCEPT 9
 #define SLAM_BA_ST_PRED_CAM 10
 #define SLAM_BA_ST_CHOL_FAIL 11 /* last solve: 0 ok, 1 not SPD, 2 dataflow solve timed out */
-/* slots 12..15: phase timers of the profiling builds */
+/* slots 12..15: phase timers of the profiling builds (SLAM_LIN_PROFILE,
+ * SLAM_SOLVE_PROFILE; scripts/ba_solve_prof.py reads state[12:16]); slots 18, 19:
+ * the per-panel timers of SLAM_SOLVE_PROFILE_PANEL (scripts/solve_trace.py) */
 #define SLAM_BA_ST_SOLVE_FAULT 16 /* sticky: camera solves that timed out waiting for a
                                      * co-resident workgroup (never set by a correct launch;
                                      * the Python layer raises when it is non-zero) */
@@ -366,6 +368,14 @@ typedef struct slam_ba_problem {
    * (the launcher reads the level counts from it); both or neither. */
   const int32_t* tl_sched;
   const int32_t* tl_sched_host;
+  /* lin_mode 1, optional (null: the separate k_assemble launch): the assembly
+   * folded into k_lin_mfma -- the supergroup that writes the LAST partial row
+   * of a block sums that block's rows (deterministic order) into sys.  int32:
+   * need[n_blocks] (partial rows per block), cnt[n_blocks] (zero-initialised;
+   * re-armed by the assembler), cam_dblk[C] (diagonal block of each camera),
+   * row_blk[n_bslots] (block of each bpart row), n_empty, empty[n_empty]
+   * (blocks with no partial row here: zeroed every build). */
+  int32_t* asm_tab;
 } slam_ba_problem;
 
 /* Largest tile count (9C / 64, rounded up) the dataflow tiled solve takes:
@@ -373,7 +383,9 @@ typedef struct slam_ba_problem {
 #define SLAM_TL_FLOW_MAX_T 128
 
 /* Problems per batched launch (slam_ba_iterate_batch splits larger batches).
- * The descriptors travel by value in the kernel arguments: 16 x 296 B. */
+ * The descriptors travel by value in the kernel arguments: 16 x 376 B
+ * (ba.hip static_asserts the size; ROCm 7.2 takes this > 4 KB argument
+ * segment, exercised by tests/test_ba.py's 16-window launch). */
 #ifndef SLAM_BA_MAX_BATCH
 #define SLAM_BA_MAX_BATCH 16
 #endif

@@ -60,6 +60,10 @@ struct BaBatch {
   slam_ba_problem p[kBaMaxBatch];
 };
 #define BA_PROB(b) const slam_ba_problem& p = (b).p[blockIdx.y]
+// the batch travels by value in the kernel arguments: 16 x 376 B,
+// beyond the traditional 4 KB; ROCm 7.2 takes it (tests/test_ba.py launches 16)
+static_assert(sizeof(slam_ba_problem) <= 376, "slam_ba_problem grew: re-check the kernarg size");
+static_assert(sizeof(BaBatch) <= 16 * 376, "BaBatch kernel argument size");
 
 // The LM kernels are short and latency-bound and usually share their CUs with
 // the (throughput-bound) ORB workgroups of the concurrent tracking stream: they
@@ -693,6 +697,152 @@ __device__ unsigned long long g_linm_stamp[4096][8];
 #define LINM_END() (void)0
 #endif
 
+// ---------------------------------------------------------------- folded assembly
+// lin_mode 1 with asm_tab (include/slam355.h): k_lin_mfma assembles the reduced
+// camera system itself.  Every supergroup adds one to the counter of each block
+// it wrote a partial row of, after its (sc1, write-through) row stores have
+// drained; the supergroup whose add completes a block (count == need) sums that
+// block's rows with sc1 loads -- its add coming last makes it the acquire for
+// all the rows (MI355X_MICROARCH.md hand-off table, row 1) -- and writes the
+// block into sys; blocks with no partial row here are zeroed by the build.  The
+// sums run in a fixed order (rows interleaved over the parts, parts added in
+// order), whichever workgroup assembles.  One dependent launch (k_assemble) and
+// its wait for CU slots fewer per LM iteration.
+struct AsmTab {
+  const int32_t* need;
+  int32_t* cnt;
+  const int32_t* cam_dblk;
+  const int32_t* row_blk;
+  int n_empty;
+  const int32_t* empty;
+  __device__ explicit AsmTab(const slam_ba_problem& p) {
+    const int nb = p.n_blocks;
+    need = p.asm_tab;
+    cnt = p.asm_tab + nb;
+    cam_dblk = p.asm_tab + 2 * nb;
+    row_blk = cam_dblk + p.n_cams;
+    n_empty = row_blk[p.n_bslots];
+    empty = row_blk + p.n_bslots + 1;
+  }
+};
+
+// out[e] (e < n) = sum over rows [rb, re) of part[row][e], with kMWG threads:
+// nparts = kMWG / n parts (rows rb + k, rb + k + nparts, ...; 4 loads in
+// flight), added in part order.  red: LDS [nparts][n].
+__device__ void fold_rows_sum(const double* __restrict__ part, int stride, int rb, int re, int n,
+                              double* red, double* out) {
+  const int t = threadIdx.x;
+  const int nparts = kMWG / n, k = t / n, e = t - k * n;
+  if (k < nparts) {
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    int r = rb + k;
+    for (; r + 3 * nparts < re; r += 4 * nparts) {
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ld_sc1(part + (size_t)(r + u * nparts) * stride + e);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += v[u];
+    }
+    for (int u = 0; r < re; r += nparts, ++u) a[u] += ld_sc1(part + (size_t)r * stride + e);
+    red[k * n + e] = (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  __syncthreads();
+  if (t < n) {
+    double v = 0.0;
+    for (int q = 0; q < nparts; ++q) v += red[q * n + t];
+    out[t] = v;
+  }
+  __syncthreads();
+}
+
+// sys block blk (+ its camera's vectors when diagonal) from the partial rows;
+// the same formulas as k_assemble
+__device__ void fold_block(const slam_ba_problem& p, int blk, double* scratch) {
+  double* red = scratch;             // [<= 3][112]
+  double* sh = scratch + 3 * kCPart;  // [112]
+  double* sb = sh + kCPart;           // [81]
+  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
+  const int C9 = 9 * p.n_cams, t = threadIdx.x;
+  double* S = p.sys;
+  double* bvec = S + sys_vec_off(p.n_cams, p.n_blocks);
+  double* gvec = bvec + C9;
+  double* diagU = gvec + C9;
+  double* costc = diagU + C9;
+  const bool diag = c1 == c2;
+  const int bb = p.blk_bslot_ptr[blk], be = p.blk_bslot_ptr[blk + 1];
+  if (diag) fold_rows_sum(p.cpart, kCPart, p.cam_cslot_ptr[c1], p.cam_cslot_ptr[c1 + 1], 109, red, sh);
+  if (be > bb) {
+    fold_rows_sum(p.bpart, 81, bb, be, 81, red, sb);
+  } else if (t < 81) {
+    sb[t] = 0.0;
+  }
+  __syncthreads();
+  if (sys_packed(p.n_cams)) {
+    if (t < 81) S[(size_t)blk * 81 + t] = diag ? sh[t] - (sb[t] + sb[9 * (t % 9) + t / 9]) : -sb[t];
+  } else if (t < 81) {
+    const int i = t / 9, j = t - 9 * (t / 9);
+    if (diag) {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c1 + j] = sh[t] - (sb[t] + sb[9 * j + i]);
+    } else {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = -sb[t];
+      S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = -sb[t];
+    }
+  }
+  if (diag && t < 9) {
+    gvec[9 * c1 + t] = -sh[81 + t];
+    bvec[9 * c1 + t] = -sh[81 + t] - sh[90 + t];
+    diagU[9 * c1 + t] = sh[99 + t];
+  }
+  if (diag && t == 0) costc[c1] = sh[108];
+  __syncthreads();
+}
+
+// a block with no partial row in this problem: zeros (and zero vectors when
+// diagonal), every build -- the packed multi-rank sys is all-reduced in place
+__device__ void fold_zero_block(const slam_ba_problem& p, int blk, int t0, int nt) {
+  const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
+  const int C9 = 9 * p.n_cams;
+  double* S = p.sys;
+  double* bvec = S + sys_vec_off(p.n_cams, p.n_blocks);
+  for (int e = t0; e < 81; e += nt) {
+    const int i = e / 9, j = e - 9 * (e / 9);
+    if (sys_packed(p.n_cams)) {
+      S[(size_t)blk * 81 + e] = 0.0;
+    } else {
+      S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = 0.0;
+      S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = 0.0;
+    }
+  }
+  if (c1 == c2)
+    for (int e = t0; e < 28; e += nt) {  // b, g, diag U (9 each), cost
+      if (e < 27) bvec[(size_t)(e / 9) * C9 + 9 * c1 + e % 9] = 0.0;
+      else bvec[3 * (size_t)C9 + c1] = 0.0;
+    }
+}
+
+__device__ void lin_fold_assemble(const slam_ba_problem& p, const int* cams, int m, int nb,
+                                  const int* brow, double* scratch) {
+  const AsmTab A(p);
+  __shared__ int done[kMCams + kMCams * (kMCams - 1) / 2];
+  __shared__ int ndone;
+  __builtin_amdgcn_s_waitcnt(0);  // this workgroup's partial rows have left (sc1)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int q = 0; q < m + nb; ++q) {
+      const int blk = q < m ? A.cam_dblk[cams[q]] : A.row_blk[brow[q - m]];
+      const int old = (int)ticket_add(reinterpret_cast<uint32_t*>(A.cnt + blk));
+      if (old == A.need[blk] - 1) {
+        done[n++] = blk;
+        __hip_atomic_store(A.cnt + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      }
+    }
+    ndone = n;
+  }
+  __syncthreads();
+  for (int q = 0; q < ndone; ++q) fold_block(p, done[q], scratch);
+}
+
 __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   BA_PROB(bat);
   const int sg = blockIdx.x;
@@ -700,6 +850,10 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
   LINM_DECL();
   lm_wave_priority();
   __shared__ MLds L;
+  if (p.asm_tab != nullptr) {  // folded assembly: this supergroup's share of the empty blocks
+    const AsmTab A(p);
+    for (int q = sg; q < A.n_empty; q += p.n_sgrps) fold_zero_block(p, A.empty[q], threadIdx.x, kMWG);
+  }
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   // the supergroup record (one hop): chunk range, slot ranges, the first
@@ -1030,15 +1184,16 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     } else {
       v = Za[9 * 16 + 9];          // |r|^2
     }
-    p.cpart[(size_t)L.crow[a] * kCPart + e] = v;
+    st_sc1(p.cpart + (size_t)L.crow[a] * kCPart + e, v);
   }
   for (int q = t; q < 81 * nb; q += kMWG) {
     const int pr = q / 81, e = q - 81 * (q / 81);
     const int ab = L.bab[pr], a = ab & 255, b = ab >> 8;
     const int i = e / 9, j = e - 9 * (e / 9);
-    p.bpart[(size_t)L.brow[pr] * 81 + e] = T[(9 * a + i) * kMRows + 9 * b + j];
+    st_sc1(p.bpart + (size_t)L.brow[pr] * 81 + e, T[(9 * a + i) * kMRows + 9 * b + j]);
   }
   LINM_T(6);
+  if (p.asm_tab != nullptr) lin_fold_assemble(p, sm + 10, m, nb, L.brow, &L.jc[0][0]);
   LINM_END();
 }
 
@@ -2936,7 +3091,9 @@ static int launch_reset(const Launch& L, double lam0, hipStream_t s) {
 }
 
 static int launch_build(const Launch& L, hipStream_t s) {
-  // every entry of sys is written by k_assemble (all upper blocks), so no clearing
+  // every entry of sys is written by the assembly (all listed blocks), so no clearing
+  bool folded = L.mode == 1;
+  for (int i = 0; i < L.n; ++i) folded = folded && L.b.p[i].asm_tab != nullptr;
   if (L.mode == 1) {
     k_lin_mfma<<<dim3(L.max_sgrps, L.n), kMWG, 0, s>>>(L.b);
     SLAM_LAUNCHED("k_lin_mfma");
@@ -2944,8 +3101,10 @@ static int launch_build(const Launch& L, hipStream_t s) {
     k_linearize<<<dim3(L.max_grps, L.n), kLinWG, 0, s>>>(L.b);
     SLAM_LAUNCHED("k_linearize");
   }
-  k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
-  SLAM_LAUNCHED("k_assemble");
+  if (!folded) {  // k_lin_mfma skips the fold of a problem without asm_tab
+    k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
+    SLAM_LAUNCHED("k_assemble");
+  }
   return SLAM_OK;
 }
 

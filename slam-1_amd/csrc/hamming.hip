@@ -202,6 +202,10 @@ constexpr int kMxWaves = kMxWG / kWave;
 #endif
 constexpr int kMxQB = SLAM_MX_QB;          // (4 per step measured 10 % slower than 8 alone)
 constexpr int kMxQWG = 16 * kMxQB;         // queries per workgroup
+// the kernel fills its two 256-entry LUTs with one thread each and merges one
+// query per thread: the -D tunables must keep both within the group
+static_assert(kMxWG >= 256 && kMxWG >= kMxQWG && kMxWG % 64 == 0,
+              "knn2_mx_kernel: SLAM_MX_WG must cover the LUTs and 16 * SLAM_MX_QB queries");
 constexpr int kMxAhead = 2;                // train steps loaded ahead
 constexpr float kMxNone = 16777215.0f;     // > every valid key (< 2^23 + 2^14)
 typedef int mx_v8i __attribute__((ext_vector_type(8)));

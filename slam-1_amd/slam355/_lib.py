@@ -39,7 +39,7 @@ class BAProblemStruct(ctypes.Structure):
         ("sys", c_p), ("chol", c_p), ("delta_c", c_p), ("red_part", c_p), ("small", c_p),
         ("state", c_p), ("ticket", c_p),
         ("sg_ptr", c_p), ("sg_meta", c_p), ("obs_meta", c_p), ("chk_optr", c_p), ("chk_cptr", c_p),
-        ("bslot_ab", c_p), ("tl_sched", c_p), ("tl_sched_host", c_p),
+        ("bslot_ab", c_p), ("tl_sched", c_p), ("tl_sched_host", c_p), ("asm_tab", c_p),
     ]
 
 

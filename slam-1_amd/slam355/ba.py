@@ -599,6 +599,28 @@ def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=Non
         n_obs=O, n_grps=G, n_sgrps=NS, chunks_per_wg=S)
 
 
+def assembly_table(n_cams, pl):
+    """asm_tab of the folded assembly (include/slam355.h): need[NB] (partial rows
+    per listed block: camera rows of its camera when diagonal + its block rows),
+    cnt[NB] (zeros), cam_dblk[C], row_blk[n_bslots] (block of each block-major
+    bpart row), n_empty, empty[] (blocks with no partial row)."""
+    blocks = pl["blocks"].astype(np.int64)
+    NB = len(blocks)
+    bptr = pl["blk_bslot_ptr"].astype(np.int64)
+    cptr = pl["cam_cslot_ptr"].astype(np.int64)
+    diag = blocks[:, 0] == blocks[:, 1]
+    need = np.diff(bptr)
+    need[diag] += np.diff(cptr)[blocks[diag, 0]]
+    cam_dblk = np.full(n_cams, -1, np.int64)
+    cam_dblk[blocks[diag, 0]] = np.nonzero(diag)[0]
+    if (cam_dblk < 0).any():
+        raise ValueError("assembly_table: a camera's diagonal block is not listed")
+    row_blk = np.repeat(np.arange(NB), np.diff(bptr))
+    empty = np.nonzero(need == 0)[0]
+    return np.concatenate([need, np.zeros(NB, np.int64), cam_dblk, row_blk, [len(empty)],
+                           empty]).astype(np.int32)
+
+
 def tiled_solve_flops(n_cams, blocks, tb=64):
     """Flops of the tiled Cholesky (csrc/ba.hip k_tl_*) for a packed block list
     [n_blocks, 2]: the 64x64 tiles it factors, solves and updates, with the
@@ -635,15 +657,18 @@ class BAProblem:
     """Device-resident BA problem + LM state.  `cams` [C,9], `pts` [P,3] float64."""
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
-                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow"):
+                 block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow",
+                 fold_assembly=True):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
         every point is seen by <= MF_CAMS cameras).  The tiled camera solve
         (9C > 120) follows the nested-dissection schedule of tl_schedule;
-        tl_mode "flow" runs it as one dataflow launch (k_tl3_flow; the library
-        falls back to levels when the tile count exceeds the CUs the stream
-        may use), "levels" one launch pair per elimination-tree level."""
+        tl_mode "flow" runs it as one dataflow launch (k_tl3_flow, on any
+        stream and CU mask), "levels" one launch pair per elimination-tree level.
+        fold_assembly (lin_mode mfma): k_lin_mfma's last supergroup per camera
+        block sums the block's partial rows into the system (no k_assemble
+        launch); False keeps the separate k_assemble launch."""
         if tl_mode not in ("flow", "levels"):
             raise ValueError(f"tl_mode must be 'flow' or 'levels', not {tl_mode!r}")
         dev = require_gpu()
@@ -712,6 +737,9 @@ class BAProblem:
         if self.tl_levels:
             s.tl_sched = t["tl_sched"].data_ptr()
             s.tl_sched_host = self._sched_host.ctypes.data
+        if pl["mode"] == 1 and fold_assembly:  # k_lin_mfma assembles sys itself
+            t["asm_tab"] = T(assembly_table(C, pl))
+            s.asm_tab = t["asm_tab"].data_ptr()
         self._s = s
         self.reset(lam0)
 

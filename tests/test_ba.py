@@ -822,3 +822,67 @@ def test_union_plan_falls_back_for_wide_tracks():
     assert ba.plan_mfma(10, 50, ci, pi) is None
     cams, pts, ci, pi, qs = make_problem(4, 10, 50, 7)
     assert ba.plan_mfma(10, 50, ci, pi) is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,P,k", [(10, 5000, 6), (64, 50000, 6)])
+def test_gpu_folded_assembly_equals_k_assemble(C, P, k):
+    """k_lin_mfma assembles the reduced camera system itself (the
+    last supergroup per block sums its partial rows; blocks without partial rows
+    zeroed every build) -- the same system as the separate k_assemble launch to
+    rounding (the sums run in another fixed order), exact zeros where no camera
+    pair shares a point, and repeated builds are bit-identical."""
+    import torch
+    from slam355 import ba
+    from slam355.synthetic import ba_problem, perturb
+
+    rng = np.random.default_rng(3 + C)
+    cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+    c0, p0 = perturb(rng, cams, pts)
+    a = ba.BAProblem(c0, p0, ci, pi, qs)  # folded (default)
+    b = ba.BAProblem(c0, p0, ci, pi, qs, fold_assembly=False)
+    assert a.lin_mode == "mfma" and "asm_tab" in a.t and "asm_tab" not in b.t
+    a.t["sys"].fill_(np.nan)  # every entry must be written by the build
+    a.build_system()
+    b.build_system()
+    sa, sb = a.t["sys"].cpu().numpy(), b.t["sys"].cpu().numpy()
+    assert np.isfinite(sa).all()
+    assert np.array_equal(sa == 0.0, sb == 0.0)
+    assert np.allclose(sa, sb, rtol=1e-12, atol=1e-12 * np.abs(sb).max())
+    a.build_system()
+    torch.cuda.synchronize()
+    assert np.array_equal(a.t["sys"].cpu().numpy(), sa)
+    for _ in range(3):
+        a.iterate(1)
+        b.iterate(1)
+    sta, stb = a.state(), b.state()
+    assert bool(sta["ACCEPTED"]) == bool(stb["ACCEPTED"])
+    assert abs(sta["COST"] - stb["COST"]) <= 1e-10 * stb["COST"]
+
+
+def test_assembly_table_counts_every_partial_row():
+    """The folded assembly's table (slam355.ba.assembly_table): every cpart row
+    is counted once at its camera's diagonal block, every bpart row once at its
+    block, blocks without rows are listed empty (C3 window: camera pairs more
+    than 5 keyframes apart share no point)."""
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(5, 10, 2000, 6)
+    pl = ba.plan_mfma(10, len(pts), ci, pi)
+    assert pl is not None
+    tab = ba.assembly_table(10, pl).astype(np.int64)
+    NB = len(pl["blocks"])
+    need, cnt = tab[:NB], tab[NB:2 * NB]
+    cam_dblk = tab[2 * NB:2 * NB + 10]
+    nbs = len(pl["bslot_blk"])
+    row_blk = tab[2 * NB + 10:2 * NB + 10 + nbs]
+    n_empty = tab[2 * NB + 10 + nbs]
+    empty = tab[2 * NB + 11 + nbs:]
+    assert not cnt.any() and len(empty) == n_empty
+    assert need.sum() == len(pl["cslot_cam"]) + nbs
+    blocks = pl["blocks"]
+    assert all(blocks[cam_dblk[c], 0] == c == blocks[cam_dblk[c], 1] for c in range(10))
+    assert np.array_equal(np.bincount(row_blk, minlength=NB), np.diff(pl["blk_bslot_ptr"]))
+    assert set(empty) == set(np.nonzero(need == 0)[0])
+    gaps = blocks[empty, 1] - blocks[empty, 0]
+    assert (gaps > 5).all() and len(empty) == sum(10 - d for d in range(6, 10))
