@@ -383,7 +383,7 @@ def run_tracking(args, world, rank):
             # (round-3 sweep; 8 was best at 32 pairs per step)
             cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 5
             bas.append(BABatch([BAProblem(*w, stream=s, chunks_per_wg=cpw,
-                                          fold_assembly=not args.no_fold)
+                                          fold_assembly=args.fold)
                                 for w in windows[i::ns]], stream=s))
     ba = bas[0]
     torch.cuda.synchronize()
@@ -521,7 +521,7 @@ def run_tracking(args, world, rank):
                 "unit": "GB/s", "kernel": "k_orb_tile+k_orb_compact", "ms_per_launch": orb_ms,
                 "bytes_per_launch": orb_bytes},
         "local_ba": {"bound": "mfma", "achieved": ba_flops / (ba_ms_iter * 1e-3) / 1e12,
-                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma (assembly folded in) + k_solve_blk + k_back_trial (one HIP graph)" if not args.no_fold else f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
+                     "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s", "kernel": f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma (assembly folded in) + k_solve_blk + k_back_trial (one HIP graph)" if args.fold else f"batched LM iteration of {n_launch} C3 windows: k_lin_mfma + k_assemble + k_solve_blk + k_back_trial (one HIP graph)",
                      "ms_per_iter": ba_ms_iter, "flops_per_iter": ba_flops},
     }
     # the stereo matcher launch (keypoint.py:44: B pairs of ~2000 x ~2000
@@ -534,7 +534,7 @@ def run_tracking(args, world, rank):
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_solve_blk", "k_back_trial<true>")
-                                            + (("k_assemble",) if args.no_fold else ()))
+                                            + (() if args.fold else ("k_assemble",)))
     roof["matcher"]["traffic"] = pmc_bytes(pmc, (roof["matcher"]["kernel"].split()[0],))
     units = {"orb": f"bytes per ORB launch ({n_img} images), HBM, from PMC",
              "local_ba": f"bytes per batched LM iteration ({n_launch} windows), HBM, from PMC",
@@ -791,7 +791,7 @@ def run_ba(args, world, rank):
         step_fn = prob.step_distributed
     else:
         prob = BAProblem(c0, p0, ci, pi, qs, chunks_per_wg=args.chunks_per_wg,
-                         fold_assembly=not args.no_fold)
+                         fold_assembly=args.fold)
         if args.no_graph:
             step_fn = lambda: prob.iterate(1)  # noqa: E731
         else:  # one LM iteration = one HIP-graph replay (3T + 5 launches for the tiled solver)
@@ -876,7 +876,7 @@ def run_ba_batch(args, world, rank):
         cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
         c0, p0 = perturb(rng, cams, pts)
         probs.append(BAProblem(c0, p0, ci, pi, qs, lin_mode=args.lin_mode,
-                               chunks_per_wg=cpw, fold_assembly=not args.no_fold))
+                               chunks_per_wg=cpw, fold_assembly=args.fold))
     # --ba-streams S: the windows split into S batches on S streams, so one
     # batch's latency-bound camera solve overlaps another's linearisation
     ns = max(1, min(args.ba_streams, len(probs)))
@@ -1117,9 +1117,9 @@ def main():
     ap.add_argument("--c4", action="store_true", help="--workload ba: C4 problem on 1 GPU")
     ap.add_argument("--c5", action="store_true",
                     help="--workload ba: C5 loop-closure global BA (500 KF x 200k pts)")
-    ap.add_argument("--no-fold", action="store_true",
-                    help="local BA: the separate k_assemble launch instead of the assembly "
-                         "folded into k_lin_mfma (A/B)")
+    ap.add_argument("--fold", action="store_true",
+                    help="local BA: the assembly folded into k_lin_mfma instead of the separate "
+                         "k_assemble launch (A/B; measured slower, BAProblem fold_assembly)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch the LM iterations eagerly instead of replaying a HIP graph")
     ap.add_argument("--ba-overlap", default="full", choices=["full", "after-orb"],

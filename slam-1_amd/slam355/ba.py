@@ -658,7 +658,7 @@ class BAProblem:
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
                  block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow",
-                 fold_assembly=True):
+                 fold_assembly=False):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
@@ -668,7 +668,10 @@ class BAProblem:
         stream and CU mask), "levels" one launch pair per elimination-tree level.
         fold_assembly (lin_mode mfma): k_lin_mfma's last supergroup per camera
         block sums the block's partial rows into the system (no k_assemble
-        launch); False keeps the separate k_assemble launch."""
+        launch).  Off by default: measured slower (the workgroup that finishes
+        last assembles every block it touched, a serial tail; 16 C3 windows
+        326 vs 225 us per iteration, C4 406 vs 324 us, tracking 19.0k vs 19.9k
+        frames/s, profiles/r4/fold_ab/)."""
         if tl_mode not in ("flow", "levels"):
             raise ValueError(f"tl_mode must be 'flow' or 'levels', not {tl_mode!r}")
         dev = require_gpu()
