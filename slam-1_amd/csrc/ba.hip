@@ -2283,13 +2283,16 @@ constexpr int kFlowSpinMax = 1 << 22;  // ~0.2 s of 128-cycle polls
 // per column: wall clock (100 MHz) at start, diagonal updates done, factor done,
 // row tiles published, y published, x inputs in, x published, end
 __device__ unsigned long long g_flow_stamp[SLAM_TL_FLOW_MAX_T][8];
-#define FLOW_T(i)                                                   \
-  do {                                                              \
-    if (threadIdx.x == 0) g_flow_stamp[blockIdx.x][i] = wall_clock64(); \
+// (stamps are kept per COLUMN: the workgroup's own column J, and (5), (6) for
+// the column k whose x it formed)
+#define FLOW_TC(col, i)                                           \
+  do {                                                            \
+    if (threadIdx.x == 0) g_flow_stamp[(col)][i] = wall_clock64(); \
   } while (0)
 #else
-#define FLOW_T(i) (void)0
+#define FLOW_TC(col, i) (void)0
 #endif
+#define FLOW_T(i) FLOW_TC(J, i)
 
 struct FlowPtrs {
   int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt, *dv;
@@ -2694,7 +2697,7 @@ void k_tl3_flow(slam_ba_problem p) {
 #pragma unroll
         for (int m = 0; m < 16; ++m) s2 = __builtin_fma(la[m], xa[m], s2);
       }
-      FLOW_T(5);
+      FLOW_TC(k, 5);
       part[w][lane] = s2;
       __syncthreads();
       if (t < kTB) rv[t] = yv[t] - (((part[0][t] + part[1][t]) + part[2][t]) + part[3][t]);
@@ -2719,6 +2722,7 @@ void k_tl3_flow(slam_ba_problem p) {
     // retire column k even when the solve failed (the counters and the ticket
     // still complete; the epilogue sees the fail code)
     flow_publish(F.xf + k, epoch);
+    FLOW_TC(k, 6);
     if (t == 0) {
       for (int u = 0; u < ksc; ++u) {
         const int c = S[kso + u];  // k is a row tile of column c
@@ -2730,7 +2734,6 @@ void k_tl3_flow(slam_ba_problem p) {
     }
     __syncthreads();
   }
-  FLOW_T(6);
   // (5) the workgroup that retired the last column runs the epilogue
   if (!last_sh) return;
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out

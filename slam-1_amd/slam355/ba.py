@@ -164,9 +164,9 @@ def tl_schedule(n_cams, blocks):
       [5] column table offset
       column table: per column J (rows_off, rows_cnt, rs_off, rs_cnt, upd_off)
         rows: I > J with L_IJ != 0 (ascending); rs: k < J with L_Jk != 0
-        (ascending: the updates of the diagonal tile and the forward
-        substitution); upd: per row I, (koff, kcnt) -- the k < J with L_Ik and
-        L_Jk both nonzero
+        (by elimination-tree level, then index: the updates of the diagonal
+        tile and the forward substitution); upd: per row I, (koff, kcnt) -- the
+        k < J with L_Ik and L_Jk both nonzero (in rs order)
       level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
@@ -260,8 +260,13 @@ def tl_schedule(n_cams, blocks):
             ents += [k, list_offs[li], len(lists[li])]
         table += [po, len(pan[lv]), uo, len(upd[lv]), bo, len(bk[lv])]
     flat = head + tperm.tolist() + itperm.tolist() + table + ents + [v for li in lists for v in li]
-    # column table of the dataflow solve
-    rs = [[k for k in range(J) if J in struct[k]] for J in range(T)]
+    # column table of the dataflow solve.  rs(J) in the order its tiles are
+    # expected to be published -- by elimination-tree level, then index -- so a
+    # column accumulates the tiles of its early (low-level) children while the
+    # late ones are still being factored, instead of waiting on the first
+    # listed tile (the sums keep this fixed order: deterministic)
+    rs = [sorted((k for k in range(J) if J in struct[k]), key=lambda k: (level[k], k))
+          for J in range(T)]
     flow_off = len(flat)
     flat[5] = flow_off
     recs = [0] * (5 * T)
