@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 B="$ROOT/bench.py --no-cpu-baseline --no-ba-scale $*"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run \
-  -- python3 $B --steps 10 --warmup 3 > "$OUT/stats.log" 2>&1 || exit 1
+  -- python3 $B --steps 20 --warmup 5 > "$OUT/stats.log" 2>&1 || exit 1
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $c --output-format csv -d "$OUT/$c" -o run \
     -- python3 $B --steps 3 --warmup 1 > "$OUT/$c.log" 2>&1 || exit 1
