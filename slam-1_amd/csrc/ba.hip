@@ -1165,6 +1165,7 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     for (int r = 0; r < 4; ++r) Z[(wid + 4 * s) * 256 + (mk + 4 * r) * 16 + mi] = zacc[s][r];
   }
   __syncthreads();
+  const bool fold = p.asm_tab != nullptr;  // uniform
   // camera rows: items (a, 112-wide row entry)
   for (int q = t; q < m * 109; q += kMWG) {
     const int a = q / 109, e = q - 109 * (q / 109);
@@ -1184,13 +1185,20 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
     } else {
       v = Za[9 * 16 + 9];          // |r|^2
     }
-    st_sc1(p.cpart + (size_t)L.crow[a] * kCPart + e, v);
+    // written through (sc1) only for the folded assembly (other CUs read them in
+    // this launch); plain stores keep the lines in L2 for k_assemble
+    double* cp = p.cpart + (size_t)L.crow[a] * kCPart + e;
+    if (fold) st_sc1(cp, v);
+    else *cp = v;
   }
   for (int q = t; q < 81 * nb; q += kMWG) {
     const int pr = q / 81, e = q - 81 * (q / 81);
     const int ab = L.bab[pr], a = ab & 255, b = ab >> 8;
     const int i = e / 9, j = e - 9 * (e / 9);
-    st_sc1(p.bpart + (size_t)L.brow[pr] * 81 + e, T[(9 * a + i) * kMRows + 9 * b + j]);
+    const double v = T[(9 * a + i) * kMRows + 9 * b + j];
+    double* bp = p.bpart + (size_t)L.brow[pr] * 81 + e;
+    if (fold) st_sc1(bp, v);
+    else *bp = v;
   }
   LINM_T(6);
   if (p.asm_tab != nullptr) lin_fold_assemble(p, sm + 10, m, nb, L.brow, &L.jc[0][0]);
@@ -1361,7 +1369,7 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
 //       (v_mfma_f64_16x16x4_f64, K = 9 padded to 12) per tile.
 // 2 barriers per camera instead of one per column.  Back substitution runs in
 // wave 0 with x in registers (two rows per lane) and x_k broadcast by readlane.
-constexpr int kBlkWG = 256;   // 4 waves, one per SIMD: 512 registers per lane
+constexpr int kBlkWG = 256;   // 4 waves, one per SIMD; <= 256 registers per lane (2 waves per SIMD)
 constexpr int kBlkWaves = kBlkWG / 64;
 constexpr int kTileMax = 9;   // lower 16x16 tiles per wave: 4 * 9 >= 36
 constexpr int kPanelW = 9;    // columns per block step (one camera)
@@ -1416,7 +1424,7 @@ __device__ unsigned long long g_solve_trace[20][6];
 #define SOLVE_TR(step, i) (void)0
 #endif
 
-__global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
+__global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) void k_solve_blk(BaBatch bat) {
   BA_PROB(bat);
   lm_wave_priority();
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -1612,29 +1620,28 @@ __global__ __launch_bounds__(kBlkWG) void k_solve_blk(BaBatch bat) {
       ok = false;
       break;
     }
-    // (c) trailing update of the tiles right of / below the panel: operands of
-    // all live tiles loaded first, then the MFMAs interleaved across tiles
+    // (c) trailing update of the tiles right of / below the panel, tile by
+    // tile (6 operand loads, then its 3 MFMAs; each tile's sum in the same kk
+    // order).  Loading every live tile's operands first held ~100 more
+    // registers (317 per lane: one wave per SIMD, so a solve workgroup waited
+    // for a whole idle CU beside ORB); at 210 (two waves per SIMD) the batched
+    // local-BA stage in the tracking bench drops 3.1 -> 2.75 ms per step
+    // (profiles/r4/solve_lowreg_ab/)
     const int tr = c0 + kPanelW;
-    bool live[kTileMax];
-    double wa[kTileMax][3], lb[kTileMax][3];
 #pragma unroll
     for (int s = 0; s < kTileMax; ++s) {
-      live[s] = tI[s] >= 0 && tJ[s] * 16 + 15 >= tr;  // uniform (I >= J)
-      if (!live[s]) continue;
+      if (!(tI[s] >= 0 && tJ[s] * 16 + 15 >= tr)) continue;  // uniform (I >= J)
       const double* wrow = WL + (tI[s] * 16 + (lane & 15)) * kWLs + (lane >> 4);
       const double* lrow = LL + (tJ[s] * 16 + (lane & 15)) * kWLs + (lane >> 4);
+      double wa[3], lb[3];
 #pragma unroll
       for (int kk = 0; kk < 3; ++kk) {
-        wa[s][kk] = wrow[4 * kk];
-        lb[s][kk] = lrow[4 * kk];
+        wa[kk] = wrow[4 * kk];
+        lb[kk] = lrow[4 * kk];
       }
-    }
 #pragma unroll
-    for (int kk = 0; kk < 3; ++kk) {
-#pragma unroll
-      for (int s = 0; s < kTileMax; ++s)
-        if (live[s])
-          acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[s][kk], lb[s][kk], acc[s], 0, 0, 0);
+      for (int kk = 0; kk < 3; ++kk)
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa[kk], lb[kk], acc[s], 0, 0, 0);
     }
 #ifdef SLAM_SOLVE_TRACE
     if (threadIdx.x == 0) {
