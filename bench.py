@@ -381,7 +381,7 @@ def run_tracking(args, world, rank):
             # per step, alternating runs: 3 / 4 / 5 / 6 / 8 -> 17.7k / 17.8k /
             # 18.1-18.3k / 18.1-18.3k / 17.6-17.9k frames/s
             # (round-3 sweep; 8 was best at 32 pairs per step)
-            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 5
+            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 8
             bas.append(BABatch([BAProblem(*w, stream=s, chunks_per_wg=cpw,
                                           fold_assembly=args.fold)
                                 for w in windows[i::ns]], stream=s))
@@ -1103,8 +1103,10 @@ def main():
     ap.add_argument("--lin-mode", default="auto", choices=["auto", "mfma", "slot"],
                     help="BA linearisation: camera-union MFMA kernel or the slot kernel")
     ap.add_argument("--chunks-per-wg", type=int, default=None,
-                    help="camera-union linearisation: chunks per workgroup (default: 5 for the "
-                         "tracking workload's batched windows, auto elsewhere)")
+                    help="camera-union linearisation: chunks per workgroup (default: 8 for the "
+                         "tracking workload's batched windows -- 3 / 4 / 5 / 6 / 8 / 12 / 16 "
+                         "measured 20.2k / 20.4k / 20.5k / 20.5k / 20.6k / 20.6k / 20.5k "
+                         "frames/s, profiles/r4/orbcus_sweep/; auto elsewhere)")
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
@@ -1140,11 +1142,12 @@ def main():
                     help="tracking: ORB on the tracking stream (default: ORB on its own stream "
                          "into double-buffered outputs, so the next batch's ORB overlaps this "
                          "batch's matching / PnP tail)")
-    ap.add_argument("--orb-cus", type=int, default=224,
-                    help="ORB pipeline: ORB's stream may use only the first N CUs (0: all); the "
-                         "rest are left to the latency-bound local-BA and tracking-tail kernels "
-                         "(at the 64-pair / 16-window default, alternating runs: 216 -> 18.8-19.0k, "
-                         "224 -> 19.2-19.3k, 232 -> 18.9-19.1k, 240 -> 18.8-19.0k frames/s)")
+    ap.add_argument("--orb-cus", type=int, default=0,
+                    help="ORB pipeline: ORB's stream may use only the first N CUs (0: all, the "
+                         "default since the camera solve fits two waves per SIMD: alternating "
+                         "runs 224 / 232 / 240 / 248 / all -> 19.7-19.8k / 19.9-20.1k / "
+                         "20.1-20.2k / 20.3k / 20.5k frames/s, profiles/r4/orbcus_sweep/; with "
+                         "the 317-register solve round 3 measured 224 best)")
     ap.add_argument("--solve-lds-floor", type=int, default=0,
                     help="LDS bytes the one-workgroup camera solve requests at least "
                          "(slam_ba_set_solve_lds_floor)")
