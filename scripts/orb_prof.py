@@ -21,7 +21,7 @@ L, R, _, _ = corridor_sequence(B + 1, 1280, 720, seed=1000, device="cuda", as_nu
 imgs = torch.cat([L, R[:B]]).contiguous()
 f = _lib.lib.slam_orb_profile_read
 f.argtypes = [ctypes.c_void_p]
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 96)()
 orb.orb_batch(imgs, KP)
 f(buf)
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -37,3 +37,7 @@ nwg = 5 * imgs.shape[0] * 36
 print(f"ms/launch {ev0.elapsed_time(ev1) / 5:.3f}; cycles per WG {tot / nwg:.0f}")
 for i, n in enumerate(names):
     print(f"  {n:9s} {buf[i] / nwg:9.0f} clk/WG  {100 * buf[i] / tot:5.1f}%")
+print("per level (clk/WG):")
+for lv in range(8):
+    row = [buf[16 + 10 * lv + i] / nwg for i in range(10)]
+    print(f"  L{lv} {sum(row):8.0f}  " + " ".join(f"{n}={v:.0f}" for n, v in zip(names, row) if v))

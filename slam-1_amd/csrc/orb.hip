@@ -196,14 +196,16 @@ __device__ __forceinline__ int lin_coeff(int d, int dsize, int ssize) {
 
 // -DSLAM_ORB_PROFILE: per-phase shader cycles (s_memtime, thread 0 of every
 // workgroup) accumulated in g_orb_prof and read by slam_orb_profile_read().
+// Slots 16 + 10 l + ph split the same cycles by pyramid level l.
 #ifdef SLAM_ORB_PROFILE
-__device__ unsigned long long g_orb_prof[16];
+__device__ unsigned long long g_orb_prof[96];
 #define ORB_T0() unsigned long long orb_tp = __builtin_amdgcn_s_memtime()
 #define ORB_T(ph)                                                          \
   do {                                                                     \
     if (threadIdx.x == 0) {                                                \
       const unsigned long long orb_tn = __builtin_amdgcn_s_memtime();      \
       atomicAdd(&g_orb_prof[ph], orb_tn - orb_tp);                         \
+      atomicAdd(&g_orb_prof[16 + 10 * orb_lv + (ph)], orb_tn - orb_tp);    \
       orb_tp = orb_tn;                                                     \
     }                                                                      \
   } while (0)
@@ -270,6 +272,9 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
   float* gsvr = reinterpret_cast<float*>(gsvc + g.cand_cap);
 
   ORB_T0();
+#ifdef SLAM_ORB_PROFILE
+  int orb_lv = 0;
+#endif
   // Level images are stored with a row pitch of the width rounded up to 4 bytes
   // (lpitch), so 4 adjacent pixels of a row are one aligned dword for the
   // resize stores and the blur's row windows.
@@ -299,6 +304,9 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
   int overflow = 0;  // uniform
   const int nlev = g.nlev[shp];
   for (int l = 0; l < nlev; ++l) {
+#ifdef SLAM_ORB_PROFILE
+    orb_lv = l;
+#endif
     const int W = g.lw[shp][l], H = g.lh[shp][l];
     const int P = lpitch(W);  // row pitch of the level image
     if (l > 0) {
@@ -573,6 +581,21 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     const int nk = ctr[1];
     ORB_T(4);
+    // the IC-angle disc masks (17 rows |v| = 0..16 x 8 dwords, 0x01 per
+    // in-disc column) into the histogram's slots, dead from here to the
+    // next level's NMS (published by the Harris barrier)
+    uint32_t* icm = reinterpret_cast<uint32_t*>(hist);
+    if (t < 17 * 8) {
+      const int vv = t >> 3, dd = t & 7;
+      const int um = vv < 16 ? (int)((0x368'9abc'ddee'efff'fULL >> (4 * vv)) & 15u) : -1;
+      uint32_t mk = 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int u = 4 * dd + j - 15;
+        mk |= ((u < 0 ? -u : u) <= um ? 1u : 0u) << (8 * j);
+      }
+      icm[t] = mk;
+    }
     // Harris: 16 lanes per survivor (4 per wave): lane s of the group takes window
     // pixels s, s + 16, s + 32, s + 48 (< 49) of the 7x7 block; the integer sums
     // a, b, c are reduced over the 16 lanes (exact in any order).
@@ -689,38 +712,45 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       overflow = 1;
       break;
     }
-    // ---- IC angle: one wave per keypoint, lanes 32h + (0..30) <-> u = -15..15;
-    // the disc column of u is |v| <= umax[|u|] (the umax table is symmetric:
-    // |u| <= umax[|v|] <=> |v| <= umax[|u|]), rows v = -1..-15 in h = 0 and
-    // 0..15 in h = 1, 16 independent masked reads per lane (integer moments:
-    // exact in any order)
-    for (int k = wid; k < m; k += kOrbWG / 64) {
-      const int cx = L[k].x, cy = L[k].y;
-      int m10 = 0, m01 = 0;
-      {
-        // u and the column limit umax[|u|] (umax = {15,15,15,15,14,14,14,13,13,
-        // 12,11,10,9,8,6,3} as a packed 4-bit table) are formed in the loop:
-        // hoisted, they would hold registers across the whole kernel.  The
-        // rows stay a rolled loop: unrolled, the kernel spills (40-60 B/lane
-        // of scratch, 1.95 vs 1.52 ms per 65 images).
-        int ln = lane;
-        __asm__ volatile("" : "+v"(ln));
-        const int u = (ln & 31) - 15, au = u < 0 ? -u : u;
-        const int ic_vlim = (ln & 31) < 31 ? (int)((0x368'9abc'ddee'efff'fULL >> (4 * au)) & 15u) : -1;
-#pragma unroll 1
-        for (int s = 0; s < 16; ++s) {
-          const int v = lane < 32 ? -(s + 1) : s;
-          const bool in = (lane < 32 ? s + 1 : s) <= ic_vlim;
-          const int val = I[(cy + (in ? v : 0)) * P + cx + (in ? u : 0)];
-          m10 += in ? u * val : 0;
-          m01 += in ? v * val : 0;
+    // ---- IC angle: two keypoints per wave, 32 lanes each.  Lane i of a half
+    // takes dword d = i & 7 of the 32-byte row window [cx-15, cx+16] on rows
+    // v = -15 + (i >> 3) + 4 it, it = 0..7 (column 16 and row 16 lie outside
+    // the disc); the disc |u| <= umax[|v|] (the umax table is symmetric:
+    // |u| <= umax[|v|] <=> |v| <= umax[|u|]) is a 0x01-per-column byte mask per
+    // (|v|, d) from the icm table, and two v_dot4_u32_u8 per row dword give
+    // sum (u + 15) val and the row sum: m10 = sum (u + 15) val - 15 sum val,
+    // m01 = sum v (row sum) -- integer moments, exact in any order
+    {
+      const int hh = lane >> 5, i = lane & 31, d = i & 7, r = i >> 3;
+      const uint32_t uoff = 0x03020100u + 0x04040404u * (uint32_t)d;  // u + 15 per byte
+      for (int k0 = 2 * wid; k0 < m; k0 += 2 * (kOrbWG / 64)) {
+        const int k = k0 + hh;
+        const bool kv = k < m;
+        const int kk = kv ? k : k0;
+        const int cx = L[kk].x, cy = L[kk].y;
+        uint32_t su = 0u, s1 = 0u;
+        int m01 = 0;
+        const int a0 = (cy - 15 + r) * P + cx - 15 + 4 * d;
+#pragma unroll 2
+        for (int it = 0; it < 8; ++it) {
+          const int v = r + 4 * it - 15;
+          const int a = a0 + 4 * it * P;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (a & ~3));
+          const uint32_t px = __builtin_amdgcn_alignbyte(wp[1], wp[0], a & 3);
+          const uint32_t ones = icm[8 * (v < 0 ? -v : v) + d];
+          const uint32_t val = px & (ones * 0xFFu);
+          su = __builtin_amdgcn_udot4(uoff, val, su, false);
+          const uint32_t rs = __builtin_amdgcn_udot4(0x01010101u, val, 0u, false);
+          s1 += rs;
+          m01 += v * (int)rs;
         }
+        int m10 = (int)su - 15 * (int)s1;
+        for (int off = 16; off > 0; off >>= 1) {
+          m10 += __shfl_xor(m10, off, 64);
+          m01 += __shfl_xor(m01, off, 64);
+        }
+        if (i == 0 && kv) L[k].angle = fast_atan2_deg((float)m01, (float)m10);
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        m10 += __shfl_xor(m10, off, 64);
-        m01 += __shfl_xor(m01, off, 64);
-      }
-      if (lane == 0) L[k].angle = fast_atan2_deg((float)m01, (float)m10);
     }
     // ---- 7x7 Gaussian (float path) over [9, W-10] x [9, H-10] into U
     const int BW = W - 2 * kBl0, BH = H - 2 * kBl0;
@@ -1092,10 +1122,10 @@ __global__ __launch_bounds__(256) void k_count_min(const int32_t* __restrict__ c
 // phases: 0 stage, 1 resize, 2 FAST map, 3 NMS, 4 retainBest(2n), 5 Harris,
 // 6 rank + retainBest(n), 7 IC angle, 8 blur, 9 rBRIEF + write (cycles summed
 // over workgroups); reads and clears the counters.
-extern "C" int slam_orb_profile_read(unsigned long long* out16) {
+extern "C" int slam_orb_profile_read(unsigned long long* out96) {
   SLAM_HIP(hipDeviceSynchronize());
-  SLAM_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_orb_prof), 16 * sizeof(unsigned long long)));
-  unsigned long long z[16] = {};
+  SLAM_HIP(hipMemcpyFromSymbol(out96, HIP_SYMBOL(g_orb_prof), 96 * sizeof(unsigned long long)));
+  unsigned long long z[96] = {};
   SLAM_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_orb_prof), z, sizeof(z)));
   return SLAM_OK;
 }
