@@ -431,16 +431,20 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
       const uint32_t cc = (uint32_t)(lo >> 24);                    // a .. a+3
       const uint32_t rt = (uint32_t)(((uint64_t)q2 << 32 | q1) >> 16);  // a+3 .. a+6
       const uint32_t okv[2] = {quick4(cc, dn, rt, up, q0), quick4(cc >> 8, dn >> 8, rt >> 8, up >> 8, q0 >> 8)};
+      // most waves hold no survivor at all (flat regions): one ballot skips
+      // the four queue appends
+      if (__ballot(gv && (okv[0] | okv[1]) != 0u) != 0ull) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool in = gv && x + q < SWd;
-        const bool ok = in && ((okv[q & 1] >> (16 * (q >> 1))) & 0xFFFFu) != 0u;
-        const uint64_t m = __ballot(ok);
-        if (ok)
-          fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-              (uint32_t)(y * SW4 + x + q);
-        nq += __popcll(m);
+        for (int q = 0; q < 4; ++q) {
+          const bool in = gv && x + q < SWd;
+          const bool ok = in && ((okv[q & 1] >> (16 * (q >> 1))) & 0xFFFFu) != 0u;
+          const uint64_t m = __ballot(ok);
+          if (ok)
+            fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                (uint32_t)(y * SW4 + x + q);
+          nq += __popcll(m);
+        }
       }
       if (gv) *reinterpret_cast<uint32_t*>(Smap + y * SW4 + x) = 0u;
       }
@@ -493,16 +497,18 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
           y = yy + kEdge;
           w4 = *reinterpret_cast<const uint32_t*>(Smap + (y - kNMS0) * SW4 + 4 * g4);
         }
+        if (__ballot(w4 != 0u) != 0ull) {  // (no scored pixel in the wave: nothing to queue)
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb) {
-          const int x = kNMS0 + 4 * g4 + bb;
-          const bool ok = ((w4 >> (8 * bb)) & 255u) != 0u && x >= kEdge && x <= W - 1 - kEdge;
-          const uint64_t m = __ballot(ok);
-          if (ok)
-            fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-                ((uint32_t)y << 12) | (uint32_t)x;
-          nq += __popcll(m);
+          for (int bb = 0; bb < 4; ++bb) {
+            const int x = kNMS0 + 4 * g4 + bb;
+            const bool ok = ((w4 >> (8 * bb)) & 255u) != 0u && x >= kEdge && x <= W - 1 - kEdge;
+            const uint64_t m = __ballot(ok);
+            if (ok)
+              fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                  ((uint32_t)y << 12) | (uint32_t)x;
+            nq += __popcll(m);
+          }
         }
         while (nq >= 64 || (!more && nq > 0)) {
           const int n = min(nq, 64);
