@@ -485,6 +485,10 @@ __device__ __forceinline__ void ep_jacobi_round(EpGroup& G, int k, int kr, bool 
     vr[P] = act ? wp : vkp;
     vr[Q] = act ? wq : vkq;
   }
+  // pin V's rotated values here: left free, the compiler defers the V chain
+  // and keeps every round's (c, s) live across the sweep (22 VGPRs a round)
+#pragma unroll
+  for (int j = 0; j < n; ++j) asm volatile("" : "+v"(vr[j]));
   // rows (J^T (A J)) of the pair holding k; a finished group copies its row
 #pragma unroll
   for (int j = 0; j < n; ++j) {
@@ -641,10 +645,15 @@ __device__ __forceinline__ void ep_approx(int approx, const double* pw, const do
     if (xb[1] < 0.0) be[0] = -be[0];
     if (approx == 2) be[2] = xb[3] / be[0];
   }
+#pragma unroll 1
   for (int it = 0; it < 5; ++it) {
     double Ag[24], bg[6], dx[4];
+    // an opaque offset: L is re-read from LDS every iteration (hoisted out of
+    // the loop, its 60 values would hold 120 registers)
+    int lo = 0;
+    asm volatile("" : "+v"(lo));
     for (int j = 0; j < 6; ++j) {
-      const double* l = G.L + 10 * j;
+      const double* l = G.L + 10 * j + lo;
       Ag[4 * j + 0] = 2.0 * l[0] * be[0] + l[1] * be[1] + l[3] * be[2] + l[6] * be[3];
       Ag[4 * j + 1] = l[1] * be[0] + 2.0 * l[2] * be[1] + l[4] * be[2] + l[7] * be[3];
       Ag[4 * j + 2] = l[3] * be[0] + l[4] * be[1] + 2.0 * l[5] * be[2] + l[8] * be[3];
