@@ -390,6 +390,42 @@ typedef struct slam_ba_problem {
 #define SLAM_BA_MAX_BATCH 16
 #endif
 
+/* ---- host planner of the camera-union linearisation (lin_mode 1) ----------
+ * slam355/ba.py plan_mfma in native code (the same tables, element for
+ * element; no HIP call, callable without a GPU): observations sorted by
+ * (point, camera), points renumbered by camera span, chunks of <= 120
+ * observations / 16 points, supergroups of <= chunks_per_wg chunks seeing
+ * <= 7 cameras.  Replaces the Python planner that BundleAdjustment-style
+ * callers (BundleAdjustment.py:331-402 via slam355.ba.BAProblem) pay per
+ * window.  The tables go into one int32 buffer `out`, table k at info->off[k]
+ * (256-byte aligned), info->len[k] entries; sizes in info.  info->ok = 0
+ * (and SLAM_OK) when a point has > 120 observations or > 7 cameras: the slot
+ * linearisation (lin_mode 0) applies.  chunks_per_wg <= 0: the default rule
+ * of plan_mfma.  block_list (packed layout, 9C > 120; may be null): the
+ * upper blocks to list, as BAProblem's block_list. */
+enum {
+  SLAM_PLAN_PERM = 0,      /* [P] device point k = caller's point perm[k]      */
+  SLAM_PLAN_ORDER,         /* [O] observation order (qs[order] -> obs_q)       */
+  SLAM_PLAN_OBS_CAM, SLAM_PLAN_OBS_PT, SLAM_PLAN_PT_PTR, SLAM_PLAN_GRP_PTR,
+  SLAM_PLAN_GRP_CSLOT, SLAM_PLAN_CSLOT_CAM, SLAM_PLAN_GRP_BSLOT, SLAM_PLAN_BSLOT_BLK,
+  SLAM_PLAN_BLOCKS, SLAM_PLAN_CAM_CSLOT_PTR, SLAM_PLAN_CSLOT_ROW, SLAM_PLAN_BLK_BSLOT_PTR,
+  SLAM_PLAN_BSLOT_ROW, SLAM_PLAN_SG_PTR, SLAM_PLAN_SG_META, SLAM_PLAN_SG_CAMS,
+  SLAM_PLAN_OBS_LA, SLAM_PLAN_CHK_COBS, SLAM_PLAN_OBS_META, SLAM_PLAN_CHK_OPTR,
+  SLAM_PLAN_CHK_CPTR, SLAM_PLAN_BSLOT_AB,
+  SLAM_PLAN_NTAB
+};
+typedef struct slam_ba_plan_info {
+  int32_t ok, n_obs, n_grps, n_sgrps, n_cslots, n_bslots, n_blocks, chunks_per_wg;
+  long long off[SLAM_PLAN_NTAB], len[SLAM_PLAN_NTAB];
+  long long total;  /* int32 slots written */
+} slam_ba_plan_info;
+/* int32 slots `out` needs for any plan of this size (0 on bad sizes). */
+long long slam_ba_plan_bound(int n_cams, int n_pts, int n_obs, int n_block_list);
+int slam_ba_plan_mfma(int n_cams, int n_pts, int n_obs, const int32_t* cam_idx,
+                      const int32_t* pt_idx, const int32_t* block_list, int n_block_list,
+                      int chunks_per_wg, int32_t* out, long long out_cap,
+                      slam_ba_plan_info* info);
+
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);
 /* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120). */

@@ -45,6 +45,21 @@ class BAProblemStruct(ctypes.Structure):
 
 _PROB = ctypes.POINTER(BAProblemStruct)
 
+PLAN_TABLES = ("perm", "order", "obs_cam", "obs_pt", "pt_ptr", "grp_ptr", "grp_cslot", "cslot_cam",
+               "grp_bslot", "bslot_blk", "blocks", "cam_cslot_ptr", "cslot_row", "blk_bslot_ptr",
+               "bslot_row", "sg_ptr", "sg_meta", "sg_cams", "obs_la", "chk_cobs", "obs_meta",
+               "chk_optr", "chk_cptr", "bslot_ab")  # SLAM_PLAN_* order
+
+
+class PlanInfo(ctypes.Structure):
+    """Mirror of `slam_ba_plan_info` (include/slam355.h)."""
+    _fields_ = [
+        ("ok", c_i32), ("n_obs", c_i32), ("n_grps", c_i32), ("n_sgrps", c_i32),
+        ("n_cslots", c_i32), ("n_bslots", c_i32), ("n_blocks", c_i32), ("chunks_per_wg", c_i32),
+        ("off", ctypes.c_longlong * len(PLAN_TABLES)), ("len", ctypes.c_longlong * len(PLAN_TABLES)),
+        ("total", ctypes.c_longlong),
+    ]
+
 # name -> argtypes (restype is int unless listed in _RESTYPE)
 SIGNATURES = {
     "slam_abi_version": [],
@@ -123,8 +138,12 @@ SIGNATURES = {
     "slam_comm_destroy": [c_p],
     "slam_comm_allreduce_f64": [c_p, c_p, ctypes.c_longlong, c_p],
     "slam_ba_step_distributed": [_PROB, c_p, c_p],
+    "slam_ba_plan_bound": [c_int, c_int, c_int, c_int],
+    "slam_ba_plan_mfma": [c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_int, c_p, c_longlong,
+                          ctypes.POINTER(PlanInfo)],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
+            "slam_ba_plan_bound": ctypes.c_longlong,
             "slam_ba_chol_len": ctypes.c_longlong, "slam_pnp_workspace_len": ctypes.c_longlong, "slam_pose_chain_workspace_len": ctypes.c_longlong}
 
 

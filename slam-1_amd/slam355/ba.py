@@ -604,6 +604,46 @@ def plan_mfma(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=Non
         n_obs=O, n_grps=G, n_sgrps=NS, chunks_per_wg=S)
 
 
+_PLAN_SHAPES = {"blocks": 2, "sg_meta": 24, "sg_cams": 8, "chk_cptr": 8}
+
+
+def plan_mfma_native(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per_wg=None):
+    """plan_mfma in native code (libslam355 slam_ba_plan_mfma, host only): the
+    same tables, as numpy views of ONE int32 buffer (`buf`, table k at
+    `offs[k]`, 256-byte aligned) so BAProblem uploads them with a single copy.
+    None when a point sees more than MF_CAMS cameras (or has more than
+    MF_CHUNK_OBS observations)."""
+    cam_idx = np.ascontiguousarray(cam_idx, np.int32).ravel()
+    pt_idx = np.ascontiguousarray(pt_idx, np.int32).ravel()
+    O = len(cam_idx)
+    bl = None if block_list is None else np.ascontiguousarray(np.unique(block_list), np.int32)
+    nbl = 0 if bl is None else len(bl)
+    cap = int(_lib.lib.slam_ba_plan_bound(n_cams, n_pts, O, nbl))
+    if cap <= 0:
+        raise ValueError("plan_mfma_native: bad sizes")
+    buf = np.empty(cap, np.int32)
+    info = _lib.PlanInfo()
+    _lib.call("slam_ba_plan_mfma", n_cams, n_pts, O, cam_idx.ctypes.data, pt_idx.ctypes.data,
+              None if bl is None else bl.ctypes.data, nbl,
+              0 if chunks_per_wg is None else int(chunks_per_wg), buf.ctypes.data, cap,
+              ctypes.byref(info))
+    if not info.ok:
+        return None
+    buf = buf[:info.total]
+    pl = dict(mode=1, buf=buf, offs={}, n_obs=info.n_obs, n_grps=info.n_grps,
+              n_sgrps=info.n_sgrps, chunks_per_wg=info.chunks_per_wg)
+    for k, name in enumerate(_lib.PLAN_TABLES):
+        off, n = info.off[k], info.len[k]
+        v = buf[off:off + n]
+        if name in _PLAN_SHAPES:
+            v = v.reshape(-1, _PLAN_SHAPES[name])
+        pl[name] = v
+        pl["offs"][name] = off
+    one = np.zeros(1, np.int32)
+    pl.update(cslot_obs_ptr=one, cslot_obs=one, bslot_pair_ptr=one, bslot_pairs=one)
+    return pl
+
+
 def assembly_table(n_cams, pl):
     """asm_tab of the folded assembly (include/slam355.h): need[NB] (partial rows
     per listed block: camera rows of its camera when diagonal + its block rows),
@@ -686,7 +726,7 @@ class BAProblem:
         cam_idx, pt_idx, qs = _check_indices(C, P, cam_idx, pt_idx, qs)
         pl = None
         if lin_mode in ("auto", "mfma"):
-            pl = plan_mfma(C, P, cam_idx, pt_idx, block_list, chunks_per_wg)
+            pl = plan_mfma_native(C, P, cam_idx, pt_idx, block_list, chunks_per_wg)
             if pl is None and lin_mode == "mfma":
                 raise ValueError(f"lin_mode 'mfma': a point is seen by more than {MF_CAMS} cameras")
         elif lin_mode != "slot":
@@ -708,9 +748,17 @@ class BAProblem:
         t["cams0"], t["cams1"] = T(cams), T(cams.copy())
         t["pts0"], t["pts1"] = T(pts), T(pts.copy())
         t["camrec0"], t["camrec1"] = z(C * 32), z(C * 32)
-        for k in _INDEX_TABLES + (_MFMA_TABLES if pl["mode"] == 1 else ()):
-            arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
-            t[k] = T(arr.astype(np.int32))
+        if "buf" in pl:  # native plan: every table in one buffer, one copy
+            t["plan_buf"] = T(pl["buf"])
+            for k in _INDEX_TABLES + _MFMA_TABLES:
+                if k in pl["offs"]:
+                    t[k] = t["plan_buf"][pl["offs"][k]:]  # (a zero-length table keeps its slot)
+                else:
+                    t[k] = T(pl[k].astype(np.int32))
+        else:
+            for k in _INDEX_TABLES + (_MFMA_TABLES if pl["mode"] == 1 else ()):
+                arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
+                t[k] = T(arr.astype(np.int32))
         t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
         C9 = 9 * C
         n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])

@@ -887,3 +887,66 @@ def test_assembly_table_counts_every_partial_row():
     assert set(empty) == set(np.nonzero(need == 0)[0])
     gaps = blocks[empty, 1] - blocks[empty, 0]
     assert (gaps > 5).all() and len(empty) == sum(10 - d for d in range(6, 10))
+
+
+def _rand_structure(rng, C, P, maxk, dup=0.02, empty=0.02):
+    ci, pi = [], []
+    for p in range(P):
+        if rng.random() < empty:
+            continue
+        k = min(int(rng.integers(1, maxk + 1)), C)
+        cs = rng.choice(C, size=k, replace=False) if rng.random() < 0.5 else \
+            (rng.integers(0, C) + np.arange(k)) % C
+        for c in cs:
+            ci.append(c)
+            pi.append(p)
+            if rng.random() < dup:  # a point observed twice by one camera
+                ci.append(c)
+                pi.append(p)
+    idx = rng.permutation(len(ci))
+    return np.asarray(ci, np.int64)[idx], np.asarray(pi, np.int64)[idx]
+
+
+def _same_plan(C, P, ci, pi, block_list=None, cpw=None):
+    from slam355 import _lib, ba
+
+    a = ba.plan_mfma(C, P, ci, pi, block_list, cpw)
+    b = ba.plan_mfma_native(C, P, ci, pi, block_list, cpw)
+    assert (a is None) == (b is None)
+    if a is None:
+        return
+    for k in ("n_obs", "n_grps", "n_sgrps", "chunks_per_wg"):
+        assert a[k] == b[k], k
+    for k in _lib.PLAN_TABLES:
+        x, y = np.asarray(a[k], np.int64), np.asarray(b[k], np.int64)
+        assert x.shape == y.shape and np.array_equal(x, y), k
+
+
+@pytest.mark.parametrize("C,P,maxk", [(8, 950, 3), (10, 5000, 6), (20, 3000, 5), (64, 4000, 7),
+                                      (3, 10, 2), (1, 5, 1), (70, 2000, 7)])
+def test_native_planner_equals_plan_mfma(C, P, maxk):
+    """slam_ba_plan_mfma (C++) gives plan_mfma's tables element for element:
+    tracked-, C3- and packed-size structures, repeated (point, camera) pairs,
+    unobserved points, every chunks_per_wg rule."""
+    rng = np.random.default_rng(C * 1000 + P)
+    for cpw in (None, 1, 3, 8):
+        ci, pi = _rand_structure(rng, C, P, maxk)
+        _same_plan(C, P, ci, pi, None, cpw)
+
+
+def test_native_planner_block_list_and_edges():
+    from slam355 import _lib, ba
+
+    rng = np.random.default_rng(5)
+    C = 20
+    ci, pi = _rand_structure(rng, C, 2000, 4)
+    bl = np.concatenate([ba.upper_blocks(C, ci, pi), [ba.block_index(0, C - 1, C)]])
+    _same_plan(C, 2000, ci, pi, bl)
+    with pytest.raises(_lib.SlamError, match="block_list misses"):
+        ba.plan_mfma_native(C, 2000, ci, pi, ba.upper_blocks(C, ci, pi)[:C])
+    _same_plan(10, 1, np.arange(8), np.zeros(8, np.int64))  # 8 cameras on a point: slot mode
+    assert ba.plan_mfma_native(10, 1, np.arange(8), np.zeros(8, np.int64)) is None
+    _same_plan(5, 0, np.zeros(0, np.int64), np.zeros(0, np.int64))
+    _same_plan(5, 3, np.zeros(0, np.int64), np.zeros(0, np.int64))
+    with pytest.raises(_lib.SlamError, match="out of range"):
+        ba.plan_mfma_native(5, 3, np.array([5]), np.array([0]))
