@@ -664,6 +664,7 @@ def tracked_window_ba(feed, B, rig, args, n_pairs=8):
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     cams, pts, ci, pi, qs = lm.problem(rig.P_l)
+    t1b = time.perf_counter()
     prob = BAProblem(cams, pts, ci, pi, qs)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
@@ -681,6 +682,8 @@ def tracked_window_ba(feed, B, rig, args, n_pairs=8):
     return {"frames": n_pairs + 1, "n_cams": int(len(cams)), "n_pts": int(len(pts)),
             "n_obs": int(len(ci)), "track_and_map_ms": (t_map - t0) * 1e3,
             "host_problem_build_ms": (t2 - t1) * 1e3,
+            "host_problem_build_split_ms": {"problem_from_map": (t1b - t1) * 1e3,
+                                            "ba_problem_plan_upload": (t2 - t1b) * 1e3},
             "lm_ms_per_iter": e0.elapsed_time(e1) / args.ba_iters, "lm_iters": args.ba_iters,
             "cost_first": cost0, "cost_final": st["COST"], "accepted": int(st["NACCEPT"]),
             "lin_mode": prob.lin_mode}

@@ -37,13 +37,14 @@ def _pose(frame):
 
 def make_cam_params(camera_frames, P_left):
     """(:16-32) [rotvec(pose R), pose t, f = P_left[0][0], 0, 0] per frame, flat."""
-    out = np.empty(9 * len(camera_frames))
-    for j, fr in enumerate(camera_frames):
-        T = _pose(fr)
-        out[9 * j: 9 * j + 3] = Rotation.from_matrix(T[:3, :3]).as_rotvec()
-        out[9 * j + 3: 9 * j + 6] = T[:3, 3]
-        out[9 * j + 6: 9 * j + 9] = (P_left[0][0], 0, 0)
-    return out
+    out = np.empty((len(camera_frames), 9))
+    if len(camera_frames):
+        Ts = np.stack([_pose(fr) for fr in camera_frames])
+        # one stacked conversion: per matrix the same operations as one call each
+        out[:, 0:3] = Rotation.from_matrix(Ts[:, :3, :3]).as_rotvec()
+        out[:, 3:6] = Ts[:, :3, 3]
+        out[:, 6:9] = (P_left[0][0], 0, 0)
+    return out.ravel()
 
 
 def make_Qs_for_BA(Qs):

@@ -743,11 +743,7 @@ class BAProblem:
         self.C, self.P, self.O = C, P, pl["n_obs"]
         self.stream = stream
         T = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        z = lambda n: torch.zeros(max(int(n), 1), dtype=torch.float64, device=dev)  # noqa: E731
         self.t = t = {}
-        t["cams0"], t["cams1"] = T(cams), T(cams.copy())
-        t["pts0"], t["pts1"] = T(pts), T(pts.copy())
-        t["camrec0"], t["camrec1"] = z(C * 32), z(C * 32)
         if "buf" in pl:  # native plan: every table in one buffer, one copy
             t["plan_buf"] = T(pl["buf"])
             for k in _INDEX_TABLES + _MFMA_TABLES:
@@ -759,24 +755,46 @@ class BAProblem:
             for k in _INDEX_TABLES + (_MFMA_TABLES if pl["mode"] == 1 else ()):
                 arr = pl[k] if pl[k].size else np.zeros(1, np.int32)
                 t[k] = T(arr.astype(np.int32))
-        t["obs_q"] = T(qs[pl["order"]] if self.O else np.zeros((1, 2)))
         C9 = 9 * C
+        G = pl["n_grps"]
         n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])
-        t["cpart"] = z(n_cs * 112)
-        t["bpart"] = z(n_bs * 81)
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
-        t["sys"] = z(self.sys_len)
-        t["chol"] = z(_lib.lib.slam_ba_chol_len(C) if C9 > LDS_MAX_N else 1)
         self.tl_levels = C9 > LDS_MAX_N
+        # every float64 buffer in ONE device allocation (256-byte aligned
+        # segments): the parameters (two LM copies + the initial copy) and the
+        # permuted observations in one upload, the workspaces in one fill
+        up = [("cams0", cams), ("pts0", pts), ("cams1", cams), ("pts1", pts), ("init_c", cams),
+              ("init_p", pts), ("obs_q", qs[pl["order"]] if self.O else np.zeros((1, 2)))]
+        zero = [("camrec0", C * 32), ("camrec1", C * 32), ("cpart", n_cs * 112), ("bpart", n_bs * 81),
+                ("sys", self.sys_len), ("chol", _lib.lib.slam_ba_chol_len(C) if self.tl_levels else 1),
+                ("delta_c", C9), ("red_part", _lib.lib.slam_ba_red_slots(G)), ("small", 4),
+                ("state", N_STATE)]
+        al = lambda n: (max(int(n), 1) + 31) // 32 * 32  # noqa: E731
+        offs, o = {}, 0
+        for k, a in up:
+            offs[k] = o
+            o += al(np.size(a))
+        n_up = o
+        for k, n in zero:
+            offs[k] = o
+            o += al(n)
+        host = np.zeros(n_up, np.float64)
+        for k, a in up:
+            host[offs[k]:offs[k] + np.size(a)] = np.ravel(a)
+        arena = torch.empty(o, dtype=torch.float64, device=dev)
+        arena[:n_up].copy_(torch.from_numpy(host))
+        arena[n_up:].zero_()
+        t["f64_arena"] = arena
+        for k, a in up:
+            t[k] = arena[offs[k]:offs[k] + np.size(a)].view(np.shape(a))
+        for k, n in zero:
+            t[k] = arena[offs[k]:offs[k] + max(int(n), 1)]
         if self.tl_levels:  # level schedule of the tiled solve (host + device copies)
             self._sched_host = tl_schedule(C, pl["blocks"])
             t["tl_sched"] = T(self._sched_host)
-        t["delta_c"] = z(C9)
-        G = pl["n_grps"]
-        t["red_part"] = z(_lib.lib.slam_ba_red_slots(G))
         t["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
-        t["small"] = z(4)
-        t["state"] = z(N_STATE)
+        if stream is not None:  # the uploads and fills above ran on the current stream
+            stream.wait_stream(torch.cuda.current_stream(dev))
         s = _Prob()
         s.n_cams, s.n_pts, s.n_obs, s.n_grps = C, P, self.O, G
         s.n_blocks = len(pl["blocks"])
@@ -799,7 +817,7 @@ class BAProblem:
         self._s = s
         self.reset(lam0)
 
-        self._init = (t["cams0"].clone(), t["pts0"].clone())
+        self._init = (t["init_c"], t["init_p"])
 
     def restore(self, lam0=1e-4):
         """Reload the initial parameters and reset the LM state (device copies)."""
