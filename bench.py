@@ -163,6 +163,18 @@ def pmc_traffic(name="pmc_traffic.json"):
     return d
 
 
+def pmc_valu(kernel, name="pmc_sq.json"):
+    """(SQ_INSTS_VALU per dispatch of `kernel`, source path) from the committed
+    SQ counter summary profiles/<name> (scripts/gpu_profile.sh), or None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    k = json.load(open(path)).get("kernels", {}).get(kernel)
+    if not k or "SQ_INSTS_VALU" not in k:
+        return None
+    return float(k["SQ_INSTS_VALU"]), os.path.relpath(path, ROOT)
+
+
 def pmc_bytes(pmc, kernels):
     if pmc is None or not all(k in pmc["kernels"] for k in kernels):
         return None
@@ -533,6 +545,15 @@ def run_tracking(args, world, rank):
     roof["matcher"]["unique_descriptor_bytes"] = float(oc[:B].sum() + oc[B + 1:2 * B + 1].sum()) * 32
     pmc = pmc_traffic()
     roof["orb"]["traffic"] = pmc_bytes(pmc, ("k_orb_tile<false>", "k_orb_compact"))
+    # ORB is bound by instruction latency, not HBM: its vector-ALU issue rate
+    # (wave64 VALU instructions per launch from the SQ pass x 64 lanes over the
+    # launch time) against the VALU peak, beside the HBM fraction
+    vi = pmc_valu("k_orb_tile<false>")
+    if vi is not None:
+        valu = vi[0] * 64 / (orb_ms * 1e-3) / 1e12
+        roof["orb"]["valu"] = {"achieved": valu, "peak": VALU_PEAK_TOPS, "unit": "T lane-ops/s",
+                               "frac": valu / VALU_PEAK_TOPS, "valu_instr_per_launch": vi[0],
+                               "source": vi[1]}
     roof["local_ba"]["traffic"] = pmc_bytes(pmc, ("k_lin_mfma", "k_solve_blk", "k_back_trial<true>")
                                             + (() if args.fold else ("k_assemble",)))
     roof["matcher"]["traffic"] = pmc_bytes(pmc, (roof["matcher"]["kernel"].split()[0],))
