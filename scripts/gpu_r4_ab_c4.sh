@@ -6,7 +6,7 @@ set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
 TAG=$1; VAR=$2; shift 2
-OUT=gpurun_out/$TAG; mkdir -p $OUT
+OUT=$TAG; case $OUT in gpurun_out/*) ;; *) OUT=gpurun_out/$TAG;; esac; mkdir -p $OUT
 for i in 1 2 3; do
   for v in def var; do
     if [ $v = var ]; then export SLAM355_LIB=$ROOT/$VAR; else unset SLAM355_LIB; fi

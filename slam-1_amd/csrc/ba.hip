@@ -1306,26 +1306,84 @@ struct EpiSrc {
 };
 
 // Shared epilogue: camera step, trial cameras, predicted reduction of the camera
-// part, LM cost at the live parameters.
+// part, LM cost at the live parameters.  GLOBAL (the tiled solves, 9C up to
+// 8192): the inputs are read from memory, so every thread issues its loads in
+// groups of 8 before using them (the per-thread order of the pc sum is the
+// same), and the per-camera cost is summed by all threads (strided, then the
+// fixed tree of block_sum2) instead of by thread 0 alone -- at C5 the serial
+// forms were ~18 dependent memory round trips per thread plus 500 dependent
+// loads and adds.
+__device__ __forceinline__ void block_sum2(double& a, double& b, double* lds) {
+  // deterministic: fixed shuffle tree then fixed LDS order (lds: 2 x 16 doubles)
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_down(a, off, 64);
+    b += __shfl_down(b, off, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    lds[wid] = a;
+    lds[16 + wid] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    a = 0.0;
+    b = 0.0;
+    for (int w = 0; w < nw; ++w) {
+      a += lds[w];
+      b += lds[16 + w];
+    }
+  }
+  __syncthreads();
+}
+
+template <bool GLOBAL = false>
 __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool ok, double* red,
                                const EpiSrc& e, int fail_code = 1) {
   const int C9 = 9 * p.n_cams, t = threadIdx.x;
   double* state = p.state;
   const double lam = state[SLAM_BA_ST_LAMBDA];
   const int cur = cur_of(state);
-  double pc = 0.0;
-  for (int i = t; i < C9; i += blockDim.x) {
-    const double d = ok ? x[i] : 0.0;
-    p.delta_c[i] = d;
-    p.cams[1 - cur][i] = e.cam[i] + d;
-    pc += d * (lam * clampd(e.dU[i]) * d + e.g[i]);
+  double pc = 0.0, cost = 0.0;
+  if constexpr (GLOBAL) {
+    const int nt = blockDim.x;
+    for (int i0 = t; i0 < C9; i0 += 8 * nt) {
+      double xv[8], cv[8], uv[8], gv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = min(i0 + q * nt, C9 - 1);
+        xv[q] = x[i];
+        cv[q] = e.cam[i];
+        uv[q] = e.dU[i];
+        gv[q] = e.g[i];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int i = i0 + q * nt;
+        if (i < C9) {
+          const double d = ok ? xv[q] : 0.0;
+          p.delta_c[i] = d;
+          p.cams[1 - cur][i] = cv[q] + d;
+          pc += d * (lam * clampd(uv[q]) * d + gv[q]);
+        }
+      }
+    }
+    for (int c = t; c < p.n_cams; c += nt) cost += e.costc[c];
+    block_sum2(pc, cost, red);  // (its barriers also publish the trial cameras to the WG)
+  } else {
+    for (int i = t; i < C9; i += blockDim.x) {
+      const double d = ok ? x[i] : 0.0;
+      p.delta_c[i] = d;
+      p.cams[1 - cur][i] = e.cam[i] + d;
+      pc += d * (lam * clampd(e.dU[i]) * d + e.g[i]);
+    }
+    pc = block_sum(pc, red);  // (its barriers also publish the trial cameras to the WG)
+    if (t == 0)
+      for (int c = 0; c < p.n_cams; ++c) cost += e.costc[c];
   }
-  pc = block_sum(pc, red);  // (its barriers also publish the trial cameras to the WG)
   for (int c = t; c < p.n_cams; c += blockDim.x)
     cam_prep(p.cams[1 - cur] + 9 * c, p.camrec[1 - cur] + kCamRec * c);
   if (t == 0) {
-    double cost = 0.0;
-    for (int c = 0; c < p.n_cams; ++c) cost += e.costc[c];
     state[SLAM_BA_ST_COST] = 0.5 * cost;
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
     state[SLAM_BA_ST_CHOL_FAIL] = ok ? 0.0 : (double)fail_code;
@@ -1908,28 +1966,54 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
       // rows of the 16x16 diagonal block in lanes i = l & 15 of every 16-lane
-      // DPP row (lower part read; the four rows of the wave hold copies).  L(m, j)
-      // (= lane m's l_ij) reaches the other lanes of the row as a DPP
-      // row_newbcast operand: no LDS round trip and no SGPR hop in the pivot chain.
+      // DPP row (lower part read; the four rows of the wave hold copies); lane
+      // m's values reach the other lanes of the row as DPP row_newbcast operands:
+      // no LDS round trip and no SGPR hop in the pivot chain.
+      //
+      // 2x2 block pivots: A = L D L^T with L unit lower and D = diag of 2x2
+      // blocks [a b; b c], eliminated a pair of columns per step.  The chain of a
+      // step is the pair's broadcast, det = ac - b^2, one reciprocal and the
+      // update of the next pair's rows -- half the steps of the scalar Cholesky,
+      // and no square root on it: the update operands (lane m's unscaled column
+      // values) are known before the reciprocal.  The Cholesky factor is L C
+      // with D's block = C C^T (C00 = sqrt(a), C10 = b / C00, C11 = sqrt(c -
+      // C10^2)), formed off the chain; so L_pp is the same lower-triangular
+      // factor as before up to rounding.
       const int i = l & 15;
       double v[16], rj[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const double djj = bcast16<j>(v[j]);
-        ok = ok && djj > 0.0 && djj < INFINITY;
-        double r = __builtin_amdgcn_rsq(djj);
-        const double h = 0.5 * djj;
-        r = r * __builtin_fma(-h * r, r, 1.5);
-        r = r * __builtin_fma(-h * r, r, 1.5);
-        rj[j] = r;
-        const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
-        v[j] = lij;
-        static_for<j + 1, 16>([&](auto Mi) {
+      static_for<0, 8>([&](auto Q) {
+        constexpr int j = 2 * decltype(Q)::value;
+        const double a = bcast16<j>(v[j]);
+        const double b = bcast16<j + 1>(v[j]);
+        const double c = bcast16<j + 1>(v[j + 1]);
+        const double det = __builtin_fma(a, c, -(b * b));
+        ok = ok && a > 0.0 && a < INFINITY && det > 0.0 && det < INFINITY;
+        const double rd = rcp_f64(det);
+        const double p0 = v[j], p1 = v[j + 1];
+        const double l0 = __builtin_fma(p0, c, -(p1 * b)) * rd;  // (p0, p1) D^-1
+        const double l1 = __builtin_fma(p1, a, -(p0 * b)) * rd;
+        static_for<j + 2, 16>([&](auto Mi) {
           constexpr int m = decltype(Mi)::value;
-          v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
+          v[m] = __builtin_fma(-l0, bcast16<m>(p0), __builtin_fma(-l1, bcast16<m>(p1), v[m]));
         });
+        // off the chain: D's block = C C^T, rows of the factor L C
+        double r0 = __builtin_amdgcn_rsq(a);
+        const double h0 = 0.5 * a;
+        r0 = r0 * __builtin_fma(-h0 * r0, r0, 1.5);
+        r0 = r0 * __builtin_fma(-h0 * r0, r0, 1.5);
+        const double c00 = a * r0, c10 = b * r0;
+        const double s1 = __builtin_fma(-c10, c10, c);
+        double r1 = __builtin_amdgcn_rsq(s1);
+        const double h1 = 0.5 * s1;
+        r1 = r1 * __builtin_fma(-h1 * r1, r1, 1.5);
+        r1 = r1 * __builtin_fma(-h1 * r1, r1, 1.5);
+        const double c11 = s1 * r1;
+        rj[j] = r0;      // 1 / l_jj
+        rj[j + 1] = r1;  // 1 / l_j+1,j+1
+        v[j] = i > j + 1 ? __builtin_fma(l0, c00, l1 * c10) : (i == j ? c00 : (i == j + 1 ? c10 : 0.0));
+        v[j + 1] = i > j + 1 ? l1 * c11 : (i == j + 1 ? c11 : 0.0);
       });
       // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
       // (column-oriented: once x_k is known, every later row's sum takes its
@@ -2028,16 +2112,32 @@ __device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) {
 }
 
 // Zero the lower tiles (identity on the padded rows' diagonal), b in the new order.
-__global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p) {
+// struct_only: only the tiles the symbolic factor touches -- (J, J) and (I, J)
+// for the rows I of column J (column table; grid T x (1 + max rows)); every
+// other lower tile is never read by either solve form (C5: 71 diagonal + row
+// tiles of 2556 lower tiles).  Otherwise all T (T + 1) / 2 lower tiles.
+__global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p, int struct_only) {
   lm_wave_priority();
   const int n = 9 * p.n_cams;
   const TlLayout L(n);
   const int32_t* S = p.tl_sched;
-  const int idx = blockIdx.x;
-  int I = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
-  while ((I + 1) * (I + 2) / 2 <= idx) ++I;
-  while (I * (I + 1) / 2 > idx) --I;
-  const int J = idx - I * (I + 1) / 2;
+  int I, J;
+  bool first;
+  if (struct_only) {
+    J = blockIdx.x;
+    const int q = blockIdx.y;
+    const int32_t* rec = S + S[5] + 5 * J;
+    if (q > rec[1]) return;  // uniform; (0, 0) always runs
+    I = q == 0 ? J : S[rec[0] + q - 1];
+    first = blockIdx.x == 0 && q == 0;
+  } else {
+    const int idx = blockIdx.x;
+    I = (int)((sqrtf(8.0f * (float)idx + 1.0f) - 1.0f) * 0.5f);
+    while ((I + 1) * (I + 2) / 2 <= idx) ++I;
+    while (I * (I + 1) / 2 > idx) --I;
+    J = idx - I * (I + 1) / 2;
+    first = idx == 0;
+  }
   double* A = p.chol + L.a;
   const int oldI = S[S[3] + I];  // padded rows live in the old last tile
   for (int e = threadIdx.x; e < kTB * kTB; e += kTlWG) {
@@ -2049,7 +2149,7 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p) {
     p.chol[L.b + I * kTB + threadIdx.x] =
         r < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
   }
-  if (idx == 0) {
+  if (first) {
     // k_tl3_flow: a new solve epoch (its flags compare against it); the retire
     // ticket, the start ticket and the per-column parent counters re-armed
     int* fl = reinterpret_cast<int*>(p.chol + L.flow) + L.T * L.T + 2 * L.T;
@@ -2248,8 +2348,8 @@ __global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
   const bool ok = !tl_failed(p, L);
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
   const double* gvec = bvec + n;
-  solve_epilogue(p, p.chol + L.y, ok, red,
-                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
+  solve_epilogue<true>(p, p.chol + L.y, ok, red,
+                       EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n});
 }
 
 // ---------------------------------------------------------------- dataflow tiled solve
@@ -2446,6 +2546,10 @@ __device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf,
   }
 }
 
+// lower 16x16 blocks (row, column) of the diagonal update per wave of k_tl3_flow
+__constant__ int kDiagBlk[4][3][2] = {{{0, 0}, {3, 0}, {3, 1}}, {{1, 0}, {1, 1}, {3, 2}},
+                                      {{2, 0}, {2, 1}, {2, 0}}, {{2, 2}, {3, 3}, {2, 2}}};
+
 __global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_tl3_flow(slam_ba_problem p) {
   lm_wave_priority();
@@ -2477,14 +2581,25 @@ void k_tl3_flow(slam_ba_problem p) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   bool ok = true;
   FLOW_T(0);
-  // A_JJ (scattered by the previous launch) in registers before any wait
-  double ajj[16];
+  // The diagonal update is symmetric and the factor reads only lower blocks:
+  // the 10 lower 16x16 blocks, three per wave (waves 2 and 3 repeat one block
+  // they do not store), so each SIMD's MFMA chain per child tile is 48 steps
+  // instead of 64.
+  int dR[3], dC[3];
 #pragma unroll
-  for (int s2 = 0; s2 < 4; ++s2)
+  for (int b = 0; b < 3; ++b) {
+    dR[b] = kDiagBlk[w][b][0];
+    dC[b] = kDiagBlk[w][b][1];
+  }
+  const int dnb = w < 2 ? 3 : 2;
+  // A_JJ's blocks (scattered by the previous launch) in registers before any wait
+  double ajj[12];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
-      ajj[4 * s2 + r] = A[(size_t)(J * kTB + row) * L.N + J * kTB + col];
+      const int row = dR[b] * 16 + (lane >> 4) + 4 * r, col = dC[b] * 16 + (lane & 15);
+      ajj[4 * b + r] = A[(size_t)(J * kTB + row) * L.N + J * kTB + col];
     }
   // ... and the first two row tiles' A_IJ
   double air[2][16];
@@ -2516,18 +2631,25 @@ void k_tl3_flow(slam_ba_problem p) {
       ok = flow_wait(F.tile + J * T + S[so + q + 1], epoch, fail, &shf);
       if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
     }
-    gemm_xyT_acc(cur, cur, acc);
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int b = 0; b < 3; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[((dR[b] * 16 + kk) << 6) + lane],
+                                                      cur[((dC[b] * 16 + kk) << 6) + lane], acc[b], 0, 0, 0);
   }
   __syncthreads();
   FLOW_T(1);
   if (ok) {
-    double* M = VX;
+    double* M = VX;  // lower blocks only (tile_chol_inv_blk reads no others)
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2)
+    for (int b = 0; b < 3; ++b)
+      if (b < dnb) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
-        M[row * kMS + col] = ajj[4 * s2 + r] - acc[s2][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = dR[b] * 16 + (lane >> 4) + 4 * r, col = dC[b] * 16 + (lane & 15);
+          M[row * kMS + col] = ajj[4 * b + r] - acc[b][r];
+        }
       }
     double* Xb = VX + kTB * kMS;
     ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf);
@@ -2746,11 +2868,18 @@ void k_tl3_flow(slam_ba_problem p) {
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
   const bool good = fcode == 0;
   double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
-  for (int i = t; i < n; i += kTlWG) xs[i] = good ? ld_sc1(p.chol + L.xo + i) : 0.0;
+  for (int i0 = t; i0 < n; i0 += 8 * kTlWG) {  // 8 loads in flight per thread
+    double xv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xv[q] = good ? ld_sc1(p.chol + L.xo + min(i0 + q * kTlWG, n - 1)) : 0.0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (i0 + q * kTlWG < n) xs[i0 + q * kTlWG] = xv[q];
+  }
   __syncthreads();
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
   const double* gvec = bvec + n;
-  solve_epilogue(p, xs, good, &part[0][0],
+  solve_epilogue<true>(p, xs, good, &part[0][0],
                  EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n}, fcode);
   FLOW_T(7);
 }
@@ -2766,11 +2895,24 @@ static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t) {
   return L.T <= SLAM_TL_FLOW_MAX_T && 9 * p.n_cams <= 2 * kTB * kTB;
 }
 
+// k_tl2_load over the structural tiles when the schedule carries the column table
+static void tl_load(const slam_ba_problem& p, hipStream_t s) {
+  const int32_t* h = p.tl_sched_host;
+  const int T = h[1];
+  if (h[5] > 0) {
+    int maxrc = 0;
+    for (int J = 0; J < T; ++J) maxrc = std::max(maxrc, (int)h[h[5] + 5 * J + 1]);
+    k_tl2_load<<<dim3(T, 1 + maxrc), kTlWG, 0, s>>>(p, 1);
+  } else {
+    k_tl2_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p, 0);
+  }
+}
+
 static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
   const TlLayout L(9 * p.n_cams);
   SLAM_REQUIRE(p.tl_sched_host[1] == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d",
                p.tl_sched_host[1], L.T);
-  k_tl2_load<<<L.T * (L.T + 1) / 2, kTlWG, 0, s>>>(p);
+  tl_load(p, s);
   k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
   k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p);
   SLAM_LAUNCHED("k_tl3_flow");
@@ -2783,7 +2925,7 @@ static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
   const int nlev = h[0], T = h[1];
   SLAM_REQUIRE(T == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d", T, L.T);
   const int32_t* tab = h + h[4];
-  k_tl2_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p);
+  tl_load(p, s);
   k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
   for (int lv = 0; lv < nlev; ++lv) {
     const int32_t* e = tab + 6 * lv;

@@ -180,12 +180,20 @@ __global__ __launch_bounds__(kWG) void knn2_kernel(
 //     wave partials are merged over the 16 column-lanes (shuffles), then over
 //     the 4 waves through LDS in wave order (keys are unique: the order is
 //     immaterial anyway);
-//   * byte -> 8 fp4 nibbles through two 1 KiB LDS tables (+1.0 / -2.0);
+//   * bits -> fp4 nibbles in registers, no tables: operand dword d of a
+//     32-bit descriptor word w is ((w >> d) & 0x11111111) times the nibble
+//     (+1.0 = 0x2, -2.0 = 0xC), i.e. nibble k of dword d is bit 4k + d -- a
+//     permutation of K shared by A and B, so every product pairs the same bit
+//     of query and train row (2-3 VALU ops per dword; the round-3 byte tables
+//     cost 2.8 LDS bank-conflict cycles per lookup);
 //   * operand map (scripts/micro/mx_hamming.hip, exact on the GPU): lane l
 //     holds row / column l & 15 and bits [32 (l >> 4), +32) of each 128-bit
-//     half as 32 nibbles, low nibble first (any k order shared by A and B is
-//     harmless); C/D: row 4 (l >> 4) + r, column l & 15 -- each lane keeps a
-//     partial top-2 of 4 queries per block over the columns = l mod 16.
+//     half as 32 nibbles (any k order shared by A and B is harmless); C/D:
+//     row 4 (l >> 4) + r, column l & 15 -- each lane keeps a partial top-2 of
+//     4 queries per block over the columns = l mod 16;
+//   * XCD-aware block order: the workgroups of one batch item are dealt to ONE
+//     XCD (blocks b and b + 8 share an XCD), so each item's train set is
+//     fetched into one L2 instead of all eight.
 // Train row index < 2^14 (t_cap <= 16383; larger sets take knn2_kernel).
 #ifndef SLAM_MX_WG
 #define SLAM_MX_WG 256
@@ -202,21 +210,32 @@ constexpr int kMxWaves = kMxWG / kWave;
 #endif
 constexpr int kMxQB = SLAM_MX_QB;          // (4 per step measured 10 % slower than 8 alone)
 constexpr int kMxQWG = 16 * kMxQB;         // queries per workgroup
-// the kernel fills its two 256-entry LUTs with one thread each and merges one
-// query per thread: the -D tunables must keep both within the group
-static_assert(kMxWG >= 256 && kMxWG >= kMxQWG && kMxWG % 64 == 0,
-              "knn2_mx_kernel: SLAM_MX_WG must cover the LUTs and 16 * SLAM_MX_QB queries");
+// the kernel merges one query per thread: the -D tunables must keep
+// every query of the workgroup within it
+static_assert(kMxWG >= kMxQWG && kMxWG % 64 == 0,
+              "knn2_mx_kernel: SLAM_MX_WG must cover 16 * SLAM_MX_QB queries");
 constexpr int kMxAhead = 2;                // train steps loaded ahead
 constexpr float kMxNone = 16777215.0f;     // > every valid key (< 2^23 + 2^14)
 typedef int mx_v8i __attribute__((ext_vector_type(8)));
 typedef float mx_v4f __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t spread8(uint32_t b, uint32_t nib) {  // 8 bits -> 8 nibbles
-  uint32_t x = b & 0xFFu;
-  x = (x | (x << 12)) & 0x000F000Fu;
-  x = (x | (x << 6)) & 0x03030303u;
-  x = (x | (x << 3)) & 0x11111111u;
-  return x * nib;
+// operand dword d (0..3) of a descriptor word: nibble k = bit 4k + d of w, as
+// fp4 +1.0 (0x2, query) or -2.0 (0xC, train)
+template <int D>
+__device__ __forceinline__ int nib_q(uint32_t w) {
+  return (int)(((w >> D) & 0x11111111u) << 1);
+}
+template <int D>
+__device__ __forceinline__ int nib_t(uint32_t w) {
+  const uint32_t x = (w >> D) & 0x11111111u;
+  return (int)((x << 3) | (x << 2));
+}
+
+// Blocks are dealt round-robin over the 8 XCDs (b and b + 8 share one): the
+// bijection that gives XCD x the contiguous virtual range of its blocks.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  const int x = b & 7, per = nb >> 3, rem = nb & 7;
+  return x * per + min(x, rem) + (b >> 3);
 }
 
 __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
@@ -224,19 +243,14 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
     const uint32_t* __restrict__ t, const int32_t* __restrict__ nt_arr, int t_cap,
     int tiles_per_item, int2* __restrict__ idx2, int2* __restrict__ dist2,
     uint8_t* __restrict__ good) {
-  __shared__ uint32_t lut[2][256];  // byte -> 8 fp4 nibbles: +1.0 (0x2), -2.0 (0xC)
   __shared__ uint32_t part[kMxWaves][kMxQWG][2];
-  const int item = blockIdx.x / tiles_per_item;
-  const int tile = blockIdx.x - item * tiles_per_item;
+  const int vb = xcd_block((int)blockIdx.x, (int)gridDim.x);
+  const int item = vb / tiles_per_item;
+  const int tile = vb - item * tiles_per_item;
   const int nq = min(max(nq_arr[item], 0), q_cap);
   const int nt = min(max(nt_arr[item], 0), t_cap);
   const int q0 = tile * kMxQWG;
   if (q0 >= nq) return;  // uniform over the workgroup
-  if (threadIdx.x < 256) {
-    lut[0][threadIdx.x] = spread8(threadIdx.x, 0x2u);
-    lut[1][threadIdx.x] = spread8(threadIdx.x, 0xCu);
-  }
-  __syncthreads();
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int l = threadIdx.x & (kWave - 1), r = l & 15, g = l >> 4;
   const uint32_t* qb = q + (size_t)item * q_cap * 8;
@@ -249,9 +263,7 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t w = qi < nq ? qb[(size_t)qi * 8 + 4 * h + g] : 0u;
-      A[b][h] = mx_v8i{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int d = 0; d < 4; ++d) A[b][h][d] = (int)lut[0][(w >> (8 * d)) & 255u];
+      A[b][h] = mx_v8i{nib_q<0>(w), nib_q<1>(w), nib_q<2>(w), nib_q<3>(w), 0, 0, 0, 0};
     }
   }
   uint32_t k1[kMxQB][4], k2[kMxQB][4];  // key bit patterns (non-negative floats)
@@ -261,7 +273,7 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
     for (int i = 0; i < 4; ++i) k1[b][i] = k2[b][i] = __float_as_uint(kMxNone);
   // this wave's steps: train rows 16 (wid + 4 s) + r; whole rows, kMxAhead
   // ahead.  Software pipeline: while the MFMAs of step s run, the operands of
-  // step s + 1 are formed (popcount, byte -> nibble tables) and the keys of
+  // step s + 1 are formed (popcount, bits -> nibbles) and the keys of
   // step s - 1 are folded into the top-2 (the loop is unrolled twice so the
   // two accumulator sets alternate by name).
   const int nsteps = (nt + 15) >> 4;
@@ -300,13 +312,8 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
     uint32_t w1 = g == 0 ? y.x : g == 1 ? y.y : g == 2 ? y.z : y.w;
     w0 = valid ? w0 : 0u;
     w1 = valid ? w1 : 0u;
-    o.B0 = mx_v8i{0, 0, 0, 0, 0, 0, 0, 0};
-    o.B1 = o.B0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      o.B0[d] = (int)lut[1][(w0 >> (8 * d)) & 255u];
-      o.B1[d] = (int)lut[1][(w1 >> (8 * d)) & 255u];
-    }
+    o.B0 = mx_v8i{nib_t<0>(w0), nib_t<1>(w0), nib_t<2>(w0), nib_t<3>(w0), 0, 0, 0, 0};
+    o.B1 = mx_v8i{nib_t<0>(w1), nib_t<1>(w1), nib_t<2>(w1), nib_t<3>(w1), 0, 0, 0, 0};
     return o;
   };
   // all first halves, then all second halves (independent accumulators
