@@ -1850,18 +1850,21 @@ __device__ __forceinline__ void tile_to_frag(const double* __restrict__ g, int l
   }
 }
 
-// acc[s] (wave w) = rows 16w.., cols 16s.. of X Y^T, X and Y in fragment order
-__device__ __forceinline__ void gemm_xyT(const double* Xf, const double* Yf, d4 acc[4]) {
+// acc[s] (wave w) = rows 16w.., cols 16s.. of X Y^T with Y LOWER triangular
+// (L_kk^-1): column block s takes only the k-steps kk <= 4s + 3 (Y's entries
+// past them are exact zeros), 40 of the 64 MFMAs -- the same sums.
+__device__ __forceinline__ void gemm_xyT_lowY(const double* Xf, const double* Yf, d4 acc[4]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll 4
-  for (int kk = 0; kk < 16; ++kk) {
+  static_for<0, 16>([&](auto K) {
+    constexpr int kk = decltype(K)::value;
     const double a = Xf[((w * 16 + kk) << 6) + lane];
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
+    static_for<kk / 4, 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
       acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + lane], acc[s], 0, 0, 0);
-  }
+    });
+  });
 }
 
 __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayout& L) {
@@ -1966,54 +1969,28 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
       // rows of the 16x16 diagonal block in lanes i = l & 15 of every 16-lane
-      // DPP row (lower part read; the four rows of the wave hold copies); lane
-      // m's values reach the other lanes of the row as DPP row_newbcast operands:
-      // no LDS round trip and no SGPR hop in the pivot chain.
-      //
-      // 2x2 block pivots: A = L D L^T with L unit lower and D = diag of 2x2
-      // blocks [a b; b c], eliminated a pair of columns per step.  The chain of a
-      // step is the pair's broadcast, det = ac - b^2, one reciprocal and the
-      // update of the next pair's rows -- half the steps of the scalar Cholesky,
-      // and no square root on it: the update operands (lane m's unscaled column
-      // values) are known before the reciprocal.  The Cholesky factor is L C
-      // with D's block = C C^T (C00 = sqrt(a), C10 = b / C00, C11 = sqrt(c -
-      // C10^2)), formed off the chain; so L_pp is the same lower-triangular
-      // factor as before up to rounding.
+      // DPP row (lower part read; the four rows of the wave hold copies).  L(m, j)
+      // (= lane m's l_ij) reaches the other lanes of the row as a DPP
+      // row_newbcast operand: no LDS round trip and no SGPR hop in the pivot chain.
       const int i = l & 15;
       double v[16], rj[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
-      static_for<0, 8>([&](auto Q) {
-        constexpr int j = 2 * decltype(Q)::value;
-        const double a = bcast16<j>(v[j]);
-        const double b = bcast16<j + 1>(v[j]);
-        const double c = bcast16<j + 1>(v[j + 1]);
-        const double det = __builtin_fma(a, c, -(b * b));
-        ok = ok && a > 0.0 && a < INFINITY && det > 0.0 && det < INFINITY;
-        const double rd = rcp_f64(det);
-        const double p0 = v[j], p1 = v[j + 1];
-        const double l0 = __builtin_fma(p0, c, -(p1 * b)) * rd;  // (p0, p1) D^-1
-        const double l1 = __builtin_fma(p1, a, -(p0 * b)) * rd;
-        static_for<j + 2, 16>([&](auto Mi) {
+      static_for<0, 16>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const double djj = bcast16<j>(v[j]);
+        ok = ok && djj > 0.0 && djj < INFINITY;
+        double r = __builtin_amdgcn_rsq(djj);
+        const double h = 0.5 * djj;
+        r = r * __builtin_fma(-h * r, r, 1.5);
+        r = r * __builtin_fma(-h * r, r, 1.5);
+        rj[j] = r;
+        const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
+        v[j] = lij;
+        static_for<j + 1, 16>([&](auto Mi) {
           constexpr int m = decltype(Mi)::value;
-          v[m] = __builtin_fma(-l0, bcast16<m>(p0), __builtin_fma(-l1, bcast16<m>(p1), v[m]));
+          v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
         });
-        // off the chain: D's block = C C^T, rows of the factor L C
-        double r0 = __builtin_amdgcn_rsq(a);
-        const double h0 = 0.5 * a;
-        r0 = r0 * __builtin_fma(-h0 * r0, r0, 1.5);
-        r0 = r0 * __builtin_fma(-h0 * r0, r0, 1.5);
-        const double c00 = a * r0, c10 = b * r0;
-        const double s1 = __builtin_fma(-c10, c10, c);
-        double r1 = __builtin_amdgcn_rsq(s1);
-        const double h1 = 0.5 * s1;
-        r1 = r1 * __builtin_fma(-h1 * r1, r1, 1.5);
-        r1 = r1 * __builtin_fma(-h1 * r1, r1, 1.5);
-        const double c11 = s1 * r1;
-        rj[j] = r0;      // 1 / l_jj
-        rj[j + 1] = r1;  // 1 / l_j+1,j+1
-        v[j] = i > j + 1 ? __builtin_fma(l0, c00, l1 * c10) : (i == j ? c00 : (i == j + 1 ? c10 : 0.0));
-        v[j + 1] = i > j + 1 ? l1 * c11 : (i == j + 1 ? c11 : 0.0);
       });
       // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
       // (column-oriented: once x_k is known, every later row's sum takes its
@@ -2237,7 +2214,7 @@ void k_tl2_panel(slam_ba_problem p, int eoff) {
   if (I == k || !ok) return;
   __syncthreads();
   d4 acc[4];
-  gemm_xyT(Xf, Vf, acc);  // L_Ik = A_Ik (L_kk^-1)^T
+  gemm_xyT_lowY(Xf, Vf, acc);  // L_Ik = A_Ik (L_kk^-1)^T
 #pragma unroll
   for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
@@ -2703,7 +2680,7 @@ void k_tl3_flow(slam_ba_problem p) {
       }
     __syncthreads();
     d4 lacc[4];
-    gemm_xyT(Xf, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+    gemm_xyT_lowY(Xf, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll

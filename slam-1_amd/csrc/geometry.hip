@@ -388,6 +388,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp(const double* __restrict__ Qall,
                                                 const int32_t* __restrict__ count, int cap,
                                                 const double* __restrict__ Kp, uint64_t seed,
                                                 int item0, int n_hyp, double* __restrict__ ws) {
+#ifdef SLAM_PNP_PRIO
+  __builtin_amdgcn_s_setprio(SLAM_PNP_PRIO);
+#endif
   __shared__ slam_epnp::EpGroup grp[kHypGroups];
   __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
   __shared__ int sidx[kHypGroups][kMinSample];
@@ -444,6 +447,9 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_lm(const double* __restrict__ Qa
                                                    const double* __restrict__ Kp, uint64_t seed,
                                                    int item0, int n_hyp, int hyp_iters,
                                                    double* __restrict__ ws) {
+#ifdef SLAM_PNP_PRIO
+  __builtin_amdgcn_s_setprio(SLAM_PNP_PRIO);
+#endif
   __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
   __shared__ int sidx[kHypGroups][kMinSample];
   __shared__ double lmt[kHypGroups][2 * kMinSample][28], lms[kHypGroups][28 + kMinSample];
@@ -492,6 +498,9 @@ __global__ __launch_bounds__(kPnPWG) void k_pnp(const double* __restrict__ Qall,
                                                 int32_t* __restrict__ ninl,
                                                 uint8_t* __restrict__ mask,
                                                 const double* __restrict__ hws) {
+#ifdef SLAM_PNP_PRIO
+  __builtin_amdgcn_s_setprio(SLAM_PNP_PRIO);
+#endif
   __shared__ double hp[kMaxHyp][6];
   __shared__ double hR[kMaxHyp][9];
   __shared__ int hcnt[kMaxHyp];

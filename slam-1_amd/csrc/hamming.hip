@@ -214,6 +214,9 @@ constexpr int kMxQWG = 16 * kMxQB;         // queries per workgroup
 // every query of the workgroup within it
 static_assert(kMxWG >= kMxQWG && kMxWG % 64 == 0,
               "knn2_mx_kernel: SLAM_MX_WG must cover 16 * SLAM_MX_QB queries");
+#ifndef SLAM_MX_XCD
+#define SLAM_MX_XCD 1  // XCD-aware block order (0: blocks in launch order, for A/B)
+#endif
 constexpr int kMxAhead = 2;                // train steps loaded ahead
 constexpr float kMxNone = 16777215.0f;     // > every valid key (< 2^23 + 2^14)
 typedef int mx_v8i __attribute__((ext_vector_type(8)));
@@ -244,7 +247,11 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
     int tiles_per_item, int2* __restrict__ idx2, int2* __restrict__ dist2,
     uint8_t* __restrict__ good) {
   __shared__ uint32_t part[kMxWaves][kMxQWG][2];
+#if SLAM_MX_XCD
   const int vb = xcd_block((int)blockIdx.x, (int)gridDim.x);
+#else
+  const int vb = (int)blockIdx.x;
+#endif
   const int item = vb / tiles_per_item;
   const int tile = vb - item * tiles_per_item;
   const int nq = min(max(nq_arr[item], 0), q_cap);
