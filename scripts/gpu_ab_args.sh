@@ -1,6 +1,6 @@
 #!/bin/bash
 # Alternating A/B of the default tracking bench (the driver's step counts):
-#   scripts/gpu_r4_ab.sh TAG N "A-args" "B-args"   (A/B args appended to bench.py)
+#   scripts/gpu_ab_args.sh TAG N "A-args" "B-args"   (A/B args appended to bench.py)
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

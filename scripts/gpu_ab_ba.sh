@@ -2,7 +2,7 @@
 # Round-4 session-2 second pass: BA tiled-solve tests at the current library,
 # C4 and C5 A/B against a variant (default: the 2x2-pivot factor alone), and
 # the per-column flow-solve timeline (profiling build of the current ba.hip).
-#   scripts/gpu_r4_s2b.sh TAG VARIANT_SO
+#   scripts/gpu_ab_ba.sh TAG VARIANT_SO
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the C4 LM iteration: the default library vs a variant (SLAM355_LIB),
 # alternating runs, then rocprof kernel stats of each.
-#   scripts/gpu_r4_ab_c4.sh TAG VARIANT_SO [bench args]
+#   scripts/gpu_ab_c4.sh TAG VARIANT_SO [bench args]
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

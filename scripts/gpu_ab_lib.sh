@@ -1,7 +1,7 @@
 #!/bin/bash
 # Alternating A/B of the default tracking bench (the driver's step counts)
 # between the default library (A) and a variant library (B, SLAM355_LIB), plus
-# the 16-window batched BA line of each.  scripts/gpu_r4_ab_lib.sh TAG N VARIANT_SO
+# the 16-window batched BA line of each.  scripts/gpu_ab_lib.sh TAG N VARIANT_SO
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

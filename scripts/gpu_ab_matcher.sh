@@ -3,7 +3,7 @@
 # matcher GPU tests on A, the C2 micro-bench and the tracking bench alternating,
 # then per library one kernel-trace stats pass and one FETCH_SIZE pass of the
 # tracking bench (knn2_mx_kernel's in-pipeline duration and HBM bytes).
-#   scripts/gpu_r4_mx.sh TAG N VARIANT_SO ['pytest -k expr']
+#   scripts/gpu_ab_matcher.sh TAG N VARIANT_SO ['pytest -k expr']
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

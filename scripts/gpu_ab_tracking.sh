@@ -1,7 +1,7 @@
 #!/bin/bash
 # Alternating N-way A/B of the tracking bench (the driver's step counts):
 # "def" = the default library, every other name = slam-1_amd/prof/libslam355_NAME.so.
-#   scripts/gpu_r4_abn.sh TAG ROUNDS def NAME1 NAME2 ...
+#   scripts/gpu_ab_tracking.sh TAG ROUNDS def NAME1 NAME2 ...
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"

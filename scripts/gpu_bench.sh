@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 bench pass: the driver's exact command (--steps 20 --warmup 5) N times,
 # plus optional extra argument sets, each under its own time limit, chained with &&.
-#   scripts/gpu_r4_bench.sh TAG N [extra bench args...]
+#   scripts/gpu_bench.sh TAG N [extra bench args...]
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$ROOT/gpurun_out/$1"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 quick pass: selected GPU tests (pytest -k EXPR), then the driver's bench
-# command, then optional extra bench workloads.  scripts/gpu_r4_quick.sh TAG 'k-expr' [bench args]
+# command, then optional extra bench workloads.  scripts/gpu_quick.sh TAG 'k-expr' [bench args]
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG="$1"; K="$2"; shift 2

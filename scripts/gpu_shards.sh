@@ -1,4 +1,5 @@
 set -o pipefail
+# tracking shards of one sequence: GPU tests + the 1-rank and 2-rank (gloo, one GPU) rehearsals
 mkdir -p gpurun_out/r4_q3
 timeout -k 10 400 python -u -m pytest tests/test_dist.py -x -v -m gpu -k "shards_gather or gather_pose or capi_comm" --timeout 300 --timeout-method thread > gpurun_out/r4_q3/pytest.log 2>&1 || { tail -30 gpurun_out/r4_q3/pytest.log; exit 1; }
 tail -2 gpurun_out/r4_q3/pytest.log

@@ -213,7 +213,7 @@ __device__ unsigned long long g_orb_prof[96];
 #define ORB_T0() (void)0
 #define ORB_T(ph) (void)0
 #endif
-// -DSLAM_ORB_CUT=k (profiling builds only, scripts/gpu_r3_orbcut.sh): every
+// -DSLAM_ORB_CUT=k (profiling builds only, scripts/build_variant.sh + scripts/gpu_profile.sh): every
 // level stops after phase k (1 resize, 2 FAST, 3 NMS, 6 rank, 7 IC angle,
 // 8 blur), so the SQ counters of successive cuts split the LDS instructions /
 // bank conflicts by phase (profiles/r3_orb_lds_phases_v1.json).
