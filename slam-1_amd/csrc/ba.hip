@@ -1209,7 +1209,11 @@ __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
 // workgroup's lanes are (part k, column e) pairs; part k takes rows rb + k,
 // rb + k + nparts, ... with 8 loads in flight, then the parts are added in
 // order k = 0, 1, ... (deterministic).  Result in out[0..n).
-constexpr int kAsmWG = 1024;
+#ifndef SLAM_ASM_WG
+#define SLAM_ASM_WG 1024  // k_assemble workgroup (>= 128: one lane per element of a 109-double row)
+#endif
+constexpr int kAsmWG = SLAM_ASM_WG;
+static_assert(kAsmWG >= 128 && kAsmWG % 64 == 0, "SLAM_ASM_WG");
 __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, int re, int n,
                          double (*red)[kCPart], double* out) {
   const int t = threadIdx.x;

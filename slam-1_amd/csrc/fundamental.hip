@@ -543,7 +543,10 @@ __global__ __launch_bounds__(kFWG) void k_fm_finish(const double* __restrict__ m
 }
 
 // Order-preserving compaction of pairs[b][k] (k < count[b]) by mask[b][k].
-constexpr int kCWG = 1024;
+#ifndef SLAM_CWG
+#define SLAM_CWG 1024
+#endif
+constexpr int kCWG = SLAM_CWG;
 __global__ __launch_bounds__(kCWG) void k_filter_pairs(const int2* __restrict__ pairs,
                                                        const int32_t* __restrict__ count,
                                                        const uint8_t* __restrict__ mask, int cap,

@@ -419,7 +419,10 @@ __global__ __launch_bounds__(kMxWG) void knn2_mx_kernel(
 }
 
 // One workgroup per batch item: order-preserving compaction of good rows.
-constexpr int kCWG = 1024;
+#ifndef SLAM_CWG
+#define SLAM_CWG 1024
+#endif
+constexpr int kCWG = SLAM_CWG;
 
 __global__ __launch_bounds__(kCWG) void compact_kernel(
     const int2* __restrict__ idx2, const uint8_t* __restrict__ good,
