@@ -1882,7 +1882,10 @@ __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayo
 // the trailing update A_ij -= L_ip L_jp^T run on the f64 matrix cores
 // (16x16x4), one block per wave.  L^-1 is then assembled by block levels:
 // X_ip = -X_ii sum_{k=p}^{i-1} L_ik X_kp.  The serial chain is 4 x 16 pivots
-// (was 64 pivots with a workgroup barrier each).  M: LDS [64][65] (A, then L's
+// (was 64 pivots with a workgroup barrier each); workgroup barriers only where
+// another wave's blocks are read: after blocks 0 and 1's factor, panel and
+// trailing steps, and once before the inverse assembly (block 2's panel and
+// trailing step are wave 0's alone; each wave assembles its own column block).  M: LDS [64][65] (A, then L's
 // off-diagonal blocks), Xb: LDS [10][16][17] (lower blocks of L^-1), Tb:
 // LDS [3][16][17] scratch.  Every wave must call it; returns false (uniform)
 // on a non-positive or non-finite pivot.
@@ -1946,6 +1949,13 @@ __device__ unsigned long long g_flow_fac[16];
 #else
 #define FAC_T(i) (void)0
 #endif
+// LDS written by this wave visible to its own later reads (no other wave involved)
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk, int ld,
                                                   double* M, double* Xb, double* Tb, int* okp,
                                                   bool tl_prof_on = false) {
@@ -2017,7 +2027,28 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
 #pragma unroll
         for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = x[ii];
       }
+      if (p == 2) {
+        // the last panel block L_32 and trailing block A_33 are wave 0's alone:
+        // it runs them itself, in order, and goes on to block 3 with no
+        // workgroup barrier (the other waves wait at the one after the loop)
+        wave_lds_fence();
+        FAC_T(7);
+        double* A32 = M + 48 * kMS + 32;
+        const d4 z = d4{0.0, 0.0, 0.0, 0.0};
+        st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
+        wave_lds_fence();
+        FAC_T(8);
+        double* A33 = M + 48 * kMS + 48;
+        st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
+        wave_lds_fence();
+        FAC_T(9);
+      } else if (p == 3) {
+        FAC_T(10);
+        FAC_T(11);
+        FAC_T(12);
+      }
     }
+    if (p >= 2) continue;  // (uniform: blocks 2 and 3 need no workgroup barriers)
     __syncthreads();
     FAC_T(1 + 3 * p);
     // panel: L_ip = A_ip X_pp^T (one block per wave)
@@ -2048,7 +2079,10 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     FAC_T(3 + 3 * p);
   }
   TL_STAMP(2);
-  // L^-1 by levels d = i - p: T = sum_k L_ik X_kp, then X_ip = -X_ii T
+  __syncthreads();  // X_ii and L final
+  // L^-1 by levels d = i - p: T = sum_k L_ik X_kp, then X_ip = -X_ii T.  Column
+  // block pp is wave pp's from level to level (it reads only its own X_kp, the
+  // diagonal inverses and L), so the levels need no workgroup barriers.
 #pragma unroll 1
   for (int d = 1; d < 4; ++d) {
     const int pp = w, i = pp + d;
@@ -2065,8 +2099,8 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
       const d4 z = d4{0.0, 0.0, 0.0, 0.0};
       const d4 xi = mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, T, kBS17, z, true);
       st16(Xb + blk_id(i, pp) * 16 * kBS17, kBS17, xi);
+      wave_lds_fence();  // X_ip and T are this wave's own from level to level
     }
-    __syncthreads();
   }
   if (w == 0 && l == 0) *okp = ok ? 1 : 0;
   __syncthreads();
