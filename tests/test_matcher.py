@@ -112,6 +112,36 @@ def test_gpu_knn2_ragged_batch_bit_exact():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("B", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_gpu_knn2_xcd_block_order_every_grid_remainder(B):
+    """knn2_mx_kernel deals a frame pair's workgroups to one XCD by a bijection
+    of the block index that depends on the grid size mod 8: batches whose
+    grids leave every remainder still match the oracle bit for bit (3
+    workgroups of 96 queries per item: grids 3B cover every residue mod 8;
+    ragged query / train counts, so some workgroups exit early)."""
+    import torch
+    from slam355 import matcher
+
+    rng = np.random.default_rng(100 + B)
+    qc, tc = 200, 260
+    q = np.zeros((B, qc, 32), np.uint8)
+    t = np.zeros((B, tc, 32), np.uint8)
+    nq = rng.integers(0, qc + 1, B).astype(np.int32)
+    nt = rng.integers(0, tc + 1, B).astype(np.int32)
+    for b in range(B):
+        qq, tt = _sets(rng, int(nq[b]), int(nt[b]), dup=10)
+        q[b, :nq[b]], t[b, :nt[b]] = qq, tt
+    dev = torch.device("cuda")
+    i2, d2, g = matcher.knn2_batch(torch.from_numpy(q).to(dev), torch.from_numpy(nq).to(dev),
+                                   torch.from_numpy(t).to(dev), torch.from_numpy(nt).to(dev))
+    torch.cuda.synchronize()
+    ei2, ed2, eg = oracle.hamming_knn2_batch(q, nq, t, nt)
+    assert np.array_equal(i2.cpu().numpy(), ei2)
+    assert np.array_equal(d2.cpu().numpy(), ed2)
+    assert np.array_equal(g.cpu().numpy(), eg)
+
+
+@pytest.mark.gpu
 def test_gpu_knn2_max_train_and_chunk_boundaries():
     import torch
     from slam355 import matcher
