@@ -2400,6 +2400,9 @@ __global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
 // solve failed: SOLVE_FAULT), and every column is retired exactly once, so the
 // retire ticket always reaches T and its last adder runs the epilogue.
 constexpr int kFlowSpinMax = 1 << 22;  // ~0.2 s of 128-cycle polls
+#ifndef SLAM_FLOW_SLEEP
+#define SLAM_FLOW_SLEEP 2  // s_sleep between flag polls (units of 64 clocks)
+#endif
 
 #ifdef SLAM_FLOW_PROFILE
 // per column: wall clock (100 MHz) at start, diagonal updates done, factor done,
@@ -2453,7 +2456,7 @@ __device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh) {
         ok = 0;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(SLAM_FLOW_SLEEP);
     }
     *sh = ok;
   }
@@ -2484,7 +2487,7 @@ __device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int
           ok = 0;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(SLAM_FLOW_SLEEP);
       }
     }
     if (lane == 0) *sh = ok;
@@ -2512,7 +2515,7 @@ __device__ bool flow_wait_count(const int* cnt, int rc, int* fail, int* sh) {
         ok = 0;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(SLAM_FLOW_SLEEP);
     }
     *sh = ok;
   }
