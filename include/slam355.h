@@ -292,9 +292,10 @@ int slam_ba_jacobian(const double* d_cams, const double* d_pts, const int32_t* d
 /* slots 12..15: phase timers of the profiling builds (SLAM_LIN_PROFILE,
  * SLAM_SOLVE_PROFILE; scripts/ba_solve_prof.py reads state[12:16]); slots 18, 19:
  * the per-panel timers of SLAM_SOLVE_PROFILE_PANEL (scripts/solve_trace.py) */
-#define SLAM_BA_ST_SOLVE_FAULT 16 /* sticky: camera solves that timed out waiting for a
-                                     * co-resident workgroup (never set by a correct launch;
-                                     * the Python layer raises when it is non-zero) */
+#define SLAM_BA_ST_SOLVE_FAULT 16 /* sticky: camera solves whose dataflow wait timed out
+                                     * (fail code 2: a hang or a hand-off ordering bug --
+                                     * the solve needs no co-residency, so a correct build
+                                     * never sets it; the Python layer raises when non-zero) */
 #define SLAM_BA_ST_SLOTS 20
 
 /* Everything the LM iteration touches; all pointers are device pointers.
@@ -402,7 +403,9 @@ typedef struct slam_ba_problem {
  * (and SLAM_OK) when a point has > 120 observations or > 7 cameras: the slot
  * linearisation (lin_mode 0) applies.  chunks_per_wg <= 0: the default rule
  * of plan_mfma.  block_list (packed layout, 9C > 120; may be null): the
- * upper blocks to list, as BAProblem's block_list. */
+ * upper blocks to list, as BAProblem's block_list.  Null means "the problem's
+ * own blocks"; a non-null pointer with n_block_list == 0 is an explicitly empty
+ * list and fails like any list that misses a block (plan_mfma raises alike). */
 enum {
   SLAM_PLAN_PERM = 0,      /* [P] device point k = caller's point perm[k]      */
   SLAM_PLAN_ORDER,         /* [O] observation order (qs[order] -> obs_q)       */

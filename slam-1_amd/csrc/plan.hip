@@ -252,7 +252,7 @@ extern "C" int slam_ba_plan_mfma(int n_cams, int n_pts, int n_obs, const int32_t
     for (int c = 0; c < C; ++c) own.push_back(block_index(c, c, C));
     std::sort(own.begin(), own.end());
     own.erase(std::unique(own.begin(), own.end()), own.end());
-    if (block_list && n_block_list > 0) {
+    if (block_list) {  // given (an empty list too: it misses every diagonal block)
       blist.assign(block_list, block_list + n_block_list);
       std::sort(blist.begin(), blist.end());
       blist.erase(std::unique(blist.begin(), blist.end()), blist.end());

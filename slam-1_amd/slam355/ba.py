@@ -618,6 +618,8 @@ def plan_mfma_native(n_cams, n_pts, cam_idx, pt_idx, block_list=None, chunks_per
     O = len(cam_idx)
     bl = None if block_list is None else np.ascontiguousarray(np.unique(block_list), np.int32)
     nbl = 0 if bl is None else len(bl)
+    if bl is not None and nbl == 0:
+        bl = np.zeros(1, np.int32)  # a non-null pointer: "given, and empty" (not "absent")
     cap = int(_lib.lib.slam_ba_plan_bound(n_cams, n_pts, O, nbl))
     if cap <= 0:
         raise ValueError("plan_mfma_native: bad sizes")
@@ -915,14 +917,17 @@ class BAProblem:
 
     # -- host views ---------------------------------------------------------------
     def state(self) -> dict:
-        """The LM state; raises SlamError when a camera solve ever timed out
-        waiting for a co-resident workgroup (SOLVE_FAULT: the dataflow solve was
-        launched where its columns could not all be resident)."""
+        """The LM state; raises SlamError when a dataflow camera solve ever
+        timed out in one of its flag waits (SOLVE_FAULT, fail code 2).  The
+        solve makes no residency assumption (a start ticket hands out columns,
+        the last retirer forms x), so a timeout means a hang or a hand-off
+        ordering bug in the kernel, not a launch that was not co-resident."""
         s = self.t["state"].cpu().numpy()
         st = {k: float(s[v]) for k, v in ST.items()}
         if st["SOLVE_FAULT"] != 0.0:
-            raise _lib.SlamError(f"BA camera solve timed out {int(st['SOLVE_FAULT'])} time(s): its "
-                                 "workgroups were not co-resident (the LM steps were rejected)")
+            raise _lib.SlamError(f"BA camera solve: a dataflow wait timed out (fail code 2) "
+                                 f"{int(st['SOLVE_FAULT'])} time(s) -- a hang or hand-off ordering "
+                                 "bug in k_tl3_flow; the affected LM steps were rejected")
         return st
 
     def params(self):

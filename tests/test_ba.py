@@ -861,6 +861,50 @@ def test_gpu_folded_assembly_equals_k_assemble(C, P, k):
     assert abs(sta["COST"] - stb["COST"]) <= 1e-10 * stb["COST"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("folds", [(True, True, True), (True, False, True)])
+def test_gpu_batch_folded_assembly_equals_k_assemble(folds):
+    """the folded assembly through BABatch (bench --fold): one
+    multi-problem k_lin_mfma launch (blockIdx.y = problem), per-problem asm_tab
+    counters re-armed across graph replays, k_assemble skipped only when every
+    problem folds (all folded) or run for the unfolded ones (mixed).  Each
+    window's iterates over repeated iterate_graphed replays equal the same
+    windows batched with k_assemble (to rounding: the sums run in another
+    fixed order), and a second replay set from the restored start repeats the
+    first bit for bit (the counters were re-armed)."""
+    import torch
+    from slam355 import ba
+    from slam355.synthetic import ba_problem, perturb
+
+    def windows(fold):
+        out = []
+        for w, f in enumerate(fold):
+            rng = np.random.default_rng(40 + w)
+            cams, pts, ci, pi, qs = ba_problem(rng, 10, 1500 + 250 * w, 6)
+            c0, p0 = perturb(rng, cams, pts)
+            out.append(ba.BAProblem(c0, p0, ci, pi, qs, fold_assembly=f))
+        return out
+
+    a, b = windows(folds), windows((False,) * len(folds))
+    assert all(("asm_tab" in p.t) == f for p, f in zip(a, folds))
+    A, B = ba.BABatch(a), ba.BABatch(b)
+    runs = []
+    for _ in range(2):
+        A.iterate_graphed(4, with_restore=True)
+        B.iterate_graphed(4, with_restore=True)
+        torch.cuda.synchronize()
+        sa, sb = A.states(), B.states()
+        for x, y in zip(sa, sb):
+            assert bool(x["ACCEPTED"]) == bool(y["ACCEPTED"]) and x["NACCEPT"] == y["NACCEPT"]
+            assert abs(x["COST"] - y["COST"]) <= 1e-10 * y["COST"]
+        for pa, pb in zip(a, b):
+            ca, cb = pa.params()[0], pb.params()[0]
+            assert np.allclose(ca, cb, rtol=1e-9, atol=1e-12)
+        runs.append([p.params()[0] for p in a])
+    for x, y in zip(*runs):
+        assert np.array_equal(x, y)
+
+
 def test_assembly_table_counts_every_partial_row():
     """The folded assembly's table (slam355.ba.assembly_table): every cpart row
     is counted once at its camera's diagonal block, every bpart row once at its
@@ -944,6 +988,12 @@ def test_native_planner_block_list_and_edges():
     _same_plan(C, 2000, ci, pi, bl)
     with pytest.raises(_lib.SlamError, match="block_list misses"):
         ba.plan_mfma_native(C, 2000, ci, pi, ba.upper_blocks(C, ci, pi)[:C])
+    # an explicitly empty block_list is "given" (ADVICE r4): both planners refuse it
+    with pytest.raises(ValueError, match="block_list misses"):
+        ba.plan_mfma(C, 2000, ci, pi, [])
+    with pytest.raises(_lib.SlamError, match="block_list misses"):
+        ba.plan_mfma_native(C, 2000, ci, pi, [])
+    _same_plan(8, 300, *_rand_structure(rng, 8, 300, 3), block_list=[])  # dense: list unused
     _same_plan(10, 1, np.arange(8), np.zeros(8, np.int64))  # 8 cameras on a point: slot mode
     assert ba.plan_mfma_native(10, 1, np.arange(8), np.zeros(8, np.int64)) is None
     _same_plan(5, 0, np.zeros(0, np.int64), np.zeros(0, np.int64))

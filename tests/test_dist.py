@@ -297,12 +297,34 @@ def test_gpu_tracking_shards_gather_one_trajectory(tmp_path):
 
 
 # ---------------------------------------------------------------- C-ABI communicator (RCCL)
+def _rccl_loadable() -> bool:
+    """A library slam_comm_* would dlopen (comm.hip: SLAM_RCCL_LIB, then
+    librccl.so.1, then librccl.so)."""
+    import ctypes
+
+    for name in (os.environ.get("SLAM_RCCL_LIB"), "librccl.so.1", "librccl.so"):
+        if not name:
+            continue
+        try:
+            ctypes.CDLL(name)
+            return True
+        except OSError:
+            pass
+    return False
+
+
 def test_comm_unique_id_loads_rccl_lazily():
     """slam_comm_unique_id resolves RCCL at run time (dlopen; no GPU needed for
-    the id) and fills SLAM_COMM_ID_BYTES bytes."""
+    the id) and fills SLAM_COMM_ID_BYTES bytes.  Skipped where RCCL itself
+    cannot be loaded (a CPU-only host without ROCm's RCCL).  Multi-rank parity
+    of the C-ABI path (slam_ba_step_distributed on > 1 rank) stays unverified
+    until a multi-GPU node runs it: RCCL refuses two ranks per device."""
     import ctypes
 
     from slam355 import _lib
+
+    if not _rccl_loadable():
+        pytest.skip("RCCL (librccl.so.1 / SLAM_RCCL_LIB) cannot be loaded here")
 
     b = (ctypes.c_uint8 * 128)()
     _lib.call("slam_comm_unique_id", ctypes.cast(b, ctypes.c_void_p))

@@ -330,7 +330,9 @@ def c1_seq():
 
 
 def test_oracle_c1_chain_is_c1_shaped(c1_seq):
-    """The C1 sequence gives ~500 kp per frame at cap 14 and a tracked pose."""
+    """The C1 sequence gives ~500 kp per frame at C1_CAP (25 per tile: at
+    640x480 only pyramid levels 0-2 of a patch hold keypoints, so cap 14 would
+    give 288) and a tracked pose."""
     import oracle
 
     L, R, poses, rig = c1_seq
@@ -345,8 +347,9 @@ def test_oracle_c1_chain_is_c1_shaped(c1_seq):
 
 @pytest.mark.gpu
 def test_gpu_tracker_c1_640x480_matches_oracle_chain(c1_seq):
-    """VERDICT r3 #1 (C1 = main.py:76-132 at 640x480, cap 14, a 2-keyframe
-    window; cap 25 per tile = 500 kp/frame): the batched Tracker against oracle.pipeline.track_pair per pair --
+    """VERDICT r3 #1 (C1 = main.py:76-132 at 640x480, 500 kp/frame, a
+    2-keyframe window; C1_CAP = 25 per tile gives the 500 kp/frame, DESIGN.md
+    §2): the batched Tracker against oracle.pipeline.track_pair per pair --
     ORB counts, stereo / F-LMedS counts and mask, X at 1e-9, temporal count,
     PnP inliers and pose at 1e-8, and the device-chained poses against the host
     chain of the oracle's PnP results (the stale-T rule included)."""
