@@ -526,7 +526,9 @@ long long slam_pose_chain_workspace_len(int n_frames);
  * subproblem) on ws[0 .. 6m) in place, one workgroup, at most max_iter outer
  * iterations per call (first != 0 starts the run: scale, Delta; else it
  * resumes from state).  Analytic Jacobian; the subproblem's SVD solves are
- * replaced by the O(m) arrow-structured dual system.  state[16]: cost0, cost,
+ * replaced by the O(m) arrow-structured dual system.  m <= 512: every frame's
+ * state in the registers of one thread (k_chain_trf_r); larger m: the LDS /
+ * workspace form (environment SLAM_CHAIN_TRF=lds selects it for any m).  state[16]: cost0, cost,
  * nfev, njev, status (0 running, 1 gtol, 2 ftol, 3 xtol, 4 ftol+xtol), Delta,
  * alpha, iterations.  Replaces least_squares(objective, ..., method='trf') of
  * bundle_adjustment_with_sparsity, BundleAdjustment.py:179-183. */

@@ -1877,18 +1877,20 @@ __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayo
 
 // Blocked factor + inverse of the 64x64 diagonal tile (4 x 4 blocks of 16):
 // per block column p, wave 0 factors the 16x16 diagonal block in registers
-// (lane i = row i, pivots and column entries broadcast by v_readlane) and
-// inverts it (lane c = column c of L_pp^-1); the panel L_ip = A_ip L_pp^-T and
-// the trailing update A_ij -= L_ip L_jp^T run on the f64 matrix cores
-// (16x16x4), one block per wave.  L^-1 is then assembled by block levels:
-// X_ip = -X_ii sum_{k=p}^{i-1} L_ik X_kp.  The serial chain is 4 x 16 pivots
-// (was 64 pivots with a workgroup barrier each); workgroup barriers only where
-// another wave's blocks are read: after blocks 0 and 1's factor, panel and
-// trailing steps, and once before the inverse assembly (block 2's panel and
-// trailing step are wave 0's alone; each wave assembles its own column block).  M: LDS [64][65] (A, then L's
-// off-diagonal blocks), Xb: LDS [10][16][17] (lower blocks of L^-1), Tb:
-// LDS [3][16][17] scratch.  Every wave must call it; returns false (uniform)
-// on a non-positive or non-finite pivot.
+// (lane i = row i, pivots and column entries broadcast by DPP row_newbcast)
+// and inverts it (lane c = column c of L_pp^-1); the panel L_ip = A_ip L_pp^-T
+// and the trailing update A_ij -= L_ip L_jp^T run on the f64 matrix cores
+// (16x16x4), one block per wave, for p = 0, 1 (workgroup barriers between);
+// block columns 2 and 3 (L_32, A_33 and both factors) are wave 0's chain
+// alone.  L^-1's off-diagonal blocks X_ip = -X_ii sum_{k=p}^{i-1} L_ik X_kp
+// are formed by waves 1-3 beside that chain as their inputs appear (round 5:
+// X_10 during block 2's factor, X_21 / X_20 and the sums T_3p during block
+// 3's, the last three products X_3p = -X_33 T_3p once X_33 is out), so after
+// the last pivot only one 16x16 product per wave is left (the assembly after
+// the factor was 2.2 us of 13.0 per tile; 0.44 now).  M: LDS [64][65] (A, then
+// L's off-diagonal blocks), Xb: LDS [10][16][17] (lower blocks of L^-1), Tb:
+// LDS [3][16][17] scratch + one int (L_32 published).  Every wave must call
+// it; returns false (uniform) on a non-positive or non-finite pivot.
 constexpr int kMS = 65;   // row stride of M (odd: MFMA operand reads spread over banks)
 constexpr int kVR = 65;   // row stride of k_tl3_flow's row-major L_JJ^-1
 constexpr int kBS17 = 17; // row stride of a 16x16 block
@@ -1956,6 +1958,54 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wave 0's part of block column p: the 16x16 diagonal block of M factored in
+// registers and inverted (X_pp = L_pp^-1 into Xb); `ok` cleared on a
+// non-positive or non-finite pivot.
+__device__ __forceinline__ void blk_factor_w0(double* M, double* Xb, int p, bool& ok) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15;
+  double v[16], rj[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
+  static_for<0, 16>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const double djj = bcast16<j>(v[j]);
+    ok = ok && djj > 0.0 && djj < INFINITY;
+    double r = __builtin_amdgcn_rsq(djj);
+    const double h = 0.5 * djj;
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    r = r * __builtin_fma(-h * r, r, 1.5);
+    rj[j] = r;
+    const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
+    v[j] = lij;
+    static_for<j + 1, 16>([&](auto Mi) {
+      constexpr int m = decltype(Mi)::value;
+      v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
+    });
+  });
+  // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
+  // (column-oriented: once x_k is known, every later row's sum takes its
+  // term -- the same k order per sum as the row form, a 16-step chain
+  // instead of 120 dependent FMAs); l_ik = lane ii's v[k], by row_newbcast
+  const int c = l & 15;
+  double x[16], sacc[16];
+#pragma unroll
+  for (int ii = 0; ii < 16; ++ii) sacc[ii] = 0.0;
+  static_for<0, 16>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    x[k] = k < c ? 0.0 : (k == c ? rj[k] : -sacc[k] * rj[k]);
+    static_for<k + 1, 16>([&](auto II) {
+      constexpr int ii = decltype(II)::value;
+      sacc[ii] = __builtin_fma(bcast16<ii>(v[k]), x[k], sacc[ii]);
+    });
+  });
+  if (l < 16) {
+    double* X = Xb + blk_id(p, p) * 16 * kBS17;
+#pragma unroll
+    for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = x[ii];
+  }
+}
+
 __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk, int ld,
                                                   double* M, double* Xb, double* Tb, int* okp,
                                                   bool tl_prof_on = false) {
@@ -1976,79 +2026,16 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     }
   }
   bool ok = true;
+  int* lflag = reinterpret_cast<int*>(Tb + 3 * 16 * kBS17);  // L_32 published (waves 1-3 wait)
+  if (t == 0) *lflag = 0;
   __syncthreads();
   TL_STAMP(1);
   FAC_T(0);
+  // Block columns 0 and 1: wave 0 factors the diagonal block, then every wave
+  // takes a panel block and trailing blocks (workgroup barriers between).
 #pragma unroll 1
-  for (int p = 0; p < 4; ++p) {
-    if (w == 0) {
-      // rows of the 16x16 diagonal block in lanes i = l & 15 of every 16-lane
-      // DPP row (lower part read; the four rows of the wave hold copies).  L(m, j)
-      // (= lane m's l_ij) reaches the other lanes of the row as a DPP
-      // row_newbcast operand: no LDS round trip and no SGPR hop in the pivot chain.
-      const int i = l & 15;
-      double v[16], rj[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
-      static_for<0, 16>([&](auto J) {
-        constexpr int j = decltype(J)::value;
-        const double djj = bcast16<j>(v[j]);
-        ok = ok && djj > 0.0 && djj < INFINITY;
-        double r = __builtin_amdgcn_rsq(djj);
-        const double h = 0.5 * djj;
-        r = r * __builtin_fma(-h * r, r, 1.5);
-        r = r * __builtin_fma(-h * r, r, 1.5);
-        rj[j] = r;
-        const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
-        v[j] = lij;
-        static_for<j + 1, 16>([&](auto Mi) {
-          constexpr int m = decltype(Mi)::value;
-          v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
-        });
-      });
-      // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
-      // (column-oriented: once x_k is known, every later row's sum takes its
-      // term -- the same k order per sum as the row form, a 16-step chain
-      // instead of 120 dependent FMAs); l_ik = lane ii's v[k], by row_newbcast
-      const int c = l & 15;
-      double x[16], sacc[16];
-#pragma unroll
-      for (int ii = 0; ii < 16; ++ii) sacc[ii] = 0.0;
-      static_for<0, 16>([&](auto K) {
-        constexpr int k = decltype(K)::value;
-        x[k] = k < c ? 0.0 : (k == c ? rj[k] : -sacc[k] * rj[k]);
-        static_for<k + 1, 16>([&](auto II) {
-          constexpr int ii = decltype(II)::value;
-          sacc[ii] = __builtin_fma(bcast16<ii>(v[k]), x[k], sacc[ii]);
-        });
-      });
-      if (l < 16) {
-        double* X = Xb + blk_id(p, p) * 16 * kBS17;
-#pragma unroll
-        for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = x[ii];
-      }
-      if (p == 2) {
-        // the last panel block L_32 and trailing block A_33 are wave 0's alone:
-        // it runs them itself, in order, and goes on to block 3 with no
-        // workgroup barrier (the other waves wait at the one after the loop)
-        wave_lds_fence();
-        FAC_T(7);
-        double* A32 = M + 48 * kMS + 32;
-        const d4 z = d4{0.0, 0.0, 0.0, 0.0};
-        st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
-        wave_lds_fence();
-        FAC_T(8);
-        double* A33 = M + 48 * kMS + 48;
-        st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
-        wave_lds_fence();
-        FAC_T(9);
-      } else if (p == 3) {
-        FAC_T(10);
-        FAC_T(11);
-        FAC_T(12);
-      }
-    }
-    if (p >= 2) continue;  // (uniform: blocks 2 and 3 need no workgroup barriers)
+  for (int p = 0; p < 2; ++p) {
+    if (w == 0) blk_factor_w0(M, Xb, p, ok);
     __syncthreads();
     FAC_T(1 + 3 * p);
     // panel: L_ip = A_ip X_pp^T (one block per wave)
@@ -2078,30 +2065,64 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     __syncthreads();
     FAC_T(3 + 3 * p);
   }
-  TL_STAMP(2);
-  __syncthreads();  // X_ii and L final
-  // L^-1 by levels d = i - p: T = sum_k L_ik X_kp, then X_ip = -X_ii T.  Column
-  // block pp is wave pp's from level to level (it reads only its own X_kp, the
-  // diagonal inverses and L), so the levels need no workgroup barriers.
-#pragma unroll 1
-  for (int d = 1; d < 4; ++d) {
-    const int pp = w, i = pp + d;
-    if (i < 4) {
-      d4 acc = d4{0.0, 0.0, 0.0, 0.0};
-      for (int k = pp; k < i; ++k)
-        acc = mm16_xy(M + (16 * i) * kMS + 16 * k, kMS, Xb + blk_id(k, pp) * 16 * kBS17, kBS17,
-                      acc, false);
-      double* T = Tb + w * 16 * kBS17;
-      st16(T, kBS17, acc);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const d4 z = d4{0.0, 0.0, 0.0, 0.0};
-      const d4 xi = mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, T, kBS17, z, true);
-      st16(Xb + blk_id(i, pp) * 16 * kBS17, kBS17, xi);
-      wave_lds_fence();  // X_ip and T are this wave's own from level to level
-    }
+  // Block columns 2 and 3 are wave 0's chain alone (block 2's factor, the last
+  // panel block L_32 and trailing block A_33, block 3's factor: no workgroup
+  // barrier on it).  Waves 1-3 assemble L^-1 beside it, block by block as its
+  // inputs appear, so that after block 3's factor only X_3p = -X_33 T_3p is
+  // left (one 16x16 product per wave):
+  //   X_ip = -X_ii T_ip,  T_ip = sum_{k=p}^{i-1} L_ik X_kp  (k ascending: the
+  //   same sums in the same order as the level-by-level form, bit-identical).
+  const d4 z = d4{0.0, 0.0, 0.0, 0.0};
+  auto T_of = [&](int i, int p, int k_end) {  // sum_{k=p}^{k_end-1} L_ik X_kp
+    d4 acc = z;
+    for (int k = p; k < k_end; ++k)
+      acc = mm16_xy(M + (16 * i) * kMS + 16 * k, kMS, Xb + blk_id(k, p) * 16 * kBS17, kBS17, acc, false);
+    return acc;
+  };
+  auto X_from = [&](int i, int p, d4 T) {  // X_ip = -X_ii T (T through this wave's Tb block)
+    double* Tw = Tb + (w - 1) * 16 * kBS17;
+    st16(Tw, kBS17, T);
+    wave_lds_fence();
+    st16(Xb + blk_id(i, p) * 16 * kBS17, kBS17, mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, Tw, kBS17, z, true));
+    wave_lds_fence();
+  };
+  if (w == 0) {
+    blk_factor_w0(M, Xb, 2, ok);
+  } else if (w == 1) {
+    X_from(1, 0, T_of(1, 0, 1));  // X_10 (X_00, X_11, L_10 final after block column 1)
   }
+  __syncthreads();  // X_22 (and X_10) published
+  FAC_T(7);
+  d4 T3 = z;
+  if (w == 0) {
+    double* A32 = M + 48 * kMS + 32;
+    st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
+    wave_lds_fence();
+    FAC_T(8);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (l == 0) __hip_atomic_store(lflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    double* A33 = M + 48 * kMS + 48;
+    st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
+    wave_lds_fence();
+    FAC_T(9);
+    blk_factor_w0(M, Xb, 3, ok);
+    FAC_T(10);
+    FAC_T(11);
+    FAC_T(12);
+  } else {
+    if (w == 1) X_from(2, 1, T_of(2, 1, 2));  // X_21
+    if (w == 2) X_from(2, 0, T_of(2, 0, 2));  // X_20 (needs X_10: published by the barrier)
+    // T_3p needs L_32 (wave 0's panel block above)
+    while (__hip_atomic_load(lflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // wave 1: T_31, wave 2: T_30, wave 3: T_32 (each wave reads only the X
+    // blocks it formed itself or that the barrier published)
+    T3 = T_of(3, w == 1 ? 1 : (w == 2 ? 0 : 2), 3);
+  }
+  __syncthreads();  // X_33 published
+  if (w > 0) X_from(3, w == 1 ? 1 : (w == 2 ? 0 : 2), T3);
+  TL_STAMP(2);
   if (w == 0 && l == 0) *okp = ok ? 1 : 0;
   __syncthreads();
   TL_STAMP(3);

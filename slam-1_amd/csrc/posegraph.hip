@@ -27,6 +27,11 @@
 //                      (J_h J_h^T + alpha I) y = f, an arrow matrix (frame
 //                      rows couple only through the two loop rows) solved
 //                      through its 2x2 Schur complement in O(m).
+//   k_chain_trf_r      the same algorithm with every per-frame quantity in the
+//                      registers / LDS column of the thread owning the frame
+//                      (m <= 512; round 5: 7.8 -> 2.4 ms per 500-keyframe
+//                      solve); k_chain_trf serves larger chains and the
+//                      SLAM_CHAIN_TRF=lds A/B.
 #include "common.hpp"
 
 #include <cmath>
@@ -176,6 +181,30 @@ __device__ void rodrigues_jac(const double r[3], const double R[9], double* dR) 
       dR[9 * k + 3 + j] = (a2 * R[j] - a0 * R[6 + j]) / th2;
       dR[9 * k + 6 + j] = (-a1 * R[j] + a0 * R[3 + j]) / th2;
     }
+  }
+}
+
+// dR/dr_k alone (rodrigues_jac's k-th 3x3, the same operations)
+__device__ __forceinline__ void rodrigues_jac_k(const double r[3], const double R[9], int k, double* D) {
+  const double th2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+  const double e0 = k == 0 ? 1.0 : 0.0, e1 = k == 1 ? 1.0 : 0.0, e2 = k == 2 ? 1.0 : 0.0;
+  if (th2 < 1e-30) {
+    D[0] = 0.0; D[1] = -e2; D[2] = e1;
+    D[3] = e2;  D[4] = 0.0; D[5] = -e0;
+    D[6] = -e1; D[7] = e0;  D[8] = 0.0;
+    return;
+  }
+  const double rk = k == 0 ? r[0] : (k == 1 ? r[1] : r[2]);
+  const double Rk0 = k == 0 ? R[0] : (k == 1 ? R[1] : R[2]);
+  const double Rk1 = k == 0 ? R[3] : (k == 1 ? R[4] : R[5]);
+  const double Rk2 = k == 0 ? R[6] : (k == 1 ? R[7] : R[8]);
+  const double u0 = e0 - Rk0, u1 = e1 - Rk1, u2 = e2 - Rk2;  // (I - R) e_k
+  const double v0 = r[1] * u2 - r[2] * u1, v1 = r[2] * u0 - r[0] * u2, v2 = r[0] * u1 - r[1] * u0;
+  const double a0 = rk * r[0] + v0, a1 = rk * r[1] + v1, a2 = rk * r[2] + v2;
+  for (int j = 0; j < 3; ++j) {
+    D[j] = (-a2 * R[3 + j] + a1 * R[6 + j]) / th2;
+    D[3 + j] = (a2 * R[j] - a0 * R[6 + j]) / th2;
+    D[6 + j] = (-a1 * R[j] + a0 * R[3 + j]) / th2;
   }
 }
 
@@ -573,6 +602,515 @@ __global__ __launch_bounds__(kLmWG) void k_chain_trf(double* __restrict__ ws, in
   }
 }
 
+// ------------------------------------------------------------------ TRF, register-resident
+// k_chain_trf_r<F>: k_chain_trf's algorithm (the same scipy-TRF steps, tests and
+// trust-radius rules) with every per-frame quantity in the registers of the
+// thread that owns the frame (frames F t .. F t + F - 1 of thread t, kRW
+// threads), so no pass over the frames touches global memory:
+//   * reductions: a wave shuffle tree, one LDS partial per wave, ONE workgroup
+//     barrier (the partial buffers alternate, so the next reduction's stores
+//     cannot overtake this one's loads); every thread sums the 8 partials in
+//     the same order, so every thread holds the same bits;
+//   * chain products: wave shuffle scans of rigid transforms (Hillis-Steele
+//     over the 64 lanes) and the 8 wave totals through LDS -- the prefix
+//     P_i, the suffix S_i and the whole chain T, as k_chain_trf's LDS scans;
+//   * the 'exact' subproblem's alpha iteration in TWO reductions per step:
+//     the first arrow solve y = (K + a)^-1 f as before; the second one's
+//     result z = (K + a)^-1 y enters only through (f - a y).z, which is
+//       sum_i w_i y_i / d_i - zl_0 sum_i w_i b1_i / d_i - zl_1 sum_i w_i b2_i / d_i
+//       + (fl - a yl).zl        (w = f - a y, d_i = d0_i + a)
+//     so z is never formed and its sums ride on the reduction that also
+//     gives f.y and y.y; the final step's c = Delta / |p| enters the step
+//     and the predicted reduction linearly or quadratically, so their sums
+//     are taken before c is known, in the same reduction as |p|'s.
+// The sums run in another order than k_chain_trf's (rounding at 1e-16
+// relative); the iterates still follow scipy's TRF to the tests' 1e-7.
+constexpr int kRW = 512;
+constexpr int kRWv = kRW / 64;
+constexpr int kRMax = 8;
+
+template <int N>
+__device__ __forceinline__ void rsum(double (&v)[N], double* red, int& ph) {
+  static_assert(N <= kRMax, "rsum: too many values");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < N; ++q)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[q] += __shfl_down(v[q], off, 64);
+  double* b = red + ph * (kRMax * kRWv);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) b[q * kRWv + wid] = v[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < N; ++q) {
+    double s = b[q * kRWv];
+#pragma unroll
+    for (int w = 1; w < kRWv; ++w) s += b[q * kRWv + w];
+    v[q] = s;
+  }
+  ph ^= 1;
+}
+
+__device__ __forceinline__ double rmax(double v, double* red, int& ph) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
+  double* b = red + ph * (kRMax * kRWv);
+  if (lane == 0) b[wid] = v;
+  __syncthreads();
+  double s = b[0];
+#pragma unroll
+  for (int w = 1; w < kRWv; ++w) s = fmax(s, b[w]);
+  ph ^= 1;
+  return s;
+}
+
+__device__ __forceinline__ Rt shfl_up_rt(const Rt& a, int d) {
+  Rt o;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) o.R[k] = __shfl_up(a.R[k], d, 64);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o.t[k] = __shfl_up(a.t[k], d, 64);
+  return o;
+}
+__device__ __forceinline__ Rt shfl_down_rt(const Rt& a, int d) {
+  Rt o;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) o.R[k] = __shfl_down(a.R[k], d, 64);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) o.t[k] = __shfl_down(a.t[k], d, 64);
+  return o;
+}
+
+// exclusive prefix product of the threads' chains (thread order) and the whole
+// chain T; wb: 12 kRWv doubles of LDS (one barrier inside)
+__device__ void chain_scan_fwd(const Rt& loc, double* wb, Rt& excl, Rt& tot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  Rt v = loc;
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    const Rt o = shfl_up_rt(v, d);
+    if (lane >= d) v = compose(o, v);
+  }
+  const Rt prev = shfl_up_rt(v, 1);
+  if (lane == 63) st_rt(wb + 12 * wid, v);
+  __syncthreads();
+  Rt Wp = identity_rt();
+  if (wid > 0) {
+    Wp = ld_rt(wb);
+    for (int w = 1; w < wid; ++w) Wp = compose(Wp, ld_rt(wb + 12 * w));
+  }
+  tot = wid > 0 ? Wp : ld_rt(wb);
+  for (int w = wid > 0 ? wid : 1; w < kRWv; ++w) tot = compose(tot, ld_rt(wb + 12 * w));
+  excl = lane > 0 ? (wid > 0 ? compose(Wp, prev) : prev) : Wp;
+}
+
+// exclusive suffix product of the threads' chains (one barrier inside)
+__device__ void chain_scan_bwd(const Rt& loc, double* wb, Rt& excl) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  Rt v = loc;
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    const Rt o = shfl_down_rt(v, d);
+    if (lane + d < 64) v = compose(v, o);
+  }
+  const Rt next = shfl_down_rt(v, 1);
+  if (lane == 0) st_rt(wb + 12 * wid, v);
+  __syncthreads();
+  Rt Ws = identity_rt();
+  if (wid < kRWv - 1) {
+    Ws = ld_rt(wb + 12 * (kRWv - 1));
+    for (int w = kRWv - 2; w > wid; --w) Ws = compose(ld_rt(wb + 12 * w), Ws);
+  }
+  excl = lane < 63 ? (wid < kRWv - 1 ? compose(next, Ws) : next) : Ws;
+}
+
+// per-thread frame state: x, the frame residuals and the scaled-row data in
+// registers; the loop rows h, the scale and the trial x in LDS (this thread's
+// column of hl: no other thread touches it, so no barrier)
+template <int F>
+struct Frames {
+  double x[F][6], r[F], d0[F], b1[F], b2[F], y[F];
+  double* hl;  // [F][24][kRW]: h (12), sinv (6), trial x (6)
+  __device__ __forceinline__ double& h(int f, int k) { return hl[(f * 24 + k) * kRW + threadIdx.x]; }
+  __device__ __forceinline__ double& si(int f, int k) { return hl[(f * 24 + 12 + k) * kRW + threadIdx.x]; }
+  __device__ __forceinline__ double& xt(int f, int k) { return hl[(f * 24 + 18 + k) * kRW + threadIdx.x]; }
+};
+
+// cost 0.5 |f(x)|^2 (every thread) and the loop residuals fl; jac: also the
+// frame residuals r, and the loop rows h (d L_t, d L_R per parameter)
+template <int F, bool JAC>
+__device__ double eval_r(Frames<F>& S, bool trial, int m, int loop, double* red,
+                         int& ph, double* wbf, double* wbb, double fl[2]) {
+  // (JAC evaluates at the live x, never at the trial x)
+  const int t = threadIdx.x;
+  double c2[1] = {0.0};
+  Rt rel[F];
+  Rt loc = identity_rt();
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    if (t * F + f >= m) continue;
+    double xf[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) xf[q] = trial ? S.xt(f, q) : S.x[f][q];
+    const double fc = frame_cost(xf);
+    c2[0] += fc * fc;
+    if (JAC) S.r[f] = fc;
+    if (loop) {
+      if (F == 1) {
+        loc = rel_of(xf);
+      } else {
+        rel[f] = rel_of(xf);
+        loc = f == 0 ? rel[f] : compose(loc, rel[f]);
+      }
+    }
+  }
+  rsum<1>(c2, red, ph);
+  fl[0] = fl[1] = 0.0;
+  if (!loop) return 0.5 * c2[0];
+  Rt ex, T;
+  chain_scan_fwd(loc, wbf, ex, T);
+  loop_residuals(T, &fl[0], &fl[1]);
+  const double cost = 0.5 * (c2[0] + (fl[0] * fl[0] + fl[1] * fl[1]));
+  if (!JAC) return cost;
+  Rt exs;
+  chain_scan_bwd(loc, wbb, exs);
+  double E1[3], E2[9];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) E1[a] = T.t[a] > 0.0 ? 1.0 : (T.t[a] < 0.0 ? -1.0 : 0.0);
+#pragma unroll
+  for (int a = 0; a < 9; ++a) {
+    const double dv = T.R[a] - ((a % 4 == 0) ? 1.0 : 0.0);
+    E2[a] = dv > 0.0 ? 1.0 : (dv < 0.0 ? -1.0 : 0.0);
+  }
+  // per frame: P_i = ex * (the thread's earlier frames), S_i = (its later frames) * exs
+  Rt Sf[F];
+  {
+    Rt Sc = exs;
+#pragma unroll
+    for (int f = F - 1; f >= 0; --f) {
+      Sf[f] = Sc;
+      if (t * F + f < m && f > 0) Sc = compose(F == 1 ? loc : rel[f], Sc);
+    }
+  }
+  Rt Pi = ex;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    if (t * F + f >= m) continue;
+    const Rt& Si = Sf[f];
+    const double* Rf = F == 1 ? loc.R : rel[f].R;
+    double u[3], PE[9], G[9];
+    for (int a = 0; a < 3; ++a) u[a] = Pi.R[a] * E1[0] + Pi.R[3 + a] * E1[1] + Pi.R[6 + a] * E1[2];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) PE[3 * a + b] = Pi.R[a] * E2[b] + Pi.R[3 + a] * E2[3 + b] + Pi.R[6 + a] * E2[6 + b];
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b)
+        G[3 * a + b] = PE[3 * a] * Si.R[3 * b] + PE[3 * a + 1] * Si.R[3 * b + 1] + PE[3 * a + 2] * Si.R[3 * b + 2];
+#pragma unroll 1
+    for (int k = 0; k < 3; ++k) {
+      double D[9];
+      rodrigues_jac_k(S.x[f], Rf, k, D);  // dR/dr_k only: 9 live values, not 27
+      double s1 = 0.0, s2 = 0.0;
+      for (int a = 0; a < 3; ++a) s1 += u[a] * (D[3 * a] * Si.t[0] + D[3 * a + 1] * Si.t[1] + D[3 * a + 2] * Si.t[2]);
+      for (int a = 0; a < 9; ++a) s2 += G[a] * D[a];
+      S.h(f, k) = 1000.0 * s1;
+      S.h(f, 3 + k) = 1000.0 * u[k];
+      S.h(f, 6 + k) = 1e5 * s2;
+      S.h(f, 9 + k) = 0.0;
+    }
+    if (f + 1 < F) Pi = compose(Pi, F == 1 ? loc : rel[f]);
+  }
+  return cost;
+}
+
+__device__ __forceinline__ double sgn(double v) { return v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0); }
+
+template <int F>
+__global__ __launch_bounds__(kRW) void k_chain_trf_r(double* __restrict__ ws, int m, int loop,
+                                                     int max_iter, int first, double ftol, double xtol,
+                                                     double gtol, int max_nfev,
+                                                     double* __restrict__ state) {
+  const ChainWs W(m);
+  __shared__ double red[2 * kRMax * kRWv];
+  __shared__ double wbf[12 * kRWv], wbb[12 * kRWv];
+  __shared__ double hl[F * 24 * kRW];
+  int ph = 0;
+  const int t = threadIdx.x;
+  Frames<F> S;
+  S.hl = hl;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int i = t * F + f;
+    const bool v = i < m;
+    S.r[f] = S.d0[f] = S.b1[f] = S.b2[f] = S.y[f] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      S.x[f][k] = v ? ws[W.x + 6 * i + k] : 0.0;
+      S.xt(f, k) = 0.0;
+      S.si(f, k) = v && !first ? ws[W.sinv + 6 * i + k] : 1.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) S.h(f, k) = 0.0;  // (own column only: no barrier)
+  }
+  auto valid = [&](int f) { return t * F + f < m; };
+  double fl[2], flt[2];
+  double cost = eval_r<F, true>(S, false, m, loop, red, ph, wbf, wbb, fl);
+  int nfev = first ? 1 : (int)state[2], njev = first ? 1 : (int)state[3];
+  auto update_scale = [&](bool init) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      if (!valid(f)) continue;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double gk = kW[k] * sgn(S.x[f][k]), h1 = S.h(f, k), h2 = S.h(f, 6 + k);
+        const double cn = sqrt((gk * gk + h1 * h1) + h2 * h2);
+        S.si(f, k) = init ? (cn == 0.0 ? 1.0 : cn) : fmax(S.si(f, k), cn);
+      }
+    }
+  };
+  double Delta, alpha;
+  if (first) {
+    update_scale(true);
+    double v[1] = {0.0};
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double a = S.x[f][k] * S.si(f, k);
+        v[0] += valid(f) ? a * a : 0.0;
+      }
+    rsum<1>(v, red, ph);
+    Delta = sqrt(v[0]);
+    if (Delta == 0.0) Delta = 1.0;
+    alpha = 0.0;
+    if (t == 0) state[0] = cost;
+  } else {
+    Delta = state[5];
+    alpha = state[6];
+  }
+  double E[3] = {0.0, 0.0, 0.0};  // |hs1|^2, hs1.hs2, |hs2|^2 of the iteration
+  int status = 0, it = 0;
+  for (; it < max_iter; ++it) {
+    double gmax = 0.0;
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      if (!valid(f)) continue;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double gk = kW[k] * sgn(S.x[f][k]) * S.r[f] + S.h(f, k) * fl[0] + S.h(f, 6 + k) * fl[1];
+        gmax = fmax(gmax, fabs(gk));
+      }
+    }
+    gmax = rmax(gmax, red, ph);
+    if (gmax < gtol) status = 1;
+    if (status != 0 || nfev >= max_nfev) break;
+    // scaled rows: d0 = |gs|^2, b1 = gs.hs1, b2 = gs.hs2; E and |J_h^T f|^2
+    double e[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      double d0 = 0.0, b1 = 0.0, b2 = 0.0;
+      if (valid(f)) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double s = 1.0 / S.si(f, k);
+          const double gs = kW[k] * sgn(S.x[f][k]) * s, h1 = S.h(f, k) * s, h2 = S.h(f, 6 + k) * s;
+          d0 += gs * gs;
+          b1 += gs * h1;
+          b2 += gs * h2;
+          e[0] += h1 * h1;
+          e[1] += h1 * h2;
+          e[2] += h2 * h2;
+          const double gh = gs * S.r[f] + h1 * fl[0] + h2 * fl[1];
+          e[3] += gh * gh;
+        }
+      }
+      S.d0[f] = d0;
+      S.b1[f] = b1;
+      S.b2[f] = b2;
+    }
+    rsum<4>(e, red, ph);
+    E[0] = e[0];
+    E[1] = e[1];
+    E[2] = e[2];
+    const double suf_norm = sqrt(e[3]);
+    double actual = -1.0, cost_new = cost;
+    // y = (K + a)^-1 f into S.y, yl; returns the 2x2 matrix (mA, mB, mC, det)
+    auto solve_y = [&](double a, double yl[2], double mat[4]) {
+      yl[0] = yl[1] = 0.0;
+      mat[0] = mat[1] = mat[2] = 0.0;
+      mat[3] = 1.0;
+      if (loop) {
+        double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          if (!valid(f)) continue;
+          const double da = S.d0[f] + a, b1 = S.b1[f], b2 = S.b2[f], ri = S.r[f];
+          s[0] += b1 * b1 / da;
+          s[1] += b1 * b2 / da;
+          s[2] += b2 * b2 / da;
+          s[3] += b1 * ri / da;
+          s[4] += b2 * ri / da;
+        }
+        rsum<5>(s, red, ph);
+        mat[0] = E[0] + a - s[0];
+        mat[1] = E[1] - s[1];
+        mat[2] = E[2] + a - s[2];
+        const double r1 = fl[0] - s[3], r2 = fl[1] - s[4];
+        mat[3] = mat[0] * mat[2] - mat[1] * mat[1];
+        yl[0] = (mat[2] * r1 - mat[1] * r2) / mat[3];
+        yl[1] = (mat[0] * r2 - mat[1] * r1) / mat[3];
+      }
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+        S.y[f] = valid(f) ? (S.r[f] - S.b1[f] * yl[0] - S.b2[f] * yl[1]) / (S.d0[f] + a) : 0.0;
+    };
+    while (actual <= 0.0 && nfev < max_nfev) {
+      double aup = suf_norm / Delta, alow = 0.0;
+      if (alpha == 0.0) alpha = fmax(0.001 * aup, sqrt(alow * aup));
+      double yl[2], mat[4], pn = 0.0;
+      for (int k = 0; k < 10; ++k) {
+        if (alpha < alow || alpha > aup) alpha = fmax(0.001 * aup, sqrt(alow * aup));
+        solve_y(alpha, yl, mat);
+        // f.y, y.y and (f - a y).z with z = (K + a)^-1 y never formed
+        double q[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // Z1 Z2 fy yy A B1 B2
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          if (!valid(f)) continue;
+          const double da = S.d0[f] + alpha, yi = S.y[f], fi = S.r[f];
+          const double w = fi - alpha * yi;
+          q[0] += S.b1[f] * yi / da;
+          q[1] += S.b2[f] * yi / da;
+          q[2] += fi * yi;
+          q[3] += yi * yi;
+          q[4] += w * yi / da;
+          q[5] += w * S.b1[f] / da;
+          q[6] += w * S.b2[f] / da;
+        }
+        rsum<7>(q, red, ph);
+        double zl0 = 0.0, zl1 = 0.0;
+        if (loop) {
+          const double s1 = yl[0] - q[0], s2 = yl[1] - q[1];
+          zl0 = (mat[2] * s1 - mat[1] * s2) / mat[3];
+          zl1 = (mat[0] * s2 - mat[1] * s1) / mat[3];
+        }
+        const double q0 = q[2] + (fl[0] * yl[0] + fl[1] * yl[1]);
+        const double q1 = q[3] + (yl[0] * yl[0] + yl[1] * yl[1]);
+        const double q2 = (q[4] - zl0 * q[5] - zl1 * q[6]) +
+                          ((fl[0] - alpha * yl[0]) * zl0 + (fl[1] - alpha * yl[1]) * zl1);
+        pn = sqrt(fmax(q0 - alpha * q1, 0.0));
+        const double phi = pn - Delta, dphi = -q2 / pn;
+        if (phi < 0.0) aup = alpha;
+        const double ratio = phi / dphi;
+        alow = fmax(alow, alpha - ratio);
+        alpha -= (phi + Delta) * ratio / Delta;
+        if (fabs(phi) < 0.01 * Delta) break;
+      }
+      // the step at the final alpha, rescaled to |p| = Delta:
+      // p = -c J_h^T y (c = Delta / |p(alpha)|), step = p / sinv; the sums the
+      // step, |step|^2 and the predicted reduction need, taken before c is known
+      solve_y(alpha, yl, mat);
+      double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // fy yy |x|^2 gp'^2 gp'r h1p' h2p' st'^2
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        if (!valid(f)) continue;
+        const double yi = S.y[f];
+        q[0] += S.r[f] * yi;
+        q[1] += yi * yi;
+        double gp = 0.0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double si = S.si(f, k);
+          const double gs = kW[k] * sgn(S.x[f][k]) / si, h1 = S.h(f, k) / si, h2 = S.h(f, 6 + k) / si;
+          const double php = -((gs * yi + h1 * yl[0]) + h2 * yl[1]);
+          const double stp = php / si;
+          q[2] += S.x[f][k] * S.x[f][k];
+          q[7] += stp * stp;
+          gp += gs * php;
+          q[5] += h1 * php;
+          q[6] += h2 * php;
+        }
+        q[3] += gp * gp;
+        q[4] += gp * S.r[f];
+      }
+      rsum<8>(q, red, ph);
+      pn = sqrt(fmax((q[0] + (fl[0] * yl[0] + fl[1] * yl[1])) - alpha * (q[1] + (yl[0] * yl[0] + yl[1] * yl[1])), 0.0));
+      const double c = Delta / pn;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const double yi = S.y[f];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double si = S.si(f, k);
+          const double gs = kW[k] * sgn(S.x[f][k]) / si, h1 = S.h(f, k) / si, h2 = S.h(f, 6 + k) / si;
+          const double ph2 = -c * ((gs * yi + h1 * yl[0]) + h2 * yl[1]);
+          S.xt(f, k) = valid(f) ? S.x[f][k] + ph2 / si : 0.0;
+        }
+      }
+      const double jp0 = c * (0.5 * c * q[3] + q[4]), jp1 = c * q[5], jp2 = c * q[6];
+      const double quad = jp0 + (jp1 * (0.5 * jp1 + fl[0]) + jp2 * (0.5 * jp2 + fl[1]));
+      const double predicted = -quad;
+      cost_new = eval_r<F, false>(S, true, m, loop, red, ph, wbf, wbb, flt);
+      ++nfev;
+      const double step_h_norm = Delta;  // |p| = Delta after the rescale
+      if (!isfinite(cost_new)) {
+        Delta = 0.25 * step_h_norm;
+        continue;
+      }
+      actual = cost - cost_new;
+      double ratio;
+      if (predicted > 0.0) ratio = actual / predicted;
+      else if (predicted == actual) ratio = 1.0;
+      else ratio = 0.0;
+      double Dn = Delta;
+      if (ratio < 0.25) Dn = 0.25 * step_h_norm;
+      else if (ratio > 0.75 && step_h_norm > 0.95 * Delta) Dn = 2.0 * Delta;
+      const double step_norm = c * sqrt(q[7]);
+      const bool ftol_ok = actual < ftol * cost && ratio > 0.25;
+      const bool xtol_ok = step_norm < xtol * (xtol + sqrt(q[2]));
+      if (ftol_ok || xtol_ok) {
+        status = ftol_ok && xtol_ok ? 4 : (ftol_ok ? 2 : 3);
+        break;
+      }
+      alpha *= Delta / Dn;
+      Delta = Dn;
+    }
+    if (actual > 0.0) {
+#pragma unroll
+      for (int f = 0; f < F; ++f)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) S.x[f][k] = S.xt(f, k);
+      cost = eval_r<F, true>(S, false, m, loop, red, ph, wbf, wbb, fl);
+      ++njev;
+      update_scale(false);
+    }
+    if (status != 0) {
+      ++it;
+      break;
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int i = t * F + f;
+    if (i >= m) continue;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      ws[W.x + 6 * i + k] = S.x[f][k];
+      ws[W.sinv + 6 * i + k] = S.si(f, k);
+    }
+  }
+  if (t == 0) {
+    state[1] = cost;
+    state[2] = nfev;
+    state[3] = njev;
+    state[4] = status;
+    state[5] = Delta;
+    state[6] = alpha;
+    state[7] = (first ? 0.0 : state[7]) + it;
+  }
+}
+
 }  // namespace
 
 extern "C" int slam_pose_chain_objective(const double* d_params, int n_vec, int n_frames, int loop,
@@ -595,9 +1133,16 @@ extern "C" int slam_pose_chain_trf(double* d_ws, int n_frames, int loop, int max
                                    double* d_state, void* stream) {
   SLAM_REQUIRE(n_frames >= 1 && max_iter >= 0 && max_nfev >= 1, "slam_pose_chain_trf: bad sizes");
   SLAM_REQUIRE(d_ws && d_state, "slam_pose_chain_trf: null pointer");
-  k_chain_trf<<<1, kLmWG, 0, slam::as_stream(stream)>>>(d_ws, n_frames, loop ? 1 : 0, max_iter,
-                                                        first ? 1 : 0, ftol, xtol, gtol, max_nfev,
-                                                        d_state);
+  hipStream_t s = slam::as_stream(stream);
+  const int lp = loop ? 1 : 0, fi = first ? 1 : 0;
+  const char* form = getenv("SLAM_CHAIN_TRF");  // "lds": the round-4 kernel (A/B)
+  if (form != nullptr && form[0] == 'l') {
+    k_chain_trf<<<1, kLmWG, 0, s>>>(d_ws, n_frames, lp, max_iter, fi, ftol, xtol, gtol, max_nfev, d_state);
+  } else if (n_frames <= kRW) {
+    k_chain_trf_r<1><<<1, kRW, 0, s>>>(d_ws, n_frames, lp, max_iter, fi, ftol, xtol, gtol, max_nfev, d_state);
+  } else {
+    k_chain_trf<<<1, kLmWG, 0, s>>>(d_ws, n_frames, lp, max_iter, fi, ftol, xtol, gtol, max_nfev, d_state);
+  }
   SLAM_LAUNCHED("k_chain_trf");
   return SLAM_OK;
 }
