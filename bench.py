@@ -731,11 +731,12 @@ def c4_sharded_iters(world, rank, steps=20, warmup=3):
     cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
     c0, p0 = perturb(rng, cams, pts)
     if world > 1:
-        from slam355.dist import shard_by_anchor
+        from slam355.dist import shard_by_anchor, shard_chunks_per_wg
 
         mine, keep, local_pi = shard_by_anchor(C, P, ci, pi, rank, world)
         prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep],
-                         block_list=upper_blocks(C, ci, pi))
+                         block_list=upper_blocks(C, ci, pi),
+                         chunks_per_wg=shard_chunks_per_wg(int(keep.sum())))
         step_fn = prob.step_distributed
         n_obs = int(keep.sum())
     else:
@@ -807,11 +808,12 @@ def run_ba(args, world, rank):
     cams, pts, ci, pi, qs = gen(rng, C, P, k)
     c0, p0 = perturb(rng, cams, pts)
     if world > 1:
-        from slam355.dist import shard_by_anchor
+        from slam355.dist import shard_by_anchor, shard_chunks_per_wg
 
         mine, keep, local_pi = shard_by_anchor(C, P, ci, pi, rank, world)
         prob = BAProblem(c0, p0[mine], ci[keep], local_pi, qs[keep],
-                         block_list=upper_blocks(C, ci, pi))
+                         block_list=upper_blocks(C, ci, pi),
+                         chunks_per_wg=shard_chunks_per_wg(int(keep.sum())))
         step_fn = prob.step_distributed
     else:
         prob = BAProblem(c0, p0, ci, pi, qs, chunks_per_wg=args.chunks_per_wg,

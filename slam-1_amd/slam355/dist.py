@@ -33,6 +33,22 @@ def shard_by_anchor(n_cams, n_pts, cam_idx, pt_idx, rank, world):
     return mine, keep, remap[pt_idx[keep]]
 
 
+def shard_chunks_per_wg(n_obs: int):
+    """Linearisation chunks per workgroup for ONE rank's landmark shard of a
+    window solved alone on its GPU (BAProblem chunks_per_wg): small shards want
+    more, smaller workgroups than the planner's default (which is tuned for
+    windows batched together).  Measured per-rank iteration at C4 / C5
+    (scripts/shard_split.py, profiles/r5/shard_split/): W = 8 (313 chunks) 1 ->
+    175 us vs 184 at the default 3; W = 4 / 2 (625 / 1250 chunks) 2 -> 192 /
+    232 us vs 200 / 237; None (the planner's rule) from 4096 chunks up."""
+    from .ba import MF_CHUNK_OBS
+
+    n_chunks = -(-int(n_obs) // MF_CHUNK_OBS)
+    if n_chunks < 512:
+        return 1
+    return 2 if n_chunks < 4096 else None
+
+
 def gather_pose_chain(rvec, tvec, ninl, pose0=None, T0=None, group=None):
     """The global trajectory of frame-pair shards: rank r tracked pairs
     r*B .. r*B + B - 1 (equal B on every rank) and holds their PnP results
