@@ -20,6 +20,7 @@
 #include "common.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace {
@@ -32,6 +33,7 @@ constexpr int kFastT = 20;
 constexpr int kOrbWG = 512;
 constexpr int kMaxTiles = 256;
 constexpr int kMaxShapes = 4;
+constexpr int kMaxBat = 4;  // small pyramid levels batched into one group
 constexpr int kNMS0 = 29;  // score-map region starts here (needs [30, w-31])
 constexpr int kBl0 = 12;   // blurred region starts here (rotated samples within +-18 of [31, w-32])
 constexpr int kFqW = 320;  // queue entries per wave: < 64 carried + 256 appended per pass
@@ -58,6 +60,16 @@ struct OrbGeom {
   int sw[kMaxShapes], sh[kMaxShapes];
   int lw[kMaxShapes][kNLev], lh[kMaxShapes][kNLev];
   int nlev[kMaxShapes];  // levels to run for this shape (0..nlev-1)
+  // Small levels bat0 .. nlev-1 run as ONE group (LDS variant, tiled mode):
+  // their images resident together in A, every phase one pass over all of
+  // them (see "batched small levels" in k_orb_tile).  bat0 == nlev: none.
+  int bat0[kMaxShapes];
+  int bslot[kMaxShapes][kMaxBat];     // A byte offset of group level j's image
+  int bhist[kMaxShapes];              // A byte offset of hist4 [kMaxBat][256], ctr4 [kMaxBat][16]
+  int bsmap[kMaxShapes][kMaxBat];     // U byte offset of level j's FAST score map
+  int bbl[kMaxShapes][kMaxBat];       // U byte offset of level j's blurred image
+  int bcand[kMaxShapes][kMaxBat + 1]; // level j's NMS candidates in the tile's scratch (entries)
+  int bnseg[kMaxShapes][kMaxBat];     // blur row segments per column group of level j
   uint8_t tile_shape[kMaxTiles];
 };
 
@@ -224,6 +236,33 @@ __device__ unsigned long long g_orb_prof[96];
 #define ORB_CUT(ph) (void)0
 #endif
 
+// Item i of a concatenation of up to 4 ranges (sizes n0, n1, n2, ...): its
+// range j, i becomes the index inside it.
+__device__ __forceinline__ int seg4(int& i, int NB, int n0, int n1, int n2) {
+  int j = 0;
+  if (NB > 1 && i >= n0) {
+    i -= n0;
+    j = 1;
+    if (NB > 2 && i >= n1) {
+      i -= n1;
+      j = 2;
+      if (NB > 3 && i >= n2) {
+        i -= n2;
+        j = 3;
+      }
+    }
+  }
+  return j;
+}
+// element j of four values (scalars, not an array in memory: a selected
+// array element can be turned into a dynamically indexed private array,
+// i.e. scratch, and LDS pointers into flat ones)
+template <typename T>
+__device__ __forceinline__ T pick4v(int j, T a0, T a1, T a2, T a3) {
+  return j == 0 ? a0 : (j == 1 ? a1 : (j == 2 ? a2 : a3));
+}
+#define pick4(j, a) pick4v((j), (a)[0], (a)[1], (a)[2], (a)[3])
+
 struct KP {  // one kept keypoint of the current level (LDS)
   int x, y;
   float resp, angle;
@@ -300,10 +339,68 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
   __syncthreads();
   ORB_T(0);
 
+  // ---- resize S (SW x SH) -> D (W x H, pitch lpitch(W)), INTER_LINEAR_EXACT;
+  // the tables live in U past the largest resize target (host layout)
+  auto resize_level = [&](const uint8_t* S, int SW, int SH, uint8_t* D, int W, int H) {
+    const int SP = lpitch(SW), P = lpitch(W);
+    // x coefficients for the padded row (columns past W: any in-bounds source)
+    for (int i = t; i < P; i += kOrbWG) tabx[i] = i < W ? lin_coeff(i, W, SW) : 0;
+    for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
+    __syncthreads();
+    // Four adjacent destination pixels per lane: their x coefficients are one
+    // 16-byte LDS read, the row coefficient one, the 16 source bytes are read
+    // before the four results leave as one dword (consecutive lanes write
+    // consecutive dwords).  The padding bytes of a row get junk, never read.
+    const int NG = P >> 2, NT = NG * H;
+    const uint32_t mNG = div_magic(NG);
+    // an opaque 1 (H > 0 is checked on the host): rp[0] / rp[1] stay two
+    // byte reads (merged, they become a ds_read_u16 at odd addresses, which
+    // made the kernel 1.5x slower)
+    const int one = g.H > 0 ? 1 : 0;
+    for (int i = t; i < NT; i += kOrbWG) {
+      const int y = fdiv(i, mNG), x = 4 * (i - y * NG);
+      const int cy = taby[y];
+      const int4 c4 = *reinterpret_cast<const int4*>(tabx + x);
+      const int cx[4] = {c4.x, c4.y, c4.z, c4.w};
+      const uint8_t* r0 = S + (cy >> 9) * SP;
+      const int d1 = cy & 511, d0 = 256 - d1;
+      int p00[4], p01[4], p10[4], p11[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint8_t* rp = r0 + (cx[q] >> 9);
+        p00[q] = rp[0];
+        if (kGlob) {
+          // global level buffers: the +1 neighbours are only read with a
+          // non-zero weight (the last column / row may sit on the buffer's end)
+          p01[q] = (cx[q] & 511) ? rp[1] : 0;
+          p10[q] = d1 ? rp[SP] : 0;
+          p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
+        } else {
+          // LDS: past the last source row / column lies more of the LDS
+          // allocation (U follows A), and a neighbour outside the source has
+          // weight 0 -- read unconditionally (no exec-mask code per byte)
+          p01[q] = rp[one];
+          p10[q] = rp[SP];
+          p11[q] = rp[SP + one];
+        }
+      }
+      uint32_t w = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c1 = cx[q] & 511, c0 = 256 - c1;
+        const int v = d0 * (c0 * p00[q] + c1 * p01[q]) + d1 * (c0 * p10[q] + c1 * p11[q]);
+        w |= (uint32_t)min((v + 32768) >> 16, 255) << (8 * q);
+      }
+      *reinterpret_cast<uint32_t*>(D + y * P + x) = w;
+    }
+    __syncthreads();
+  };
+
   int nout = 0;      // keypoints written for this tile (uniform)
   int overflow = 0;  // uniform
   const int nlev = g.nlev[shp];
-  for (int l = 0; l < nlev; ++l) {
+  const int lb = kGlob ? nlev : g.bat0[shp];  // levels lb .. nlev-1: the batched group below
+  for (int l = 0; l < lb; ++l) {
 #ifdef SLAM_ORB_PROFILE
     orb_lv = l;
 #endif
@@ -311,60 +408,7 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int P = lpitch(W);  // row pitch of the level image
     if (l > 0) {
       // ---- resize level l-1 (A) -> l (U, INTER_LINEAR_EXACT), then U -> A
-      const int SW = g.lw[shp][l - 1], SH = g.lh[shp][l - 1];
-      const int SP = lpitch(SW);
-      const uint8_t* S = A;
-      // x coefficients for the padded row (columns past W: any in-bounds source)
-      for (int i = t; i < P; i += kOrbWG) tabx[i] = i < W ? lin_coeff(i, W, SW) : 0;
-      for (int i = t; i < H; i += kOrbWG) taby[i] = lin_coeff(i, H, SH);
-      __syncthreads();
-      // Four adjacent destination pixels per lane: their x coefficients are one
-      // 16-byte LDS read, the row coefficient one, the 16 source bytes are read
-      // before the four results leave as one dword (consecutive lanes write
-      // consecutive dwords).  The padding bytes of a row get junk, never read.
-      const int NG = P >> 2, NT = NG * H;
-      const uint32_t mNG = div_magic(NG);
-      // an opaque 1 (H > 0 is checked on the host): rp[0] / rp[1] stay two
-      // byte reads (merged, they become a ds_read_u16 at odd addresses, which
-      // made the kernel 1.5x slower)
-      const int one = g.H > 0 ? 1 : 0;
-      for (int i = t; i < NT; i += kOrbWG) {
-        const int y = fdiv(i, mNG), x = 4 * (i - y * NG);
-        const int cy = taby[y];
-        const int4 c4 = *reinterpret_cast<const int4*>(tabx + x);
-        const int cx[4] = {c4.x, c4.y, c4.z, c4.w};
-        const uint8_t* r0 = S + (cy >> 9) * SP;
-        const int d1 = cy & 511, d0 = 256 - d1;
-        int p00[4], p01[4], p10[4], p11[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint8_t* rp = r0 + (cx[q] >> 9);
-          p00[q] = rp[0];
-          if (kGlob) {
-            // global level buffers: the +1 neighbours are only read with a
-            // non-zero weight (the last column / row may sit on the buffer's end)
-            p01[q] = (cx[q] & 511) ? rp[1] : 0;
-            p10[q] = d1 ? rp[SP] : 0;
-            p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
-          } else {
-            // LDS: past the last source row / column lies more of the LDS
-            // allocation (U follows A), and a neighbour outside the source has
-            // weight 0 -- read unconditionally (no exec-mask code per byte)
-            p01[q] = rp[one];
-            p10[q] = rp[SP];
-            p11[q] = rp[SP + one];
-          }
-        }
-        uint32_t w = 0u;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c1 = cx[q] & 511, c0 = 256 - c1;
-          const int v = d0 * (c0 * p00[q] + c1 * p01[q]) + d1 * (c0 * p10[q] + c1 * p11[q]);
-          w |= (uint32_t)min((v + 32768) >> 16, 255) << (8 * q);
-        }
-        *reinterpret_cast<uint32_t*>(U + y * P + x) = w;
-      }
-      __syncthreads();
+      resize_level(A, g.lw[shp][l - 1], g.lh[shp][l - 1], U, W, H);
       if (kGlob) {  // global level buffers: swap roles instead of copying
         uint8_t* tmp = A;
         A = U;
@@ -922,6 +966,607 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     ORB_T(9);
   }
+
+  // ======================= batched small levels lb .. nlev-1 =======================
+  // The small levels' per-keypoint phases cost about the same fixed latency on
+  // every level whatever its size (round-4 per-level profile: levels 3-6 of a
+  // 216x192 patch hold 29 % of the pixels and 40 % of the cycles).  Here their
+  // images are resident together in A (slots g.bslot), and each phase is ONE
+  // pass over all of them: resize chain, FAST maps (U, g.bsmap), NMS (per-level
+  // candidate ranges g.bcand, histograms / counters hist4 / ctr4 in A),
+  // retainBest(2n) thresholds (wave j: level j), survivors, Harris, rank +
+  // retainBest(n) (wave j: level j when every level has <= 64 survivors),
+  // IC angle, records, blurred levels (U, g.bbl), rBRIEF.  Every keypoint's
+  // arithmetic and the level-major output order are those of the per-level
+  // loop above: bit-identical output.
+  if (!kGlob && lb < nlev && !overflow) {
+#ifdef SLAM_ORB_PROFILE
+    orb_lv = lb;
+#endif
+    const int NB = nlev - lb;
+    int* hist4 = reinterpret_cast<int*>(A + g.bhist[shp]);  // [kMaxBat][256]
+    int* ctr4 = hist4 + kMaxBat * 256;  // [kMaxBat][16]: 0 candidates, 1 survivors, 2 T, 3 kept, 4 count
+    int bW[kMaxBat], bH[kMaxBat], bP[kMaxBat], bSWd[kMaxBat], bSW4[kMaxBat], bNG[kMaxBat];
+    int bSN4[kMaxBat], bNT[kMaxBat], bCap[kMaxBat], bC0[kMaxBat];
+    uint32_t bmG[kMaxBat], bmS[kMaxBat];
+    const uint8_t* bI[kMaxBat];
+    uint8_t* bSm[kMaxBat];
+#pragma unroll
+    for (int j = 0; j < kMaxBat; ++j) {
+      const int l = min(lb + j, nlev - 1);
+      bW[j] = g.lw[shp][l];
+      bH[j] = g.lh[shp][l];
+      bP[j] = lpitch(bW[j]);
+      bSWd[j] = bW[j] - 2 * kNMS0;
+      bSW4[j] = (bSWd[j] + 3) & ~3;
+      bNG[j] = bSW4[j] >> 2;
+      bSN4[j] = j < NB ? bNG[j] * (bH[j] - 2 * kNMS0) : 0;
+      bNT[j] = j < NB ? bNG[j] * (bH[j] - 2 * kEdge) : 0;
+      bmG[j] = div_magic(bNG[j]);
+      bmS[j] = div_magic(bSW4[j]);
+      bI[j] = A + g.bslot[shp][min(j, NB - 1)];
+      bSm[j] = U + g.bsmap[shp][min(j, NB - 1)];
+      bC0[j] = g.bcand[shp][min(j, NB - 1)];
+      bCap[j] = j < NB ? g.bcand[shp][j + 1] - g.bcand[shp][j] : 0;
+    }
+    // ---- (1) resize chain: level lb via U into slot 0 (level lb-1 in A is dead
+    // after it), then slot j-1 -> slot j directly
+    for (int j = 0; j < NB; ++j) {
+      const int l = lb + j;
+      uint8_t* D = j == 0 ? U : A + g.bslot[shp][j];
+      const uint8_t* Sp = j == 0 ? A : A + g.bslot[shp][j - 1];
+      resize_level(Sp, g.lw[shp][l - 1], g.lh[shp][l - 1], D, g.lw[shp][l], g.lh[shp][l]);
+      if (j == 0) {
+        for (int i = t; i < (bP[0] * bH[0] + 15) >> 4; i += kOrbWG)
+          reinterpret_cast<uint4*>(A + g.bslot[shp][0])[i] = reinterpret_cast<const uint4*>(U)[i];
+        __syncthreads();
+      }
+    }
+    for (int i = t; i < NB * 256; i += kOrbWG) hist4[i] = 0;
+    if (t < kMaxBat * 16) ctr4[t] = 0;
+    ORB_T(1);
+    // ---- (2) FAST score maps of every level, one pass (as the per-level
+    // form; queue entries carry the level in bits 30-31)
+    uint32_t* fq = reinterpret_cast<uint32_t*>(lds + g.lds_fq) + wid * kFqW;
+    {
+      const int tot = bSN4[0] + bSN4[1] + bSN4[2] + bSN4[3];
+      auto fast_drain = [&](int j0) {
+        const uint32_t e = fq[j0 + lane];
+        const int j = (int)(e >> 30), i = (int)(e & 0x3FFFFFFFu);
+        const int sw4 = pick4(j, bSW4), P = pick4(j, bP);
+        const int y = fdiv(i, pick4(j, bmS)), x = i - y * sw4;
+        pick4(j, bSm)[i] = (uint8_t)fast_full(pick4(j, bI) + (y + kNMS0) * P + x + kNMS0, P);
+      };
+      int nq = 0;
+      for (int gb = wid * 64;; gb += kOrbWG) {
+        const bool more = gb < tot;  // wave-uniform
+        if (more) {
+          const bool gv = gb + lane < tot;
+          int loc = min(gb + lane, tot - 1);
+          const int j = seg4(loc, NB, bSN4[0], bSN4[1], bSN4[2]);
+          const uint8_t* I = pick4(j, bI);
+          const int P = pick4(j, bP), NG4 = pick4(j, bNG), SW4 = pick4(j, bSW4), SWd = pick4(j, bSWd);
+          uint8_t* Smap = pick4(j, bSm);
+          auto win4 = [&](int a) {
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (a & ~3));
+            return __builtin_amdgcn_alignbyte(wp[1], wp[0], a & 3);
+          };
+          const int y = fdiv(loc, pick4(j, bmG)), x = 4 * (loc - y * NG4);
+          const int a = (y + kNMS0) * P + x + kNMS0;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + ((a - 3) & ~3));
+          const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2], d3 = wp[3];
+          const int sh = (a - 3) & 3;
+          const uint32_t up = win4(a - 3 * P), dn = win4(a + 3 * P);
+          const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+          const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+          const uint32_t q2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+          const uint64_t lo = ((uint64_t)q1 << 32) | q0;
+          const uint32_t cc = (uint32_t)(lo >> 24);
+          const uint32_t rt = (uint32_t)(((uint64_t)q2 << 32 | q1) >> 16);
+          const uint32_t okv[2] = {quick4(cc, dn, rt, up, q0), quick4(cc >> 8, dn >> 8, rt >> 8, up >> 8, q0 >> 8)};
+          if (__ballot(gv && (okv[0] | okv[1]) != 0u) != 0ull) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const bool in = gv && x + q < SWd;
+              const bool ok = in && ((okv[q & 1] >> (16 * (q >> 1))) & 0xFFFFu) != 0u;
+              const uint64_t m = __ballot(ok);
+              if (ok)
+                fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                    ((uint32_t)j << 30) | (uint32_t)(y * SW4 + x + q);
+              nq += __popcll(m);
+            }
+          }
+          if (gv) *reinterpret_cast<uint32_t*>(Smap + y * SW4 + x) = 0u;
+        }
+        while (nq >= 64 || (!more && nq > 0)) {
+          const int n = min(nq, 64);
+          nq -= n;
+          if (lane < n) fast_drain(nq);
+        }
+        if (!more) break;
+      }
+    }
+    __syncthreads();
+    ORB_T(2);
+    // ---- (3) strict 3x3 NMS + border over every level's map, one pass
+    // (queue entries: level in bits 24-25, y in 12-22, x in 0-11)
+    {
+      const int tot = bNT[0] + bNT[1] + bNT[2] + bNT[3];
+      auto nms_drain = [&](int j0) {
+        const uint32_t e = fq[j0 + lane];
+        const int j = (int)(e >> 24);
+        const uint32_t yx = e & 0xFFFFFFu;
+        const int yq = (int)(yx >> 12), xq = (int)(yx & 4095u);
+        const int SW4 = pick4(j, bSW4);
+        const uint8_t* sp = pick4(j, bSm) + (yq - kNMS0) * SW4 + (xq - kNMS0);
+        const int s = sp[0];
+        if (s > sp[-1] && s > sp[1] && s > sp[-SW4 - 1] && s > sp[-SW4] && s > sp[-SW4 + 1] &&
+            s > sp[SW4 - 1] && s > sp[SW4] && s > sp[SW4 + 1]) {
+          const int k = atomicAdd(&ctr4[16 * j], 1);
+          if (k < pick4(j, bCap)) gcand[pick4(j, bC0) + k] = ((uint32_t)s << 23) | yx;
+          atomicAdd(&hist4[256 * j + s], 1);
+        }
+      };
+      int nq = 0;
+      for (int base = wid * 64;; base += kOrbWG) {
+        const bool more = base < tot;  // wave-uniform
+        uint32_t w4 = 0u;
+        int y = 0, g4 = 0, j = 0;
+        if (more && base + lane < tot) {
+          int loc = base + lane;
+          j = seg4(loc, NB, bNT[0], bNT[1], bNT[2]);
+          const int yy = fdiv(loc, pick4(j, bmG));
+          g4 = loc - yy * pick4(j, bNG);
+          y = yy + kEdge;
+          w4 = *reinterpret_cast<const uint32_t*>(pick4(j, bSm) + (y - kNMS0) * pick4(j, bSW4) + 4 * g4);
+        }
+        if (__ballot(w4 != 0u) != 0ull) {
+          const int Wj = pick4(j, bW);
+#pragma unroll
+          for (int bb = 0; bb < 4; ++bb) {
+            const int x = kNMS0 + 4 * g4 + bb;
+            const bool ok = ((w4 >> (8 * bb)) & 255u) != 0u && x >= kEdge && x <= Wj - 1 - kEdge;
+            const uint64_t m = __ballot(ok);
+            if (ok)
+              fq[nq + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                  ((uint32_t)j << 24) | ((uint32_t)y << 12) | (uint32_t)x;
+            nq += __popcll(m);
+          }
+        }
+        while (nq >= 64 || (!more && nq > 0)) {
+          const int n = min(nq, 64);
+          nq -= n;
+          if (lane < n) nms_drain(nq);
+        }
+        if (!more) break;
+      }
+    }
+    __syncthreads();
+    ORB_T(3);
+    // ---- (4) retainBest(2 n_l) thresholds: wave j, level j
+    if (wid < NB) {
+      const int j = wid;
+      const int* hist = hist4 + 256 * j;
+      const int ncand = ctr4[16 * j];
+      int T = 0;
+      const int K = 2 * g.nl[lb + j];
+      if (ncand > K) {
+        const int c0 = hist[4 * lane], c1 = hist[4 * lane + 1];
+        const int c2 = hist[4 * lane + 2], c3 = hist[4 * lane + 3];
+        const int sm = c0 + c1 + c2 + c3;
+        int suf = sm;
+        for (int off = 1; off < 64; off <<= 1) {
+          const int o = __shfl_down(suf, off, 64);
+          if (lane + off < 64) suf += o;
+        }
+        int acc = suf - sm;
+        int tl = -1;
+        acc += c3;
+        if (acc >= K) tl = 4 * lane + 3;
+        else {
+          acc += c2;
+          if (acc >= K) tl = 4 * lane + 2;
+          else {
+            acc += c1;
+            if (acc >= K) tl = 4 * lane + 1;
+            else {
+              acc += c0;
+              if (acc >= K) tl = 4 * lane;
+            }
+          }
+        }
+        for (int off = 32; off > 0; off >>= 1) tl = max(tl, __shfl_xor(tl, off, 64));
+        T = tl;
+      }
+      int cnt = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cnt += 4 * lane + q >= T ? hist[4 * lane + q] : 0;
+      for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+      if (lane == 0) {
+        ctr4[16 * j + 2] = T;
+        ctr4[16 * j + 4] = cnt;
+      }
+    }
+    __syncthreads();
+    int bN[kMaxBat], bT[kMaxBat], bCnt[kMaxBat];
+    bool ovf = false;
+#pragma unroll
+    for (int j = 0; j < kMaxBat; ++j) {
+      bN[j] = j < NB ? ctr4[16 * j] : 0;
+      bT[j] = ctr4[16 * j + 2];
+      bCnt[j] = j < NB ? ctr4[16 * j + 4] : 0;
+      ovf = ovf || bN[j] > bCap[j];
+    }
+    if (ovf) {  // cannot happen for strict maxima (density <= 1/4); guard anyway
+      overflow = 1;
+    } else {
+      // ---- (5) survivors of every level, packed level after level (LDS when
+      // they all fit, the tile's global scratch otherwise)
+      const int cnt_tot = bCnt[0] + bCnt[1] + bCnt[2] + bCnt[3];
+      const bool sv_lds = cnt_tot <= g.list_cap;  // uniform
+      uint32_t* cand = sv_lds ? svc : gsvc;
+      float* cresp = sv_lds ? svr : gsvr;
+      int bSo[kMaxBat];
+      bSo[0] = 0;
+#pragma unroll
+      for (int j = 1; j < kMaxBat; ++j) bSo[j] = bSo[j - 1] + bCnt[j - 1];
+      {
+        const int tot = bN[0] + bN[1] + bN[2] + bN[3];
+        for (int i = t; i < tot; i += kOrbWG) {
+          int loc = i;
+          const int j = seg4(loc, NB, bN[0], bN[1], bN[2]);
+          const uint32_t c = gcand[pick4(j, bC0) + loc];
+          if ((int)(c >> 23) >= pick4(j, bT)) {
+            const int k = atomicAdd(&ctr4[16 * j + 1], 1);
+            cand[pick4(j, bSo) + k] = c;
+          }
+        }
+      }
+      __syncthreads();
+      ORB_T(4);
+      // the IC-angle disc masks into the (unused) per-level histogram slots
+      uint32_t* icm = reinterpret_cast<uint32_t*>(hist);
+      if (t < 17 * 8) {
+        const int vv = t >> 3, dd = t & 7;
+        const int um = vv < 16 ? (int)((0x368'9abc'ddee'efff'fULL >> (4 * vv)) & 15u) : -1;
+        uint32_t mk = 0u;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int u = 4 * dd + jj - 15;
+          mk |= ((u < 0 ? -u : u) <= um ? 1u : 0u) << (8 * jj);
+        }
+        icm[t] = mk;
+      }
+      // ---- (6) Harris on every survivor (16 lanes per survivor, as above)
+      {
+        const int sub = lane >> 4, sl = lane & 15;
+        for (int k0 = 4 * wid; k0 < cnt_tot; k0 += 4 * (kOrbWG / 64)) {
+          const int k = k0 + sub;
+          int loc = k < cnt_tot ? k : k0;
+          const uint32_t c = cand[loc];
+          const int j = seg4(loc, NB, bCnt[0], bCnt[1], bCnt[2]);
+          const uint8_t* I = pick4(j, bI);
+          const int P = pick4(j, bP);
+          const int hx = (int)(c & 4095u), hy = (int)((c >> 12) & 2047u);
+          int a = 0, bq = 0, cq = 0;
+#pragma unroll 2
+          for (int u = 0; u < 4; ++u) {
+            const int e = sl + 16 * u;
+            if (e < 49) {
+              const int i = e / 7, jx = e - 7 * (e / 7);
+              const uint8_t* pp = I + (hy - 3 + i) * P + (hx - 3 + jx);
+              const int Ix = (pp[1] - pp[-1]) * 2 + (pp[-P + 1] - pp[-P - 1]) + (pp[P + 1] - pp[P - 1]);
+              const int Iy = (pp[P] - pp[-P]) * 2 + (pp[P - 1] - pp[-P - 1]) + (pp[P + 1] - pp[-P + 1]);
+              a += Ix * Ix;
+              bq += Iy * Iy;
+              cq += Ix * Iy;
+            }
+          }
+#pragma unroll
+          for (int off = 8; off > 0; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            bq += __shfl_xor(bq, off, 64);
+            cq += __shfl_xor(cq, off, 64);
+          }
+          if (sl == 0 && k < cnt_tot) cresp[k] = harris_resp(a, bq, cq);
+        }
+      }
+      __syncthreads();
+      ORB_T(5);
+      // ---- (7) exact rank per level + retainBest(n_l); the kept keypoints of
+      // level j at L[sum of the earlier levels' kept counts ...]
+      const bool small = bCnt[0] <= 64 && bCnt[1] <= 64 && bCnt[2] <= 64 && bCnt[3] <= 64;
+      if (small) {
+        int rank = 0, mm = 0;
+        bool live = false;
+        uint32_t ci = 0u;
+        float ri = 0.f;
+        if (wid < NB) {
+          const int j = wid, nk = pick4(j, bCnt), off = pick4(j, bSo), n_l = g.nl[lb + j];
+          live = lane < nk;
+          ci = live ? cand[off + lane] : 0u;
+          ri = live ? cresp[off + lane] : 0.f;
+          const uint32_t yxi = ci & 0x7FFFFFu;
+          for (int jj = 0; jj < nk; ++jj) {
+            const float rj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ri), jj));
+            const uint32_t yxj = (uint32_t)__builtin_amdgcn_readlane((int)yxi, jj);
+            rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
+          }
+          mm = nk;
+          if (nk > n_l) {
+            const uint64_t bm = __ballot(live && rank == n_l - 1);
+            const float rs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ri),
+                                                                      (int)__builtin_ctzll(bm)));
+            mm = n_l + (int)__popcll(__ballot(live && rank >= n_l && ri == rs));
+          }
+          if (lane == 0) ctr4[16 * j + 3] = mm;
+        }
+        __syncthreads();
+        if (wid < NB) {
+          int Loff = 0;
+          for (int jj = 0; jj < wid; ++jj) Loff += ctr4[16 * jj + 3];
+          if (live && rank < mm) {
+            L[Loff + rank].x = (int)(ci & 4095u);
+            L[Loff + rank].y = (int)((ci >> 12) & 2047u);
+            L[Loff + rank].resp = ri;
+          }
+        }
+      } else {
+        int Loff = 0;
+        for (int j = 0; j < NB; ++j) {
+          const int nk = pick4(j, bCnt), off = pick4(j, bSo), n_l = g.nl[lb + j];
+          for (int i = t; i < nk; i += kOrbWG) {
+            const float ri = cresp[off + i];
+            const uint32_t ci = cand[off + i];
+            const uint32_t yxi = ci & 0x7FFFFFu;
+            int rank = 0;
+            for (int jj = 0; jj < nk; ++jj) {
+              const float rj = cresp[off + jj];
+              const uint32_t yxj = cand[off + jj] & 0x7FFFFFu;
+              rank += (rj > ri || (rj == ri && yxj < yxi)) ? 1 : 0;
+            }
+            if (Loff + rank < g.list_cap) {
+              L[Loff + rank].x = (int)(ci & 4095u);
+              L[Loff + rank].y = (int)((ci >> 12) & 2047u);
+              L[Loff + rank].resp = ri;
+            }
+          }
+          __syncthreads();
+          if (t == 0) {
+            int mm = nk, bad = 0;
+            if (nk > n_l) {
+              if (Loff + n_l > g.list_cap) {
+                bad = 1;
+              } else {
+                const float rs = L[Loff + n_l - 1].resp;
+                mm = n_l;
+                while (mm < nk && Loff + mm < g.list_cap && L[Loff + mm].resp == rs) ++mm;
+                if (Loff + mm == g.list_cap && mm < nk) bad = 1;
+              }
+            } else if (Loff + nk > g.list_cap) {
+              bad = 1;
+            }
+            ctr4[16 * j + 3] = bad ? -1 : mm;
+          }
+          __syncthreads();
+          const int mj = ctr4[16 * j + 3];
+          if (mj < 0) break;  // (uniform) reported as overflow below
+          Loff += mj;
+        }
+      }
+      __syncthreads();
+      ORB_T(6);
+      int bM[kMaxBat];
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < kMaxBat; ++j) {
+        bM[j] = j < NB ? ctr4[16 * j + 3] : 0;
+        bad = bad || bM[j] < 0;
+      }
+      const int M = bad ? 0 : bM[0] + bM[1] + bM[2] + bM[3];
+      if (bad || nout + M > g.tcap) {
+        overflow = 1;
+      } else {
+        // ---- (8) IC angle of every kept keypoint (two per wave, as above)
+        {
+          const int hh = lane >> 5, i = lane & 31, d = i & 7, r = i >> 3;
+          const uint32_t uoff = 0x03020100u + 0x04040404u * (uint32_t)d;
+          for (int k0 = 2 * wid; k0 < M; k0 += 2 * (kOrbWG / 64)) {
+            const int k = k0 + hh;
+            const bool kv = k < M;
+            const int kk = kv ? k : k0;
+            int loc = kk;
+            const int j = seg4(loc, NB, bM[0], bM[1], bM[2]);
+            const uint8_t* I = pick4(j, bI);
+            const int P = pick4(j, bP);
+            const int cx = L[kk].x, cy = L[kk].y;
+            uint32_t su = 0u, s1 = 0u;
+            int m01 = 0;
+            const int a0 = (cy - 15 + r) * P + cx - 15 + 4 * d;
+#pragma unroll 2
+            for (int it = 0; it < 8; ++it) {
+              const int v = r + 4 * it - 15;
+              const int a = a0 + 4 * it * P;
+              const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + (a & ~3));
+              const uint32_t px = __builtin_amdgcn_alignbyte(wp[1], wp[0], a & 3);
+              const uint32_t ones = icm[8 * (v < 0 ? -v : v) + d];
+              const uint32_t val = px & (ones * 0xFFu);
+              su = __builtin_amdgcn_udot4(uoff, val, su, false);
+              const uint32_t rs = __builtin_amdgcn_udot4(0x01010101u, val, 0u, false);
+              s1 += rs;
+              m01 += v * (int)rs;
+            }
+            int m10 = (int)su - 15 * (int)s1;
+            for (int off = 16; off > 0; off >>= 1) {
+              m10 += __shfl_xor(m10, off, 64);
+              m01 += __shfl_xor(m01, off, 64);
+            }
+            if (i == 0 && kv) L[k].angle = fast_atan2_deg((float)m01, (float)m10);
+          }
+        }
+        __syncthreads();  // the maps and survivor lists are dead (L holds the group)
+        ORB_T(7);
+        // ---- (9) keypoint records (wave 0, one lane per keypoint), then the
+        // blurred levels into U (threads shared in proportion to the pixels)
+        if (wid == 0) {
+          for (int k = lane; k < M; k += 64) {
+            int loc = k;
+            const int j = seg4(loc, NB, bM[0], bM[1], bM[2]);
+            const int l = lb + j;
+            const float ls = g.ls[l];
+            const KP kp = L[k];
+            const float xl = (float)kp.x * ls, yl = (float)kp.y * ls;
+            const float inv = 1.f / ls;
+            const int o = nout + k;
+            okp[(size_t)o * 5 + 0] = (float)((double)xl + (double)x0);
+            okp[(size_t)o * 5 + 1] = (float)((double)yl + (double)y0);
+            okp[(size_t)o * 5 + 2] = 31.f * ls;
+            okp[(size_t)o * 5 + 3] = kp.angle;
+            okp[(size_t)o * 5 + 4] = kp.resp;
+            ooct[o] = l;
+            float ang = kp.angle;
+            ang *= (float)(3.14159265358979323846 / 180.f);
+            KP q;
+            q.x = rne_f(xl * inv) - kBl0;
+            q.y = rne_f(yl * inv) - kBl0;
+            q.resp = (float)cos((double)ang);
+            q.angle = (float)sin((double)ang);
+            L[k] = q;
+          }
+        }
+        int bBP[kMaxBat], bBH[kMaxBat], bSeg[kMaxBat], bItems[kMaxBat], bNcg[kMaxBat];
+        uint8_t* bBl[kMaxBat];
+#pragma unroll
+        for (int j = 0; j < kMaxBat; ++j) {
+          bBP[j] = lpitch(bW[j] - 2 * kBl0);
+          bBH[j] = bH[j] - 2 * kBl0;
+          bNcg[j] = bBP[j] >> 2;
+          const int nseg = g.bnseg[shp][min(j, NB - 1)];
+          bSeg[j] = (bBH[j] + nseg - 1) / nseg;
+          bItems[j] = j < NB ? bNcg[j] * nseg : 0;
+          bBl[j] = U + g.bbl[shp][min(j, NB - 1)];
+        }
+        {
+          const float k0 = g.gk[0], k1 = g.gk[1], k2 = g.gk[2], k3 = g.gk[3];
+          const float k4 = g.gk[4], k5 = g.gk[5], k6 = g.gk[6];
+          const int tot = bItems[0] + bItems[1] + bItems[2] + bItems[3];
+          for (int item = t; item < tot; item += kOrbWG) {
+            int loc = item;
+            const int j = seg4(loc, NB, bItems[0], bItems[1], bItems[2]);
+            const int ncg = pick4(j, bNcg), seg = pick4(j, bSeg), BH = pick4(j, bBH), BP = pick4(j, bBP);
+            const uint8_t* I = pick4(j, bI);
+            const int P = pick4(j, bP);
+            uint8_t* Bl = pick4(j, bBl);
+            const int sg = loc / ncg, cg = loc - sg * ncg;
+            const int r0 = sg * seg, r1 = min(BH, r0 + seg);
+            if (r0 >= r1) continue;
+            const int c4 = 4 * cg, x = c4 + kBl0;
+            auto rowf4 = [&](int y, float4& o) {
+              const uint32_t* wp = reinterpret_cast<const uint32_t*>(I + y * P + x - 4);
+              const uint32_t d0 = wp[0], d1 = wp[1], d2 = wp[2];
+              const uint32_t q0 = __builtin_amdgcn_alignbyte(d1, d0, 1);
+              const uint32_t q1 = __builtin_amdgcn_alignbyte(d2, d1, 1);
+              const uint32_t q2 = d2 >> 8;
+              float pq[10];
+              pq[0] = (float)((q0 >> 0) & 0xFFu);
+              pq[1] = (float)((q0 >> 8) & 0xFFu);
+              pq[2] = (float)((q0 >> 16) & 0xFFu);
+              pq[3] = (float)((q0 >> 24) & 0xFFu);
+              pq[4] = (float)((q1 >> 0) & 0xFFu);
+              pq[5] = (float)((q1 >> 8) & 0xFFu);
+              pq[6] = (float)((q1 >> 16) & 0xFFu);
+              pq[7] = (float)((q1 >> 24) & 0xFFu);
+              pq[8] = (float)((q2 >> 0) & 0xFFu);
+              pq[9] = (float)((q2 >> 8) & 0xFFu);
+              float rr[4];
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj) {
+                float acc = 0.f;
+                acc = fmaf(pq[jj], k0, acc);
+                acc = fmaf(pq[jj + 1], k1, acc);
+                acc = fmaf(pq[jj + 2], k2, acc);
+                acc = fmaf(pq[jj + 3], k3, acc);
+                acc = fmaf(pq[jj + 4], k4, acc);
+                acc = fmaf(pq[jj + 5], k5, acc);
+                acc = fmaf(pq[jj + 6], k6, acc);
+                rr[jj] = acc;
+              }
+              o = make_float4(rr[0], rr[1], rr[2], rr[3]);
+            };
+            const int yb = r0 + kBl0;
+            float4 w[7];
+            static_for<0, 7>([&](auto Iq) { rowf4(yb - 3 + decltype(Iq)::value, w[decltype(Iq)::value]); });
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 kk3 = {k3, k3}, kk4 = {k4, k4}, kk5 = {k5, k5}, kk6 = {k6, k6};
+            for (int r = r0; r < r1; r += 7) {
+              static_for<0, 7>([&](auto K) {
+                constexpr int k = decltype(K)::value;
+                if (r + k < r1) {
+                  const float4 a0 = w[k % 7], a1 = w[(k + 1) % 7], a2 = w[(k + 2) % 7];
+                  const float4 a3 = w[(k + 3) % 7], a4 = w[(k + 4) % 7], a5 = w[(k + 5) % 7];
+                  const float4 a6 = w[(k + 6) % 7];
+                  auto col = [&](f2 x0_, f2 x1_, f2 x2_, f2 x3_, f2 x4_, f2 x5_, f2 x6_) {
+                    f2 s0 = x3_ * kk3;
+                    s0 = __builtin_elementwise_fma(x4_ + x2_, kk4, s0);
+                    s0 = __builtin_elementwise_fma(x5_ + x1_, kk5, s0);
+                    return __builtin_elementwise_fma(x6_ + x0_, kk6, s0);
+                  };
+                  const f2 lo = col(f2{a0.x, a0.y}, f2{a1.x, a1.y}, f2{a2.x, a2.y}, f2{a3.x, a3.y},
+                                    f2{a4.x, a4.y}, f2{a5.x, a5.y}, f2{a6.x, a6.y});
+                  const f2 hi = col(f2{a0.z, a0.w}, f2{a1.z, a1.w}, f2{a2.z, a2.w}, f2{a3.z, a3.w},
+                                    f2{a4.z, a4.w}, f2{a5.z, a5.w}, f2{a6.z, a6.w});
+                  uint32_t packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(lo.x), 0, 0u);
+                  packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(lo.y), 1, packed);
+                  packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(hi.x), 2, packed);
+                  packed = __builtin_amdgcn_cvt_pk_u8_f32(rintf(hi.y), 3, packed);
+                  *reinterpret_cast<uint32_t*>(Bl + (r + k) * BP + c4) = packed;
+                  if (r + k + 1 < r1) rowf4(r + k + 1 + kBl0 + 3, w[k]);
+                }
+              });
+            }
+          }
+        }
+        __syncthreads();
+        ORB_T(8);
+        // ---- (10) rBRIEF of every kept keypoint (32 lanes per keypoint)
+        {
+          const int half = lane >> 5, byte = lane & 31;
+          uint32_t pat[8];
+#pragma unroll
+          for (int bit = 0; bit < 8; ++bit)
+            pat[bit] = reinterpret_cast<const uint32_t*>(c_pattern)[byte * 8 + bit];
+          for (int k = 2 * wid + half; k < M; k += 2 * (kOrbWG / 64)) {
+            int loc = k;
+            const int j = seg4(loc, NB, bM[0], bM[1], bM[2]);
+            const uint8_t* Bl = pick4(j, bBl);
+            const int BP = pick4(j, bBP);
+            const KP kp = L[k];
+            const int cx = kp.x, cy = kp.y;
+            const float a = kp.resp, bb = kp.angle;
+            int val = 0;
+#pragma unroll
+            for (int bit = 0; bit < 8; ++bit) {
+              uint32_t pw = pat[bit];
+              __asm__ volatile("" : "+v"(pw));
+              const float px1 = (float)(int8_t)(pw & 0xFFu), py1 = (float)(int8_t)((pw >> 8) & 0xFFu);
+              const float px2 = (float)(int8_t)((pw >> 16) & 0xFFu), py2 = (float)(int8_t)(pw >> 24);
+              const int ix1 = rne_f(px1 * a - py1 * bb), iy1 = rne_f(px1 * bb + py1 * a);
+              const int ix2 = rne_f(px2 * a - py2 * bb), iy2 = rne_f(px2 * bb + py2 * a);
+              const int t0 = Bl[(cy + iy1) * BP + cx + ix1];
+              const int t1 = Bl[(cy + iy2) * BP + cx + ix2];
+              val |= (t0 < t1 ? 1 : 0) << bit;
+            }
+            odesc[(size_t)(nout + k) * 32 + byte] = (uint8_t)val;
+          }
+        }
+        nout += M;
+        __syncthreads();
+        ORB_T(9);
+      }
+    }
+  }
   if (t == 0) ws_cnt[slot] = overflow ? -1 : nout;
 }
 
@@ -1103,6 +1748,49 @@ int build_geom(int H, int W, int stride, int max_kp, int overlap_div, int height
   g->lds_s = g->lds_l + al(g->list_cap * (int)sizeof(KP));
   g->lds_m = g->lds_s + al(g->list_cap * 8);
   g->lds_total = g->lds_m + (256 + 16) * 4;
+  // the small-level group of each shape: the smallest first level whose
+  // images (+ per-level histograms / counters) fit A, FAST maps fit U below
+  // the queues, blurred images fit U, candidates fit the tile scratch
+  // (tiled LDS variant only; SLAM_ORB_NOBATCH=1 turns it off for A/B)
+  const char* nob = getenv("SLAM_ORB_NOBATCH");
+  const bool batch_ok = !g->glob && g->n_tiles > 1 && !(nob != nullptr && nob[0] == '1');
+  for (int s = 0; s < g->nshapes; ++s) {
+    const int nl = g->nlev[s];
+    g->bat0[s] = nl;
+    if (!batch_ok) continue;
+    for (int lb = max(1, nl - kMaxBat); lb <= nl - 2; ++lb) {
+      const int NB = nl - lb;
+      bool fit = true;
+      int ao = 0, uo = 0, bo = 0, co = 0;
+      long px_tot = 0;
+      for (int j = 0; j < NB; ++j) {
+        const int l = lb + j, W = g->lw[s][l], H = g->lh[s][l];
+        fit = fit && W > 2 * kEdge && H > 2 * kEdge && g->nl[l] > 0;
+        g->bslot[s][j] = ao;
+        ao += al(lpitch(W) * H);
+        g->bsmap[s][j] = uo;
+        uo += al((((W - 2 * kNMS0) + 3) & ~3) * (H - 2 * kNMS0));
+        g->bbl[s][j] = bo;
+        bo += al(lpitch(W - 2 * kBl0) * (H - 2 * kBl0));
+        g->bcand[s][j] = co;
+        co += ((W - 2 * kEdge + 1) / 2) * ((H - 2 * kEdge + 1) / 2);
+        px_tot += (long)lpitch(W - 2 * kBl0) * (H - 2 * kBl0);
+      }
+      g->bcand[s][NB] = co;
+      g->bhist[s] = ao;
+      ao += kMaxBat * (256 + 16) * 4;
+      fit = fit && ao <= al(max_a) && uo <= al(max_smap) && bo <= max_u && co <= g->cand_cap;
+      if (!fit) continue;
+      for (int j = 0; j < NB; ++j) {  // blur threads in proportion to the level's pixels
+        const int l = lb + j, W = g->lw[s][l], H = g->lh[s][l];
+        const int BP = lpitch(W - 2 * kBl0), ncg = BP >> 2;
+        const double share = (double)kOrbWG * BP * (H - 2 * kBl0) / (double)px_tot;
+        g->bnseg[s][j] = max(1, (int)(share / ncg));
+      }
+      g->bat0[s] = lb;
+      break;
+    }
+  }
   // slots per tile: the budget plus 64 for retainBest's boundary ties; a single
   // patch (orb_extraction_detect) gets room for a full tie list on every level
   g->tcap = g->n_tiles == 1 ? kNLev * g->list_cap : max_kp + 64;
