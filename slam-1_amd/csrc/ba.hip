@@ -2031,18 +2031,73 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   __syncthreads();
   TL_STAMP(1);
   FAC_T(0);
-  // Block columns 0 and 1: wave 0 factors the diagonal block, then every wave
-  // takes a panel block and trailing blocks (workgroup barriers between).
+  // One loop over the block columns with ONE instance of wave 0's 16x16 code
+  // (an instance per block column measured 0.4-1.0 us slower per block: the
+  // unrolled factor is ~16 KB of code and the copies missed the instruction
+  // cache).  Block columns 0 and 1: wave 0 factors the diagonal block, then
+  // every wave takes a panel block and trailing blocks (workgroup barriers
+  // between).  Block columns 2 and 3 are wave 0's chain alone (block 2's
+  // factor, the last panel block L_32 and trailing block A_33, block 3's
+  // factor: no workgroup barrier on it).  Waves 1-3 assemble L^-1 beside it,
+  // block by block as its inputs appear, so that after block 3's factor only
+  // X_3p = -X_33 T_3p is left (one 16x16 product per wave):
+  //   X_ip = -X_ii T_ip,  T_ip = sum_{k=p}^{i-1} L_ik X_kp  (k ascending: the
+  //   same sums in the same order as the level-by-level form, bit-identical).
+  const d4 z = d4{0.0, 0.0, 0.0, 0.0};
+  auto T_of = [&](int i, int p, int k_end) {  // sum_{k=p}^{k_end-1} L_ik X_kp
+    d4 acc = z;
+    for (int k = p; k < k_end; ++k)
+      acc = mm16_xy(M + (16 * i) * kMS + 16 * k, kMS, Xb + blk_id(k, p) * 16 * kBS17, kBS17, acc, false);
+    return acc;
+  };
+  auto X_from = [&](int i, int p, d4 T) {  // X_ip = -X_ii T (T through this wave's Tb block)
+    double* Tw = Tb + (w - 1) * 16 * kBS17;
+    st16(Tw, kBS17, T);
+    wave_lds_fence();
+    st16(Xb + blk_id(i, p) * 16 * kBS17, kBS17, mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, Tw, kBS17, z, true));
+    wave_lds_fence();
+  };
+  d4 T3 = z;
 #pragma unroll 1
-  for (int p = 0; p < 2; ++p) {
-    if (w == 0) blk_factor_w0(M, Xb, p, ok);
+  for (int p = 0; p < 4; ++p) {
+    if (w == 0) {
+      if (p == 3) {  // the last panel and trailing blocks, then block 3's factor
+        double* A32 = M + 48 * kMS + 32;
+        st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
+        wave_lds_fence();
+        FAC_T(8);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (l == 0) __hip_atomic_store(lflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        double* A33 = M + 48 * kMS + 48;
+        st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
+        wave_lds_fence();
+        FAC_T(9);
+      }
+      blk_factor_w0(M, Xb, p, ok);
+    } else if (p == 2) {
+      if (w == 1) X_from(1, 0, T_of(1, 0, 1));  // X_10 (X_00, X_11, L_10 final after block column 1)
+    } else if (p == 3) {
+      if (w == 1) X_from(2, 1, T_of(2, 1, 2));  // X_21
+      if (w == 2) X_from(2, 0, T_of(2, 0, 2));  // X_20 (needs X_10: published by the barrier)
+      // T_3p needs L_32 (wave 0's panel block above)
+      while (__hip_atomic_load(lflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      // wave 1: T_31, wave 2: T_30, wave 3: T_32 (each wave reads only the X
+      // blocks it formed itself or that the barrier published)
+      T3 = T_of(3, w == 1 ? 1 : (w == 2 ? 0 : 2), 3);
+    }
+    if (p == 2) {
+      __syncthreads();  // X_22 (and X_10) published
+      FAC_T(7);
+    }
+    if (p >= 2) continue;  // (uniform)
     __syncthreads();
     FAC_T(1 + 3 * p);
     // panel: L_ip = A_ip X_pp^T (one block per wave)
     const int ip = p + 1 + w;
     if (ip < 4) {
       double* Aip = M + (16 * ip) * kMS + 16 * p;
-      const d4 z = d4{0.0, 0.0, 0.0, 0.0};
       const d4 acc = mm16_xyT(Aip, kMS, Xb + blk_id(p, p) * 16 * kBS17, kBS17, z, false);
       st16(Aip, kMS, acc);
     }
@@ -2065,61 +2120,9 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     __syncthreads();
     FAC_T(3 + 3 * p);
   }
-  // Block columns 2 and 3 are wave 0's chain alone (block 2's factor, the last
-  // panel block L_32 and trailing block A_33, block 3's factor: no workgroup
-  // barrier on it).  Waves 1-3 assemble L^-1 beside it, block by block as its
-  // inputs appear, so that after block 3's factor only X_3p = -X_33 T_3p is
-  // left (one 16x16 product per wave):
-  //   X_ip = -X_ii T_ip,  T_ip = sum_{k=p}^{i-1} L_ik X_kp  (k ascending: the
-  //   same sums in the same order as the level-by-level form, bit-identical).
-  const d4 z = d4{0.0, 0.0, 0.0, 0.0};
-  auto T_of = [&](int i, int p, int k_end) {  // sum_{k=p}^{k_end-1} L_ik X_kp
-    d4 acc = z;
-    for (int k = p; k < k_end; ++k)
-      acc = mm16_xy(M + (16 * i) * kMS + 16 * k, kMS, Xb + blk_id(k, p) * 16 * kBS17, kBS17, acc, false);
-    return acc;
-  };
-  auto X_from = [&](int i, int p, d4 T) {  // X_ip = -X_ii T (T through this wave's Tb block)
-    double* Tw = Tb + (w - 1) * 16 * kBS17;
-    st16(Tw, kBS17, T);
-    wave_lds_fence();
-    st16(Xb + blk_id(i, p) * 16 * kBS17, kBS17, mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, Tw, kBS17, z, true));
-    wave_lds_fence();
-  };
-  if (w == 0) {
-    blk_factor_w0(M, Xb, 2, ok);
-  } else if (w == 1) {
-    X_from(1, 0, T_of(1, 0, 1));  // X_10 (X_00, X_11, L_10 final after block column 1)
-  }
-  __syncthreads();  // X_22 (and X_10) published
-  FAC_T(7);
-  d4 T3 = z;
-  if (w == 0) {
-    double* A32 = M + 48 * kMS + 32;
-    st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
-    wave_lds_fence();
-    FAC_T(8);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (l == 0) __hip_atomic_store(lflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    double* A33 = M + 48 * kMS + 48;
-    st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
-    wave_lds_fence();
-    FAC_T(9);
-    blk_factor_w0(M, Xb, 3, ok);
-    FAC_T(10);
-    FAC_T(11);
-    FAC_T(12);
-  } else {
-    if (w == 1) X_from(2, 1, T_of(2, 1, 2));  // X_21
-    if (w == 2) X_from(2, 0, T_of(2, 0, 2));  // X_20 (needs X_10: published by the barrier)
-    // T_3p needs L_32 (wave 0's panel block above)
-    while (__hip_atomic_load(lflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-      __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // wave 1: T_31, wave 2: T_30, wave 3: T_32 (each wave reads only the X
-    // blocks it formed itself or that the barrier published)
-    T3 = T_of(3, w == 1 ? 1 : (w == 2 ? 0 : 2), 3);
-  }
+  FAC_T(10);
+  FAC_T(11);
+  FAC_T(12);
   __syncthreads();  // X_33 published
   if (w > 0) X_from(3, w == 1 ? 1 : (w == 2 ? 0 : 2), T3);
   TL_STAMP(2);
@@ -2653,11 +2656,24 @@ void k_tl3_flow(slam_ba_problem p) {
         air[q][4 * s2 + r] = A[(size_t)(I * kTB + row) * L.N + J * kTB + col];
       }
   }
-  // (1) diagonal tile: L_Jk operands double-buffered (Xf / VX[4096:]) so the
-  // next tile's loads are in flight while the current one's MFMAs run
+  // (1) diagonal tile, child tiles k in rs order: L_Jk operands double-buffered
+  // (Xf / VX[4096:]); the next child's tile is fetched before this one's MFMAs
+  // when its flag is already up (loads in flight under the MFMAs), after them
+  // otherwise (a child that is not ready yet never holds up the MFMAs of the
+  // ones that are).  Row tiles 0 and 1 take their updates sum_k L_Ik L_Jk^T
+  // here too, child by child as it arrives (L_Ik staged in VR, free until the
+  // factor), for every child but the last: the last child's row tiles are
+  // published after its L_Jk, so they are folded in after the factor (2).
+  // The sums run over k in the same order as before: bit-identical.
   d4 acc[4];
 #pragma unroll
   for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+  d4 racc[2][4];
+#pragma unroll
+  for (int q2 = 0; q2 < 2; ++q2)
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) racc[q2][s2] = d4{0.0, 0.0, 0.0, 0.0};
+  int rptr[2] = {0, 0};  // next entry of row tile q2's k list (uniform)
   if (sc > 0) {
     ok = flow_wait(F.tile + J * T + S[so], epoch, fail, &shf);
     if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so] * kTB, L.N, Xf);
@@ -2665,10 +2681,15 @@ void k_tl3_flow(slam_ba_problem p) {
   for (int q = 0; q < sc && ok; ++q) {
     double* cur = (q & 1) ? Yf : Xf;
     double* nxt = (q & 1) ? Xf : Yf;
+    const int k = S[so + q];
     __syncthreads();  // cur filled; the previous MFMAs' reads of nxt done
+    bool pre = false;
     if (q + 1 < sc) {
-      ok = flow_wait(F.tile + J * T + S[so + q + 1], epoch, fail, &shf);
-      if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
+      if (t == 0) shf = ld_flag(F.tile + J * T + S[so + q + 1]) == epoch ? 1 : 0;
+      __syncthreads();
+      pre = shf != 0;
+      __syncthreads();
+      if (pre) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
     }
 #pragma unroll 4
     for (int kk = 0; kk < 16; ++kk)
@@ -2676,6 +2697,26 @@ void k_tl3_flow(slam_ba_problem p) {
       for (int b = 0; b < 3; ++b)
         acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[((dR[b] * 16 + kk) << 6) + lane],
                                                       cur[((dC[b] * 16 + kk) << 6) + lane], acc[b], 0, 0, 0);
+    if (q + 1 < sc) {
+#pragma unroll
+      for (int q2 = 0; q2 < 2; ++q2) {
+        if (q2 >= rc) break;
+        const int ko = S[uo + 2 * q2], kc = S[uo + 2 * q2 + 1];
+        if (rptr[q2] >= kc || S[ko + rptr[q2]] != k) continue;  // (uniform)
+        ++rptr[q2];
+        const int I = S[ro + q2];
+        ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);
+        if (!ok) break;
+        tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, VR);
+        __syncthreads();  // VR filled
+        gemm_xyT_acc(VR, cur, racc[q2]);
+        __syncthreads();  // VR reads done
+      }
+      if (ok && !pre) {
+        ok = flow_wait(F.tile + J * T + S[so + q + 1], epoch, fail, &shf);
+        if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
+      }
+    }
   }
   __syncthreads();
   FLOW_T(1);
@@ -2717,9 +2758,10 @@ void k_tl3_flow(slam_ba_problem p) {
   for (int q = 0; q < rc && ok; ++q) {
     const int I = S[ro + q];
     const int ko = S[uo + 2 * q], kc = S[uo + 2 * q + 1];
+    // rows 0 and 1: the children folded in during (1), the rest from here
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
-    for (int u = 0; u < kc && ok; ++u) {
+    for (int s2 = 0; s2 < 4; ++s2) acc[s2] = q == 0 ? racc[0][s2] : (q == 1 ? racc[1][s2] : d4{0.0, 0.0, 0.0, 0.0});
+    for (int u = q < 2 ? rptr[q] : 0; u < kc && ok; ++u) {
       const int k = S[ko + u];
       ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);  // (J, k) was waited for in (1)
       if (!ok) break;
