@@ -408,6 +408,17 @@ def run_tracking(args, world, rank):
         ev.record(s)
         return ev
 
+    # the tracked leg (beside `value`, never it): local-BA windows formed from
+    # the frames this bench tracks -- per step, every `ba_every` tracked pairs
+    # mapped on the device (WindowMapper: k_rel_to_abs + one device map per
+    # window), copied to pinned host memory, and one step later turned into BA
+    # problems on the host (native planner, thread pool) and advanced
+    # `ba_iters` LM iterations on the BA stream (lag-1 pipeline: the host build
+    # of step k-1's windows overlaps step k's tracking on the GPU)
+    leg = {"tracked": False}
+    tleg = {"wms": None, "pool": None, "build_s": [], "shapes": [], "modes": {}, "sets": [],
+            "up": None}
+
     ba_done = [None]
     step_no, pending = [0], [0]
     flush_at = {args.warmup, args.warmup + args.steps}  # step numbers that flush a launch set
@@ -415,6 +426,57 @@ def run_tracking(args, world, rank):
     def step(marks):
         with torch.cuda.stream(tstream):
             tracked_step(marks)
+
+    def tracked_ba(marks, tmarks, h0):
+        """BA of the previous step's tracked windows (lag 1), on the BA stream."""
+        from slam355.ba import BABatch, BAProblem
+
+        prev = tleg["wms"][(step_no[0] - 1) % 2]
+        if not prev.filled:
+            if marks is not None:
+                marks["track"] = tmarks
+            return
+        hb = time.perf_counter()
+        prev.event.synchronize()  # step k-1's maps are on the host (step k is queued behind)
+        pool = tleg["pool"]
+        probs = prev.problems(rig.P_l)
+        prev.filled = False
+
+        def mk(pr):
+            # uploads on an idle stream (a pageable copy on the BA stream would
+            # block this thread until the BA work queued there has drained); the
+            # BA stream waits for them (BAProblem with stream=...)
+            with torch.cuda.stream(tleg["up"]):
+                return BAProblem(*pr, stream=ba_stream)
+
+        bps = list(pool.map(mk, probs))
+        groups = {}
+        for bp in bps:
+            groups.setdefault(bp.lin_mode, []).append(bp)
+        tleg["build_s"].append(time.perf_counter() - hb)
+        tleg["shapes"].append([(len(pr[0]), len(pr[1]), len(pr[2])) for pr in probs])
+        for mode, g in groups.items():
+            tleg["modes"][mode] = tleg["modes"].get(mode, 0) + len(g)
+        h0 = trk._ht("ba_window_build", hb)
+        bmarks = [("ba_start", ev_on(ba_stream))] if marks is not None else None
+        with torch.cuda.stream(ba_stream):
+            for g in groups.values():
+                for i in range(0, len(g), BABatch.MAX_BATCH):
+                    BABatch(g[i:i + BABatch.MAX_BATCH], stream=ba_stream).iterate(args.ba_iters)
+        # the sets' device memory was allocated on the upload stream and is read on
+        # the BA stream: a set is released only once the BA stream has finished it
+        done = torch.cuda.Event()
+        done.record(ba_stream)
+        tleg["sets"].append((bps, done))
+        while len(tleg["sets"]) > 2:
+            tleg["sets"][0][1].synchronize()  # (finished long ago: two steps back)
+            tleg["sets"].pop(0)
+        tleg["last"] = bps
+        if bmarks is not None:
+            bmarks.append(("local_ba", ev_on(ba_stream)))
+            marks["ba"] = bmarks
+            marks["track"] = tmarks
+        trk._ht("ba_launch", h0)
 
     def tracked_step(marks):
         tmarks = [] if marks is not None else None
@@ -433,7 +495,12 @@ def run_tracking(args, world, rank):
             h0 = trk._ht("reset_chain", h0)
         if args.ba_overlap == "after-orb" and ba_done[0] is not None:
             ist.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
+        if leg["tracked"]:
+            wm = tleg["wms"][step_no[0] % 2]
+            wm.save_pose0(tstream)
         trk.track(f0s[win], imgs=imgs, marks=tmarks, chain=gchain is None)
+        if leg["tracked"]:
+            wm.map_batch(tstream)
         h0 = time.perf_counter()
         if gchain is not None:
             gchain.step(trk.rvec, trk.tvec, trk.p_ninl, tstream)
@@ -443,6 +510,10 @@ def run_tracking(args, world, rank):
             marks["orb"] = trk.orb_marks  # ORB's own stream: start -> done there
         if marks is None and args.keep_poses:
             all_poses[win] = trk.poses.clone()
+        if leg["tracked"]:
+            tracked_ba(marks, tmarks, h0)
+            step_no[0] += 1
+            return
         step_no[0] += 1
         pending[0] += 1
         k = step_no[0]
@@ -504,6 +575,40 @@ def run_tracking(args, world, rank):
                 "note": "frames streamed from pinned host memory inside the timed region "
                         "(copy stream, two device slots); not the headline"}
         feeds[0] = feed
+    tracked = None
+    if not args.no_tracked_leg and world == 1 and B % args.ba_every == 0:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from slam355.pipeline import WindowMapper
+
+        tleg["wms"] = [WindowMapper(trk, args.ba_every) for _ in range(2)]
+        tleg["pool"] = ThreadPoolExecutor(max_workers=8)
+        tleg["up"] = torch.cuda.Stream()
+        leg["tracked"] = True
+        feeds[0] = feed
+        feed.prime()
+        trk.host_times = None
+        dt_t, st_t = timed_loop(step, args.steps, args.warmup, world, dict_marks=True)
+        leg["tracked"] = False
+        shp = np.array([x for s_ in tleg["shapes"][-args.steps:] for x in s_], float)
+        last = tleg.get("last") or []
+        sts = [bp.state() for bp in last]
+        tracked = {"frames_per_s": float(B * args.steps) / dt_t, "ms_per_step": dt_t / args.steps * 1e3,
+                   "host_issue_ms_per_step": timed_loop.host_s / args.steps * 1e3,
+                   "host_issue_sites": host_site_summary(trk, args.steps),
+                   "windows_per_step": B // args.ba_every, "pairs_per_window": args.ba_every,
+                   "lm_iters": args.ba_iters,
+                   "window_cams_pts_obs_mean": shp.mean(0).tolist() if len(shp) else None,
+                   "window_pts_obs_max": shp.max(0)[1:].tolist() if len(shp) else None,
+                   "host_build_ms_per_step": float(np.mean(tleg["build_s"][-args.steps:])) * 1e3,
+                   "lin_modes": tleg["modes"], "local_ba_ms_per_step": st_t.get("local_ba"),
+                   "last_set_cost_mean": float(np.mean([s_["COST"] for s_ in sts])) if sts else None,
+                   "last_set_accepted_mean": float(np.mean([s_["NACCEPT"] for s_ in sts])) if sts else None,
+                   "note": ("local BA on windows built from the bench's own tracked frames (lag 1: "
+                            "host build of step k-1's windows overlaps step k's tracking); not the headline")}
+        tleg["pool"].shutdown()
+        torch.cuda.synchronize()
+        tleg["wms"], tleg["sets"], tleg["last"] = None, [], None
     frames = reduce_scalar(float(B * args.steps), world, "sum")
     cnt = trk.counters()  # raises on any ORB workspace overflow since the start
     # accuracy of the tracked trajectory (the last tracked window; the device
@@ -630,6 +735,8 @@ def run_tracking(args, world, rank):
     }
     if pcie is not None:
         rec["pcie_inclusive"] = pcie
+    if tracked is not None:
+        rec["tracked_source"] = tracked
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, windows[0],
                                                     pairs=CPU_PAIRS, lm_iters=CPU_PAIRS)
@@ -1185,6 +1292,8 @@ def main():
     ap.add_argument("--no-pcie-leg", action="store_true",
                     help="tracking: skip the PCIe-inclusive run (frames streamed from pinned host "
                          "memory inside the timed region) reported beside the headline")
+    ap.add_argument("--no-tracked-leg", action="store_true",
+                    help="skip the tracked-source leg (local BA on windows built from the tracked frames)")
     ap.add_argument("--no-tracked-ba", action="store_true",
                     help="tracking: skip the local BA of a window built from tracked frames")
     ap.add_argument("--ba-cus", type=int, default=0,

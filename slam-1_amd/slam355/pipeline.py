@@ -319,3 +319,94 @@ class LocalMap:
 
         return problem_from_map(self.optimization_matrix(), self.poses,
                                 self.store.points().cpu().numpy(), P_left)
+
+
+class WindowMapper:
+    """The local maps of a tracked batch's windows on the device, for local BA
+    on tracked data at throughput (bench.py's tracked leg): main.py:120-127 per
+    window of `n` consecutive frame pairs of one Tracker batch.
+
+    `map_batch(stream)` (after Tracker.track on `stream`): the batch's temporal
+    3-D points to the world frame (one k_rel_to_abs launch, the NEW pose as in
+    LocalMap), then, window by window, a fresh device map fed the window's pairs
+    in order (appendKeyPoints, MapStore: frame index = the pair's index inside
+    the window), and one device -> pinned-host copy of the rows, counts, poses
+    and maps, recorded by `event`.  `problems(P_left)` (host, once the event
+    has fired) forms each window's BA problem as XXXport_files.problem_from_map
+    does: cameras = the window's first n frames (rotation vector, t, f, 0, 0),
+    points = its map, one observation per row.  Call `save_pose0(stream)`
+    before Tracker.track so the window at the batch start has its first frame's
+    pose (the chain state before the batch)."""
+
+    def __init__(self, tracker: Tracker, n: int, threshold=0.01):
+        from .mapping import MapStore
+
+        self.trk, self.n = tracker, int(n)
+        B, cap, d = tracker.B, tracker.cap, tracker.dev
+        if self.n < 1 or B % self.n:
+            raise ValueError(f"window of {n} pairs must divide the batch of {B}")
+        self.n_win = B // self.n
+        self.threshold = float(threshold)
+        self.stores = [MapStore(capacity=self.n * cap, max_queries=cap) for _ in range(self.n_win)]
+        f64 = dict(dtype=torch.float64, device=d)
+        self.abs = torch.zeros((B, cap, 3), **f64)
+        self.rows = torch.zeros((B, cap, 4), **f64)
+        self.pose0 = torch.eye(4, **f64)
+        pin = dict(pin_memory=True)
+        self.h_rows = torch.zeros((B, cap, 4), dtype=torch.float64, **pin)
+        self.h_cnt = torch.zeros((B,), dtype=torch.int32, **pin)
+        self.h_poses = torch.zeros((B, 4, 4), dtype=torch.float64, **pin)
+        self.h_pose0 = torch.zeros((4, 4), dtype=torch.float64, **pin)
+        self.h_maps = torch.zeros((self.n_win, self.n * cap, 3), dtype=torch.float64, **pin)
+        self.h_M = torch.zeros((self.n_win,), dtype=torch.int32, **pin)
+        self.d_M = torch.zeros((self.n_win,), dtype=torch.int32, device=d)
+        self.event = torch.cuda.Event()
+        self.filled = False
+
+    def save_pose0(self, stream):
+        with torch.cuda.stream(stream):
+            self.pose0.copy_(self.trk.chain_state[:16].view(4, 4), non_blocking=True)
+
+    def map_batch(self, stream):
+        t = self.trk
+        with torch.cuda.stream(stream):
+            _lib.call("slam_rel_to_abs", ptr(t.Q1), ptr(t.t_cnt), t.cap, t.B, ptr(t.poses),
+                      ptr(self.abs), stream_ptr(stream))
+            for w, st in enumerate(self.stores):
+                st.M.zero_()
+                st.m_bound = 0
+                for b in range(w * self.n, (w + 1) * self.n):
+                    st.append(self.abs[b], t.Q1[b], t.q1[b], b - w * self.n, self.threshold,
+                              count=t.t_cnt[b:b + 1], rows=self.rows[b], stream=stream)
+                self.d_M[w:w + 1].copy_(st.M)
+                self.h_maps[w].copy_(st.map[: self.n * t.cap], non_blocking=True)
+            self.h_rows.copy_(self.rows, non_blocking=True)
+            self.h_cnt.copy_(t.t_cnt, non_blocking=True)
+            self.h_poses.copy_(t.poses, non_blocking=True)
+            self.h_pose0.copy_(self.pose0, non_blocking=True)
+            self.h_M.copy_(self.d_M, non_blocking=True)
+            self.event.record(stream)
+        self.filled = True
+
+    def problems(self, P_left):
+        """Every window's (cams [n,9], pts [M,3], cam_idx, pt_idx, qs [O,2]) from
+        the host copy (call after event.synchronize()); the camera parameters of
+        the batch's frames in one make_cam_params call."""
+        from .XXXport_files import U_OFF, V_OFF, make_cam_params
+
+        n = self.n
+        cnt = self.h_cnt.numpy()
+        rows = self.h_rows.numpy()
+        poses = self.h_poses.numpy()
+        # frame b of the batch = pose before pair b (window w: frames w n .. w n + n - 1)
+        frames = np.concatenate([self.h_pose0.numpy()[None], poses[:-1]])
+        allcams = make_cam_params(frames, P_left).reshape(-1, 9)
+        out = []
+        for w in range(self.n_win):
+            b0 = w * n
+            om = np.concatenate([rows[b, :max(int(cnt[b]), 0)] for b in range(b0, b0 + n)])
+            pts = self.h_maps[w, :int(self.h_M[w])].numpy().copy()
+            qs = np.stack([om[:, 2] - U_OFF, om[:, 3] - V_OFF], 1)
+            out.append((allcams[b0:b0 + n].copy(), pts, om[:, 0].astype(np.int64),
+                        om[:, 1].astype(np.int64), qs))
+        return out
