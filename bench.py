@@ -412,12 +412,12 @@ def run_tracking(args, world, rank):
     # the frames this bench tracks -- per step, every `ba_every` tracked pairs
     # mapped on the device (WindowMapper: k_rel_to_abs + one device map per
     # window), copied to pinned host memory, and one step later turned into BA
-    # problems on the host (native planner, thread pool) and advanced
-    # `ba_iters` LM iterations on the BA stream (lag-1 pipeline: the host build
-    # of step k-1's windows overlaps step k's tracking on the GPU)
+    # problems on the host (native planner, one staged upload) and advanced
+    # `ba_iters` LM iterations on the BA stream (lag-2 pipeline: the host build
+    # of step k-2's windows overlaps step k's tracking on the GPU, and their
+    # maps' copy to the host has completed while step k-1 ran)
     leg = {"tracked": False}
-    tleg = {"wms": None, "pool": None, "build_s": [], "shapes": [], "modes": {}, "sets": [],
-            "up": None}
+    tleg = {"wms": None, "ws": None, "build_s": [], "shapes": [], "modes": {}, "sets": []}
 
     ba_done = [None]
     step_no, pending = [0], [0]
@@ -428,28 +428,23 @@ def run_tracking(args, world, rank):
             tracked_step(marks)
 
     def tracked_ba(marks, tmarks, h0):
-        """BA of the previous step's tracked windows (lag 1), on the BA stream."""
-        from slam355.ba import BABatch, BAProblem
+        """BA of the tracked windows of two steps back (lag 2), on the BA stream."""
+        from slam355.ba import BABatch
 
-        prev = tleg["wms"][(step_no[0] - 1) % 2]
+        # lag 2: step k-2's maps (its copy event has fired while step k-1 ran)
+        prev = tleg["wms"][(step_no[0] - 2) % len(tleg["wms"])]
         if not prev.filled:
             if marks is not None:
                 marks["track"] = tmarks
             return
         hb = time.perf_counter()
         prev.event.synchronize()  # step k-1's maps are on the host (step k is queued behind)
-        pool = tleg["pool"]
         probs = prev.problems(rig.P_l)
         prev.filled = False
 
-        def mk(pr):
-            # uploads on an idle stream (a pageable copy on the BA stream would
-            # block this thread until the BA work queued there has drained); the
-            # BA stream waits for them (BAProblem with stream=...)
-            with torch.cuda.stream(tleg["up"]):
-                return BAProblem(*pr, stream=ba_stream)
-
-        bps = list(pool.map(mk, probs))
+        # every window planned natively, staged in one pinned buffer, uploaded by
+        # one asynchronous copy on the BA stream (slam355.ba.BAWindowSet)
+        bps = tleg["ws"].build(probs, ba_stream)
         groups = {}
         for bp in bps:
             groups.setdefault(bp.lin_mode, []).append(bp)
@@ -496,7 +491,7 @@ def run_tracking(args, world, rank):
         if args.ba_overlap == "after-orb" and ba_done[0] is not None:
             ist.wait_event(ba_done[0])  # ORB never shares the chip with the BA chain
         if leg["tracked"]:
-            wm = tleg["wms"][step_no[0] % 2]
+            wm = tleg["wms"][step_no[0] % len(tleg["wms"])]
             wm.save_pose0(tstream)
         trk.track(f0s[win], imgs=imgs, marks=tmarks, chain=gchain is None)
         if leg["tracked"]:
@@ -577,13 +572,12 @@ def run_tracking(args, world, rank):
         feeds[0] = feed
     tracked = None
     if not args.no_tracked_leg and world == 1 and B % args.ba_every == 0:
-        from concurrent.futures import ThreadPoolExecutor
-
         from slam355.pipeline import WindowMapper
 
-        tleg["wms"] = [WindowMapper(trk, args.ba_every) for _ in range(2)]
-        tleg["pool"] = ThreadPoolExecutor(max_workers=8)
-        tleg["up"] = torch.cuda.Stream()
+        tleg["wms"] = [WindowMapper(trk, args.ba_every) for _ in range(3)]
+        from slam355.ba import BAWindowSet
+
+        tleg["ws"] = BAWindowSet()
         leg["tracked"] = True
         feeds[0] = feed
         feed.prime()
@@ -604,9 +598,8 @@ def run_tracking(args, world, rank):
                    "lin_modes": tleg["modes"], "local_ba_ms_per_step": st_t.get("local_ba"),
                    "last_set_cost_mean": float(np.mean([s_["COST"] for s_ in sts])) if sts else None,
                    "last_set_accepted_mean": float(np.mean([s_["NACCEPT"] for s_ in sts])) if sts else None,
-                   "note": ("local BA on windows built from the bench's own tracked frames (lag 1: "
-                            "host build of step k-1's windows overlaps step k's tracking); not the headline")}
-        tleg["pool"].shutdown()
+                   "note": ("local BA on windows built from the bench's own tracked frames (lag 2: "
+                            "host build of step k-2's windows overlaps step k's tracking); not the headline")}
         torch.cuda.synchronize()
         tleg["wms"], tleg["sets"], tleg["last"] = None, [], None
     frames = reduce_scalar(float(B * args.steps), world, "sum")

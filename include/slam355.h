@@ -221,6 +221,18 @@ int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int M_bound,
                        const double* d_abs, const double* d_rel, const double* d_pts2d,
                        const int32_t* d_n, int N, double threshold, int frame_index,
                        double* d_rows, void* d_ws, size_t ws_size, void* stream);
+/* The local maps of a tracked batch's windows (main.py:120-127 per window of n
+ * consecutive frame pairs; bench.py's tracked leg): for window w < n_win, map
+ * d_maps[w] ([map_cap][3], map_cap >= n * cap) restarted empty (d_M[w] = 0)
+ * and fed pairs b = w n + j, j < n, in order -- slam_map_associate of
+ * d_abs[b], d_rel[b] ([cap][3]), d_pts2d[b] ([cap][2]), d_count[b] valid
+ * points, frame_index j, rows into d_rows[b] ([cap][4]).  One call for the
+ * whole batch (the same launches as n_win * n slam_map_associate calls);
+ * workspace from slam_map_workspace_bytes(cap, (n - 1) * cap). */
+int slam_map_windows(double* d_maps, int32_t* d_M, int map_cap, int n_win, int n,
+                     const double* d_abs, const double* d_rel, const double* d_pts2d,
+                     const int32_t* d_count, int cap, double threshold, double* d_rows,
+                     void* d_ws, size_t ws_size, void* stream);
 
 /* ------------------------------------------------------------------------
  * Tiled ORB detector + rBRIEF descriptor.

@@ -23,7 +23,7 @@ from slam355.synthetic import ba_problem, ba_problem_loop, perturb  # noqa: E402
 
 name, W, r = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
-cpw = int(sys.argv[5]) if len(sys.argv) > 5 else None
+cpw = (int(sys.argv[5]) or None) if len(sys.argv) > 5 else None
 C, P, gen = (64, 50000, ba_problem) if name == "C4" else (500, 200000, ba_problem_loop)
 rng = np.random.default_rng(7)
 cams, pts, ci, pi, qs = gen(rng, C, P, 6)

@@ -1268,6 +1268,21 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
   const int t = threadIdx.x;
   const bool diag = c1 == c2;
   const int bb = p.blk_bslot_ptr[blk], be = p.blk_bslot_ptr[blk + 1];
+  if (!diag && be == bb) {
+    // a block without partial rows (most listed blocks of a landmark shard:
+    // the global block list, this rank's points): its zeros (-sum of nothing,
+    // bit for bit what the sum path writes) without the row sums' barriers
+    if (t < 81) {
+      if (sys_packed(p.n_cams)) {
+        S[(size_t)blk * 81 + t] = -0.0;
+      } else {
+        const int i = t / 9, j = t - 9 * (t / 9);
+        S[(size_t)(9 * c1 + i) * C9 + 9 * c2 + j] = -0.0;
+        S[(size_t)(9 * c2 + j) * C9 + 9 * c1 + i] = -0.0;
+      }
+    }
+    return;
+  }
   if (diag) rows_sum(p.cpart, kCPart, p.cam_cslot_ptr[c1], p.cam_cslot_ptr[c1 + 1], 109, red, sh);
   if (!diag || be > bb) {
     rows_sum(p.bpart, 81, bb, be, 81, red, sb);

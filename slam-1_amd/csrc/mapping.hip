@@ -179,3 +179,28 @@ extern "C" int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int 
   SLAM_LAUNCHED("k_map_assoc");
   return SLAM_OK;
 }
+
+extern "C" int slam_map_windows(double* d_maps, int32_t* d_M, int map_cap, int n_win, int n,
+                                const double* d_abs, const double* d_rel, const double* d_pts2d,
+                                const int32_t* d_count, int cap, double threshold, double* d_rows,
+                                void* d_ws, size_t ws_size, void* stream) {
+  SLAM_REQUIRE(n_win >= 0 && n >= 1 && cap >= 0 && map_cap >= 0, "slam_map_windows: bad shape");
+  SLAM_REQUIRE((long long)n * cap <= map_cap, "slam_map_windows: map capacity %d < %d pairs x %d",
+               map_cap, n, cap);
+  SLAM_REQUIRE(ws_size >= ws_bytes(cap, (n - 1) * cap), "slam_map_windows: workspace too small");
+  if (n_win == 0 || cap == 0) return SLAM_OK;
+  SLAM_REQUIRE(d_maps && d_M && d_abs && d_rel && d_pts2d && d_count && d_rows && d_ws,
+               "slam_map_windows: null pointer");
+  hipStream_t s = slam::as_stream(stream);
+  SLAM_HIP(hipMemsetAsync(d_M, 0, sizeof(int32_t) * (size_t)n_win, s));
+  for (int w = 0; w < n_win; ++w)
+    for (int j = 0; j < n; ++j) {
+      const size_t b = (size_t)w * n + j;
+      if (int rc = slam_map_associate(d_maps + (size_t)w * map_cap * 3, d_M + w, map_cap, j * cap,
+                                      d_abs + b * cap * 3, d_rel + b * cap * 3, d_pts2d + b * cap * 2,
+                                      d_count + b, cap, threshold, j, d_rows + b * cap * 4, d_ws,
+                                      ws_size, stream))
+        return rc;
+    }
+  return SLAM_OK;
+}

@@ -86,6 +86,8 @@ SIGNATURES = {
     "slam_vo_residuals": [c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_p, c_p, c_p],
     "slam_map_workspace_bytes": [c_int, c_int, ctypes.POINTER(c_size_t)],
     "slam_rel_to_abs": [c_p, c_p, c_int, c_int, c_p, c_p, c_p],
+    "slam_map_windows": [c_p, c_p, c_int, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_double, c_p,
+                         c_p, c_size_t, c_p],
     "slam_map_associate": [c_p, c_p, c_int, c_int, c_p, c_p, c_p, c_p, c_int, c_double, c_int,
                            c_p, c_p, c_size_t, c_p],
     "slam_fundamental_lmeds": [c_p, c_p, c_p, c_int, c_int, c_uint64, c_int, c_int, c_p, c_p, c_p,

@@ -1058,3 +1058,133 @@ def residuals(cams, pts, cam_idx, pt_idx, qs, *, jacobian=False):
     _lib.call("slam_ba_residual", ptr(tc), ptr(tp), ptr(ti), ptr(tj), ptr(tq), O, ptr(r),
               stream_ptr())
     return r.cpu().numpy()
+
+
+class _WindowProblem(BAProblem):
+    """A BAProblem whose buffers are views into a BAWindowSet's shared device
+    memory (built by BAWindowSet.build, not by __init__)."""
+
+    def __init__(self):  # noqa: D107 (constructed by BAWindowSet only)
+        pass
+
+
+class BAWindowSet:
+    """Many small BA problems built together for one launch set -- the local-BA
+    windows formed from tracked frames (bench.py's tracked leg): each window
+    planned by the native planner, every window's tables and float64 data
+    (parameters, observations, zeroed workspaces: BAProblem's layout) staged in
+    ONE pinned host buffer per type and uploaded by ONE asynchronous copy each,
+    on the BA stream, into device buffers kept across calls; the returned
+    problems have BAProblem's interface (state(), params(), BABatch).  Windows
+    that need the slot linearisation (a point seen by more than MF_CAMS
+    cameras) or the tiled solve (9C > 120) are built as ordinary BAProblems.
+
+    The device buffers are reused call after call: a call's upload is ordered on
+    `stream` after the launches of the previous call's problems (same stream),
+    and the host staging buffers alternate between two sets, each reused only
+    after its previous upload has run (an event)."""
+
+    def __init__(self):
+        self.dev = require_gpu()
+        self.d_f64 = self.d_i32 = None
+        self.h = [None, None]  # (f64, i32, event) per staging set
+        self.k = 0
+
+    @staticmethod
+    def _al(n):
+        return (max(int(n), 1) + 31) // 32 * 32
+
+    def build(self, problems, stream, lam0=1e-4):
+        specs, extra = [], []
+        n64 = n32 = 0
+        for w, (cams, pts, ci, pi, qs) in enumerate(problems):
+            cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
+            pts = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+            C, P = len(cams), len(pts)
+            ci, pi, qs = _check_indices(C, P, ci, pi, qs)
+            pl = plan_mfma_native(C, P, ci, pi) if 9 * C <= LDS_MAX_N else None
+            if pl is None:
+                extra.append(BAProblem(cams, pts, ci, pi, qs, lam0=lam0, stream=stream))
+                continue
+            if pl["perm"] is not None:
+                pts = pts[pl["perm"]]
+            O, G = pl["n_obs"], pl["n_grps"]
+            n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])
+            sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
+            up = [("cams0", cams), ("pts0", pts), ("cams1", cams), ("pts1", pts), ("init_c", cams),
+                  ("init_p", pts), ("obs_q", qs[pl["order"]] if O else np.zeros((1, 2)))]
+            zero = [("camrec0", C * 32), ("camrec1", C * 32), ("cpart", n_cs * 112),
+                    ("bpart", n_bs * 81), ("sys", sys_len), ("chol", 1), ("delta_c", 9 * C),
+                    ("red_part", _lib.lib.slam_ba_red_slots(G)), ("small", 4), ("state", N_STATE)]
+            o64 = {}
+            for k, a in up:
+                o64[k] = (n64, np.shape(a))
+                n64 += self._al(np.size(a))
+            for k, n in zero:
+                o64[k] = (n64, (max(int(n), 1),))
+                n64 += self._al(n)
+            o32 = n32
+            n32 += self._al(len(pl["buf"]) + 8)  # plan tables, 4 one-element stand-ins, ticket
+            specs.append((w, C, P, pl, up, o64, o32))
+        # staging (pinned, alternating sets) and device buffers (grown as needed)
+        hs = self.h[self.k & 1]
+        if hs is not None:
+            hs[2].synchronize()  # that set's previous upload has run
+        if hs is None or hs[0].numel() < n64 or hs[1].numel() < n32:
+            hs = [torch.zeros(max(n64, 1) * 3 // 2, dtype=torch.float64, pin_memory=True),
+                  torch.zeros(max(n32, 1) * 3 // 2, dtype=torch.int32, pin_memory=True),
+                  torch.cuda.Event()]
+            self.h[self.k & 1] = hs
+        self.k += 1
+        h64, h32 = hs[0].numpy(), hs[1].numpy()
+        h64[:n64] = 0.0
+        for w, C, P, pl, up, o64, o32 in specs:
+            for k, a in up:
+                h64[o64[k][0]:o64[k][0] + np.size(a)] = np.ravel(a)
+            nb = len(pl["buf"])
+            h32[o32:o32 + nb] = pl["buf"]
+            h32[o32 + nb:o32 + nb + 8] = 0
+        with torch.cuda.stream(stream):
+            if self.d_f64 is None or self.d_f64.numel() < n64:
+                self.d_f64 = torch.empty(max(n64, 1) * 3 // 2, dtype=torch.float64, device=self.dev)
+            if self.d_i32 is None or self.d_i32.numel() < n32:
+                self.d_i32 = torch.empty(max(n32, 1) * 3 // 2, dtype=torch.int32, device=self.dev)
+            self.d_f64[:n64].copy_(hs[0][:n64], non_blocking=True)
+            self.d_i32[:n32].copy_(hs[1][:n32], non_blocking=True)
+            hs[2].record(stream)
+        out = [None] * len(problems)
+        for w, C, P, pl, up, o64, o32 in specs:
+            bp = _WindowProblem()
+            t = {}
+            for k, (o, shp) in o64.items():
+                t[k] = self.d_f64[o:o + int(np.prod(shp))].view(shp)
+            nb = len(pl["buf"])
+            pb = self.d_i32[o32:o32 + nb]
+            t["plan_buf"] = pb
+            for k in _INDEX_TABLES + _MFMA_TABLES:
+                t[k] = pb[pl["offs"][k]:] if k in pl["offs"] else self.d_i32[o32 + nb:o32 + nb + 1]
+            t["ticket"] = self.d_i32[o32 + nb + 4:o32 + nb + 5]
+            bp.plan, bp.lin_mode, bp.perm = pl, "mfma", pl["perm"]
+            bp.C, bp.P, bp.O, bp.stream, bp.t = C, P, pl["n_obs"], stream, t
+            bp.sys_len, bp.tl_levels = int(t["sys"].numel()), False
+            s = _Prob()
+            s.n_cams, s.n_pts, s.n_obs, s.n_grps = C, P, pl["n_obs"], pl["n_grps"]
+            s.n_blocks = len(pl["blocks"])
+            s.n_cslots, s.n_bslots = len(pl["cslot_cam"]), len(pl["bslot_blk"])
+            s.lin_mode, s.n_sgrps, s.tl_mode = 1, pl["n_sgrps"], 0
+            s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
+            s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
+            s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
+            for k in _INDEX_TABLES + ("obs_q", "cpart", "bpart", "sys", "chol", "delta_c",
+                                      "red_part", "small", "state", "ticket") + _MFMA_TABLES:
+                setattr(s, k, t[k].data_ptr())
+            bp._s = s
+            bp._init = (t["init_c"], t["init_p"])
+            out[w] = bp
+        it = iter(extra)
+        out = [p if p is not None else next(it) for p in out]
+        # LM states of the set's problems reset together (the upload runs first: same stream)
+        built = [p for p in out if isinstance(p, _WindowProblem)]
+        for i in range(0, len(built), BABatch.MAX_BATCH):
+            BABatch(built[i:i + BABatch.MAX_BATCH], stream=stream).reset(lam0)
+        return out

@@ -329,9 +329,10 @@ class WindowMapper:
     `map_batch(stream)` (after Tracker.track on `stream`): the batch's temporal
     3-D points to the world frame (one k_rel_to_abs launch, the NEW pose as in
     LocalMap), then, window by window, a fresh device map fed the window's pairs
-    in order (appendKeyPoints, MapStore: frame index = the pair's index inside
-    the window), and one device -> pinned-host copy of the rows, counts, poses
-    and maps, recorded by `event`.  `problems(P_left)` (host, once the event
+    in order (appendKeyPoints as MapStore does, all windows in one
+    slam_map_windows call; frame index = the pair's index inside the window),
+    and one device -> pinned-host copy of the rows, counts, poses and maps,
+    recorded by `event`.  `problems(P_left)` (host, once the event
     has fired) forms each window's BA problem as XXXport_files.problem_from_map
     does: cameras = the window's first n frames (rotation vector, t, f, 0, 0),
     points = its map, one observation per row.  Call `save_pose0(stream)`
@@ -339,7 +340,7 @@ class WindowMapper:
     pose (the chain state before the batch)."""
 
     def __init__(self, tracker: Tracker, n: int, threshold=0.01):
-        from .mapping import MapStore
+        import ctypes
 
         self.trk, self.n = tracker, int(n)
         B, cap, d = tracker.B, tracker.cap, tracker.dev
@@ -347,7 +348,11 @@ class WindowMapper:
             raise ValueError(f"window of {n} pairs must divide the batch of {B}")
         self.n_win = B // self.n
         self.threshold = float(threshold)
-        self.stores = [MapStore(capacity=self.n * cap, max_queries=cap) for _ in range(self.n_win)]
+        self.maps = torch.zeros((self.n_win, self.n * cap, 3), dtype=torch.float64, device=d)
+        self.d_M = torch.zeros((self.n_win,), dtype=torch.int32, device=d)
+        nb = ctypes.c_size_t(0)
+        _lib.call("slam_map_workspace_bytes", cap, (self.n - 1) * cap, ctypes.byref(nb))
+        self.ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=d)
         f64 = dict(dtype=torch.float64, device=d)
         self.abs = torch.zeros((B, cap, 3), **f64)
         self.rows = torch.zeros((B, cap, 4), **f64)
@@ -359,7 +364,6 @@ class WindowMapper:
         self.h_pose0 = torch.zeros((4, 4), dtype=torch.float64, **pin)
         self.h_maps = torch.zeros((self.n_win, self.n * cap, 3), dtype=torch.float64, **pin)
         self.h_M = torch.zeros((self.n_win,), dtype=torch.int32, **pin)
-        self.d_M = torch.zeros((self.n_win,), dtype=torch.int32, device=d)
         self.event = torch.cuda.Event()
         self.filled = False
 
@@ -372,14 +376,12 @@ class WindowMapper:
         with torch.cuda.stream(stream):
             _lib.call("slam_rel_to_abs", ptr(t.Q1), ptr(t.t_cnt), t.cap, t.B, ptr(t.poses),
                       ptr(self.abs), stream_ptr(stream))
-            for w, st in enumerate(self.stores):
-                st.M.zero_()
-                st.m_bound = 0
-                for b in range(w * self.n, (w + 1) * self.n):
-                    st.append(self.abs[b], t.Q1[b], t.q1[b], b - w * self.n, self.threshold,
-                              count=t.t_cnt[b:b + 1], rows=self.rows[b], stream=stream)
-                self.d_M[w:w + 1].copy_(st.M)
-                self.h_maps[w].copy_(st.map[: self.n * t.cap], non_blocking=True)
+            # every window's device map in one call (slam_map_windows: the
+            # appendKeyPoints launches of its pairs, in order, maps restarted empty)
+            _lib.call("slam_map_windows", ptr(self.maps), ptr(self.d_M), self.n * t.cap, self.n_win,
+                      self.n, ptr(self.abs), ptr(t.Q1), ptr(t.q1), ptr(t.t_cnt), t.cap,
+                      self.threshold, ptr(self.rows), ptr(self.ws), self.ws.numel(), stream_ptr(stream))
+            self.h_maps.copy_(self.maps, non_blocking=True)
             self.h_rows.copy_(self.rows, non_blocking=True)
             self.h_cnt.copy_(t.t_cnt, non_blocking=True)
             self.h_poses.copy_(t.poses, non_blocking=True)

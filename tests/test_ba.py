@@ -905,6 +905,42 @@ def test_gpu_batch_folded_assembly_equals_k_assemble(folds):
         assert np.array_equal(x, y)
 
 
+@pytest.mark.gpu
+def test_gpu_window_set_equals_separate_problems():
+    """BAWindowSet (the tracked leg's batched window build: native plans, one
+    staged upload into shared device buffers, one reset launch) gives each
+    window the iterates BAProblem gives it alone, bit for bit, and a second
+    build into the reused buffers repeats them (a window with 9 cameras per
+    point falls back to an ordinary slot-mode BAProblem)."""
+    import torch
+    from slam355 import ba
+    from slam355.synthetic import ba_problem, perturb
+
+    probs = []
+    for w, (C, P, k) in enumerate([(8, 800, 3), (9, 600, 4), (8, 1000, 2), (10, 300, 9)]):
+        rng = np.random.default_rng(60 + w)
+        cams, pts, ci, pi, qs = ba_problem(rng, C, P, k)
+        c0, p0 = perturb(rng, cams, pts)
+        probs.append((c0, p0, ci, pi, qs))
+    s = torch.cuda.Stream()
+    ws = ba.BAWindowSet()
+    runs = []
+    for _ in range(2):
+        got = ws.build(probs, s)
+        assert [p.lin_mode for p in got] == ["mfma", "mfma", "mfma", "slot"]
+        with torch.cuda.stream(s):
+            ba.BABatch(got[:3], stream=s).iterate(4)
+            got[3].iterate(4)
+        torch.cuda.synchronize()
+        runs.append([p.params() for p in got])
+    for w, pr in enumerate(probs):
+        ref = ba.BAProblem(*pr)
+        ref.iterate(4)
+        rc, rp = ref.params()
+        for r in runs:
+            assert np.array_equal(r[w][0], rc) and np.array_equal(r[w][1], rp), w
+
+
 def test_assembly_table_counts_every_partial_row():
     """The folded assembly's table (slam355.ba.assembly_table): every cpart row
     is counted once at its camera's diagonal block, every bpart row once at its

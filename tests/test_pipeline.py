@@ -180,6 +180,47 @@ def corridor9():
 
 
 @pytest.mark.gpu
+def test_gpu_window_mapper_equals_per_frame_maps(corridor9):
+    """WindowMapper (the bench's tracked leg): one slam_map_windows call maps
+    every window of the batch exactly as MapStore.append frame by frame does
+    (rows and map points bit for bit, frame index = pair index in the window);
+    problems() gives each window the export_data / read_bal_data problem of its
+    frames (make_cam_params of the window's first n poses)."""
+    import torch
+    from slam355.mapping import MapStore
+    from slam355.pipeline import Tracker, WindowMapper
+    from slam355.XXXport_files import U_OFF, V_OFF, make_cam_params
+
+    L, R, poses, rig = corridor9
+    B, n = 8, 4
+    trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=6)
+    wm = WindowMapper(trk, n)
+    trk.imgs.copy_(torch.from_numpy(np.concatenate([L[:B + 1], R[:B]])))
+    wm.save_pose0(None)
+    trk.track(0)
+    wm.map_batch(torch.cuda.current_stream())
+    wm.event.synchronize()
+    probs = wm.problems(rig.P_l)
+    assert len(probs) == B // n
+    t_cnt = trk.t_cnt.cpu().numpy()
+    dev_poses = trk.poses.cpu().numpy()
+    for w in range(B // n):
+        st = MapStore(capacity=n * trk.cap, max_queries=trk.cap)
+        rows = []
+        for j in range(n):
+            b = w * n + j
+            r = st.append(wm.abs[b], trk.Q1[b], trk.q1[b], j, 0.01, count=trk.t_cnt[b:b + 1])
+            rows.append(r[: int(t_cnt[b])].cpu().numpy())
+        om = np.vstack(rows)
+        cams, pts, ci, pi, qs = probs[w]
+        assert np.array_equal(pts, st.points().cpu().numpy())
+        assert np.array_equal(ci, om[:, 0].astype(np.int64)) and np.array_equal(pi, om[:, 1].astype(np.int64))
+        assert np.array_equal(qs, np.stack([om[:, 2] - U_OFF, om[:, 3] - V_OFF], 1))
+        frames = [np.eye(4) if w == 0 else dev_poses[w * n - 1]] + [dev_poses[w * n + j] for j in range(n - 1)]
+        assert np.array_equal(cams, make_cam_params(frames, rig.P_l).reshape(-1, 9))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("B", [3, 8])
 def test_gpu_tracked_frames_feed_local_ba(request, B):
     """tracking and local BA as one pipeline.  B tracked pairs
