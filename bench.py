@@ -1232,7 +1232,7 @@ def main():
                     help="camera-union linearisation: chunks per workgroup (default: 8 for the "
                          "tracking workload's batched windows -- 3 / 4 / 5 / 6 / 8 / 12 / 16 "
                          "measured 20.2k / 20.4k / 20.5k / 20.5k / 20.6k / 20.6k / 20.5k "
-                         "frames/s, profiles/r4/orbcus_sweep/; auto elsewhere)")
+                         "frames/s, round-4 sweep in git history at f26058c; auto elsewhere)")
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
@@ -1272,7 +1272,7 @@ def main():
                     help="ORB pipeline: ORB's stream may use only the first N CUs (0: all, the "
                          "default since the camera solve fits two waves per SIMD: alternating "
                          "runs 224 / 232 / 240 / 248 / all -> 19.7-19.8k / 19.9-20.1k / "
-                         "20.1-20.2k / 20.3k / 20.5k frames/s, profiles/r4/orbcus_sweep/; with "
+                         "20.1-20.2k / 20.3k / 20.5k frames/s, round-4 sweep in git history at f26058c; with "
                          "the 317-register solve round 3 measured 224 best)")
     ap.add_argument("--solve-lds-floor", type=int, default=0,
                     help="LDS bytes the one-workgroup camera solve requests at least "

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-4 evidence set: GPU tests + smoke, the driver's bench command x3,
+# Evidence set of a round: GPU tests + smoke, the driver's bench command x3,
 # C4 / C5 / batched-BA / matcher lines, then the profile passes of the default
 # bench (kernel stats, FETCH_SIZE / WRITE_SIZE, two SQ passes).  Each GPU step
 # has its own time limit; the steps are chained with && (a failure ends the call).
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOT"
-TAG=${1:-r4_final}
+TAG=${1:-r5_final}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 timeout -k 10 700 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
@@ -26,5 +26,5 @@ import json
 for f in ('ba_c4','ba_c5','ba_b16','ba_c3','matcher_b32'):
     d=json.load(open('$OUT/'+f+'.json')); print(f, round(d['value'],1), d['unit'], round(d['ms_per_step']*1e3,1))
 "
-bash scripts/gpu_profile.sh $TAG --no-pcie-leg --no-tracked-ba || exit 1
+bash scripts/gpu_profile.sh $TAG --no-pcie-leg --no-tracked-ba --no-tracked-leg || exit 1
 echo done
