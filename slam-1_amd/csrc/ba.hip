@@ -1501,6 +1501,71 @@ __device__ unsigned long long g_solve_trace[20][6];
 #define SOLVE_TR(step, i) (void)0
 #endif
 
+// k_solve_blk's panel pivots, the same fused form (9-wide panels):
+// u[i] += bcast_i(uj) * nl for i = J+2..8 (column J's updates after the next
+// pivot's entry, which stays in compiler code)
+template <int J> struct PanelRest;
+static_assert(kPanelW == 9, "PanelRest is written for 9-wide panels");
+template <> struct PanelRest<0> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %7, %8 row_newbcast:2 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %7, %8 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %7, %8 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %7, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %7, %8 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %7, %8 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %7, %8 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<1> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %6, %7 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %6, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %6, %7 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %6, %7 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %6, %7 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %6, %7 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<2> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %5, %6 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %5, %6 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %5, %6 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %5, %6 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %5, %6 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<3> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %4, %5 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %4, %5 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %4, %5 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %4, %5 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[5]), "+v"(u[6]), "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<4> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %3, %4 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %3, %4 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %3, %4 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[6]), "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<5> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %2, %3 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %2, %3 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[7]), "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<6> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %1, %2 row_newbcast:8 row_mask:0xf bank_mask:0xf\n"
+        : "+v"(u[8])
+        : "v"(uj), "v"(nl));
+  }
+};
+template <> struct PanelRest<7> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    (void)u; (void)uj; (void)nl;
+  }
+};
+template <> struct PanelRest<8> {
+  static __device__ __forceinline__ void run(double (&u)[9], double uj, double nl) {
+    (void)u; (void)uj; (void)nl;
+  }
+};
+
 __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) void k_solve_blk(BaBatch bat) {
   BA_PROB(bat);
   lm_wave_priority();
@@ -1636,10 +1701,8 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
         bad |= !(d > 0.0) || !isfinite(d);
         Dinv[j] = rcp_f64(d);
         const double l = u[j] * Dinv[j];
-        static_for<j + 1, kPanelW>([&](auto I) {
-          constexpr int i = decltype(I)::value;
-          u[i] = __builtin_fma(-l, bcast16<i>(u[j]), u[i]);
-        });
+        if constexpr (j + 1 < kPanelW) u[j + 1] = __builtin_fma(-l, bcast16<j + 1>(u[j]), u[j + 1]);
+        PanelRest<j>::run(u, u[j], -l);
       });
 #ifdef SLAM_SOLVE_PROFILE_PANEL
       {
@@ -1973,6 +2036,238 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Fused broadcast-FMA updates of the 16x16 register factor (v_fmac_f64 with a
+// DPP row_newbcast source: one instruction per update instead of a
+// v_mov_b64_dpp + v_fma_f64 pair -- the compiler does not combine 64-bit DPP
+// moves into VOP2).  FacRest<J>: v[m] += bcast_m(nl) * l for m = J+1..15;
+// InvRest<K>: s[i] += bcast_i(vk) * xk for i = K+1..15.  The leading s_nop 1
+// covers the VALU-write -> DPP-read hazard of the broadcast source; no
+// register these blocks write is read by a DPP (compiler or asm) before
+// compiler code rewrites it.  Bit for bit the products and sums of the
+// two-instruction form.
+template <int J> struct FacRest;
+template <int K> struct InvRest;
+template <> struct FacRest<0> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %15, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %15, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %15, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %15, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %15, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %15, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %15, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %15, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %15, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %15, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %15, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %15, %16 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %15, %16 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %13, %15, %16 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %14, %15, %16 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<1> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %14, %15 row_newbcast:2 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %14, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %14, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %14, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %14, %15 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %14, %15 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %14, %15 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %14, %15 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %14, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %14, %15 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %14, %15 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %14, %15 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %14, %15 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %13, %14, %15 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<2> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %13, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %13, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %13, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %13, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %13, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %13, %14 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %13, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %13, %14 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %13, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %13, %14 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %13, %14 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %13, %14 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %13, %14 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<3> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %12, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %12, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %12, %13 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %12, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %12, %13 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %12, %13 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %12, %13 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %12, %13 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<4> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %11, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %11, %12 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %11, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %11, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %11, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %11, %12 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %11, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %11, %12 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %11, %12 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %11, %12 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %11, %12 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[5]), "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<5> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %10, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %10, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %10, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %10, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %10, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %10, %11 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %10, %11 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %10, %11 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %10, %11 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[6]), "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<6> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %9, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %9, %10 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %9, %10 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %9, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %9, %10 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %9, %10 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %9, %10 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %9, %10 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %9, %10 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<7> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %8, %9 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %8, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %8, %9 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %8, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %8, %9 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %8, %9 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %8, %9 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %8, %9 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<8> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %7, %8 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %7, %8 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %7, %8 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %7, %8 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %7, %8 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %7, %8 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %7, %8 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<9> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %6, %7 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %6, %7 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %6, %7 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %6, %7 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %6, %7 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %6, %7 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<10> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %5, %6 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %5, %6 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %5, %6 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %5, %6 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %5, %6 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<11> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %4, %5 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %4, %5 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %4, %5 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %4, %5 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<12> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %3, %4 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %3, %4 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %3, %4 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<13> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %2, %3 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %2, %3 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[14]), "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<14> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(v[15])
+                 : "v"(nl), "v"(l));
+  }
+};
+template <> struct FacRest<15> {
+  static __device__ __forceinline__ void run(double (&v)[16], double nl, double l) {
+    (void)v; (void)nl; (void)l;
+  }
+};
+template <> struct InvRest<0> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %15, %16 row_newbcast:1 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %15, %16 row_newbcast:2 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %15, %16 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %15, %16 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %15, %16 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %15, %16 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %15, %16 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %15, %16 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %15, %16 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %15, %16 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %15, %16 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %15, %16 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %15, %16 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %13, %15, %16 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %14, %15, %16 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[1]), "+v"(s[2]), "+v"(s[3]), "+v"(s[4]), "+v"(s[5]), "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<1> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %14, %15 row_newbcast:2 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %14, %15 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %14, %15 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %14, %15 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %14, %15 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %14, %15 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %14, %15 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %14, %15 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %14, %15 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %14, %15 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %14, %15 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %14, %15 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %14, %15 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %13, %14, %15 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[2]), "+v"(s[3]), "+v"(s[4]), "+v"(s[5]), "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<2> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %13, %14 row_newbcast:3 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %13, %14 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %13, %14 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %13, %14 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %13, %14 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %13, %14 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %13, %14 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %13, %14 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %13, %14 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %13, %14 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %13, %14 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %13, %14 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %12, %13, %14 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[3]), "+v"(s[4]), "+v"(s[5]), "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<3> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %12, %13 row_newbcast:4 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %12, %13 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %12, %13 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %12, %13 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %12, %13 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %12, %13 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %12, %13 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %12, %13 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %12, %13 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %12, %13 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %12, %13 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %11, %12, %13 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[4]), "+v"(s[5]), "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<4> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %11, %12 row_newbcast:5 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %11, %12 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %11, %12 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %11, %12 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %11, %12 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %11, %12 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %11, %12 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %11, %12 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %11, %12 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %11, %12 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %10, %11, %12 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[5]), "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<5> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %10, %11 row_newbcast:6 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %10, %11 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %10, %11 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %10, %11 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %10, %11 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %10, %11 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %10, %11 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %10, %11 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %10, %11 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %9, %10, %11 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[6]), "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<6> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %9, %10 row_newbcast:7 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %9, %10 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %9, %10 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %9, %10 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %9, %10 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %9, %10 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %9, %10 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %9, %10 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %8, %9, %10 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[7]), "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<7> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %8, %9 row_newbcast:8 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %8, %9 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %8, %9 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %8, %9 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %8, %9 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %8, %9 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %8, %9 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %7, %8, %9 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[8]), "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<8> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %7, %8 row_newbcast:9 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %7, %8 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %7, %8 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %7, %8 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %7, %8 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %7, %8 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %6, %7, %8 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[9]), "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<9> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %6, %7 row_newbcast:10 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %6, %7 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %6, %7 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %6, %7 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %6, %7 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %5, %6, %7 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[10]), "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<10> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %5, %6 row_newbcast:11 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %5, %6 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %5, %6 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %5, %6 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %4, %5, %6 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[11]), "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<11> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %4, %5 row_newbcast:12 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %4, %5 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %4, %5 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %3, %4, %5 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[12]), "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<12> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %3, %4 row_newbcast:13 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %3, %4 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %2, %3, %4 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[13]), "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<13> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %2, %3 row_newbcast:14 row_mask:0xf bank_mask:0xf\n" "v_fmac_f64_dpp %1, %2, %3 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[14]), "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<14> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    asm("s_nop 1\n" "v_fmac_f64_dpp %0, %1, %2 row_newbcast:15 row_mask:0xf bank_mask:0xf\n"
+                 : "+v"(s[15])
+                 : "v"(vk), "v"(xk));
+  }
+};
+template <> struct InvRest<15> {
+  static __device__ __forceinline__ void run(double (&s)[16], double vk, double xk) {
+    (void)s; (void)vk; (void)xk;
+  }
+};
+
 // Wave 0's part of block column p: the 16x16 diagonal block of M factored in
 // registers and inverted (X_pp = L_pp^-1 into Xb); `ok` cleared on a
 // non-positive or non-finite pivot.
@@ -1982,42 +2277,47 @@ __device__ __forceinline__ void blk_factor_w0(double* M, double* Xb, int p, bool
   double v[16], rj[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) v[c] = c <= i ? M[(16 * p + i) * kMS + 16 * p + c] : 0.0;
+  // Pivot chain: d_j -> rsq + 2 Newton steps -> p = v_j r (row i's L_ij for
+  // i > j) -> lane j+1's own update d_{j+1} = v_{j+1} - p^2 -> broadcast.  The
+  // broadcasts of column j to the other rows read p from rows m > j only, so
+  // they need no select; the whole-row update of column j (fused DPP FMAs)
+  // is off the chain.  Same operations as the plain right-looking form.
+  double dn = bcast16<0>(v[0]);
   static_for<0, 16>([&](auto J) {
     constexpr int j = decltype(J)::value;
-    const double djj = bcast16<j>(v[j]);
+    const double djj = dn;
     ok = ok && djj > 0.0 && djj < INFINITY;
     double r = __builtin_amdgcn_rsq(djj);
     const double h = 0.5 * djj;
     r = r * __builtin_fma(-h * r, r, 1.5);
     r = r * __builtin_fma(-h * r, r, 1.5);
     rj[j] = r;
-    const double lij = i > j ? v[j] * r : (i == j ? djj * r : 0.0);
+    const double pj = v[j] * r;
+    if constexpr (j + 1 < 16) dn = bcast16<j + 1>(__builtin_fma(-pj, pj, v[j + 1]));
+    const double lij = i > j ? pj : (i == j ? djj * r : 0.0);
     v[j] = lij;
-    static_for<j + 1, 16>([&](auto Mi) {
-      constexpr int m = decltype(Mi)::value;
-      v[m] = __builtin_fma(-lij, bcast16<m>(lij), v[m]);
-    });
+    FacRest<j>::run(v, -pj, lij);
   });
   // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
   // (column-oriented: once x_k is known, every later row's sum takes its
   // term -- the same k order per sum as the row form, a 16-step chain
-  // instead of 120 dependent FMAs); l_ik = lane ii's v[k], by row_newbcast
+  // instead of 120 dependent FMAs); l_ik = lane ii's v[k], by row_newbcast.
+  // The sum of row c starts at -1 so that x_k = -s_k / l_kk holds for every
+  // k >= c with no select on the chain (x_c = 1 / l_cc exactly; the rows
+  // above c carry signed zeros, written as 0 below)
   const int c = l & 15;
   double x[16], sacc[16];
 #pragma unroll
-  for (int ii = 0; ii < 16; ++ii) sacc[ii] = 0.0;
+  for (int ii = 0; ii < 16; ++ii) sacc[ii] = ii == c ? -1.0 : 0.0;
   static_for<0, 16>([&](auto K) {
     constexpr int k = decltype(K)::value;
-    x[k] = k < c ? 0.0 : (k == c ? rj[k] : -sacc[k] * rj[k]);
-    static_for<k + 1, 16>([&](auto II) {
-      constexpr int ii = decltype(II)::value;
-      sacc[ii] = __builtin_fma(bcast16<ii>(v[k]), x[k], sacc[ii]);
-    });
+    x[k] = -sacc[k] * rj[k];
+    InvRest<k>::run(sacc, v[k], x[k]);
   });
   if (l < 16) {
     double* X = Xb + blk_id(p, p) * 16 * kBS17;
 #pragma unroll
-    for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = x[ii];
+    for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + c] = ii < c ? 0.0 : x[ii];
   }
 }
 
