@@ -411,11 +411,13 @@ def run_tracking(args, world, rank):
     # the tracked leg (beside `value`, never it): local-BA windows formed from
     # the frames this bench tracks -- per step, every `ba_every` tracked pairs
     # mapped on the device (WindowMapper: k_rel_to_abs + one device map per
-    # window), copied to pinned host memory, and one step later turned into BA
-    # problems on the host (native planner, one staged upload) and advanced
+    # window), copied to pinned host memory, and TRK_LAG steps later turned into
+    # BA problems on the host (native planner, one staged upload) and advanced
     # `ba_iters` LM iterations on the BA stream (lag-2 pipeline: the host build
     # of step k-2's windows overlaps step k's tracking on the GPU, and their
-    # maps' copy to the host has completed while step k-1 ran)
+    # maps' copy to the host has completed while step k-1 ran; lag 3 measured
+    # 14.3k vs 15.5-15.7k tracked frames/s, alternating runs, profiles/r5/tracked_leg)
+    TRK_LAG = args.tracked_lag
     leg = {"tracked": False}
     tleg = {"wms": None, "ws": None, "build_s": [], "shapes": [], "modes": {}, "sets": []}
 
@@ -428,17 +430,17 @@ def run_tracking(args, world, rank):
             tracked_step(marks)
 
     def tracked_ba(marks, tmarks, h0):
-        """BA of the tracked windows of two steps back (lag 2), on the BA stream."""
+        """BA of the tracked windows of TRK_LAG steps back, on the BA stream."""
         from slam355.ba import BABatch
 
-        # lag 2: step k-2's maps (its copy event has fired while step k-1 ran)
-        prev = tleg["wms"][(step_no[0] - 2) % len(tleg["wms"])]
+        # step k-TRK_LAG's maps (their copy event has fired while step k-1 ran)
+        prev = tleg["wms"][(step_no[0] - TRK_LAG) % len(tleg["wms"])]
         if not prev.filled:
             if marks is not None:
                 marks["track"] = tmarks
             return
         hb = time.perf_counter()
-        prev.event.synchronize()  # step k-1's maps are on the host (step k is queued behind)
+        prev.event.synchronize()  # step k-lag's maps are on the host
         probs = prev.problems(rig.P_l)
         prev.filled = False
 
@@ -574,7 +576,7 @@ def run_tracking(args, world, rank):
     if not args.no_tracked_leg and world == 1 and B % args.ba_every == 0:
         from slam355.pipeline import WindowMapper
 
-        tleg["wms"] = [WindowMapper(trk, args.ba_every) for _ in range(3)]
+        tleg["wms"] = [WindowMapper(trk, args.ba_every) for _ in range(TRK_LAG + 1)]
         from slam355.ba import BAWindowSet
 
         tleg["ws"] = BAWindowSet()
@@ -1285,6 +1287,8 @@ def main():
     ap.add_argument("--no-pcie-leg", action="store_true",
                     help="tracking: skip the PCIe-inclusive run (frames streamed from pinned host "
                          "memory inside the timed region) reported beside the headline")
+    ap.add_argument("--tracked-lag", type=int, default=2,
+                    help="steps between a batch's tracking and its tracked-window BA (>= 1)")
     ap.add_argument("--no-tracked-leg", action="store_true",
                     help="skip the tracked-source leg (local BA on windows built from the tracked frames)")
     ap.add_argument("--no-tracked-ba", action="store_true",

@@ -1062,10 +1062,31 @@ def residuals(cams, pts, cam_idx, pt_idx, qs, *, jacobian=False):
 
 class _WindowProblem(BAProblem):
     """A BAProblem whose buffers are views into a BAWindowSet's shared device
-    memory (built by BAWindowSet.build, not by __init__)."""
+    memory (built by BAWindowSet.build, not by __init__).  The kernels see raw
+    pointers set at build time; the torch views (`t`, `_init`) that the
+    BAProblem methods read are made on first use only."""
 
     def __init__(self):  # noqa: D107 (constructed by BAWindowSet only)
         pass
+
+    @property
+    def t(self):
+        if self._t is None:
+            d64, d32, o64, o32, nb, offs = self._views
+            t = {}
+            for k, (o, shp) in o64.items():
+                t[k] = d64[o:o + int(np.prod(shp))].view(shp)
+            pb = d32[o32:o32 + nb]
+            t["plan_buf"] = pb
+            for k in _INDEX_TABLES + _MFMA_TABLES:
+                t[k] = pb[offs[k]:] if k in offs else d32[o32 + nb:o32 + nb + 1]
+            t["ticket"] = d32[o32 + nb + 4:o32 + nb + 5]
+            self._t = t
+        return self._t
+
+    @property
+    def _init(self):
+        return (self.t["init_c"], self.t["init_p"])
 
 
 class BAWindowSet:
@@ -1153,33 +1174,34 @@ class BAWindowSet:
             self.d_i32[:n32].copy_(hs[1][:n32], non_blocking=True)
             hs[2].record(stream)
         out = [None] * len(problems)
+        b64, b32 = self.d_f64.data_ptr(), self.d_i32.data_ptr()
         for w, C, P, pl, up, o64, o32 in specs:
+            # raw pointers from the offsets (no torch view per buffer: ~30 per
+            # window were most of the host build); the views are made on demand
             bp = _WindowProblem()
-            t = {}
-            for k, (o, shp) in o64.items():
-                t[k] = self.d_f64[o:o + int(np.prod(shp))].view(shp)
             nb = len(pl["buf"])
-            pb = self.d_i32[o32:o32 + nb]
-            t["plan_buf"] = pb
-            for k in _INDEX_TABLES + _MFMA_TABLES:
-                t[k] = pb[pl["offs"][k]:] if k in pl["offs"] else self.d_i32[o32 + nb:o32 + nb + 1]
-            t["ticket"] = self.d_i32[o32 + nb + 4:o32 + nb + 5]
+            offs = pl["offs"]
+            bp._t = None
+            bp._views = (self.d_f64, self.d_i32, o64, o32, nb, offs)
             bp.plan, bp.lin_mode, bp.perm = pl, "mfma", pl["perm"]
-            bp.C, bp.P, bp.O, bp.stream, bp.t = C, P, pl["n_obs"], stream, t
-            bp.sys_len, bp.tl_levels = int(t["sys"].numel()), False
+            bp.C, bp.P, bp.O, bp.stream = C, P, pl["n_obs"], stream
+            bp.sys_len, bp.tl_levels = int(o64["sys"][1][0]), False
+            f64p = lambda k: b64 + 8 * o64[k][0]  # noqa: E731
+            i32p = lambda k: b32 + 4 * (o32 + (offs[k] if k in offs else nb))  # noqa: E731
             s = _Prob()
             s.n_cams, s.n_pts, s.n_obs, s.n_grps = C, P, pl["n_obs"], pl["n_grps"]
             s.n_blocks = len(pl["blocks"])
             s.n_cslots, s.n_bslots = len(pl["cslot_cam"]), len(pl["bslot_blk"])
             s.lin_mode, s.n_sgrps, s.tl_mode = 1, pl["n_sgrps"], 0
-            s.cams[0], s.cams[1] = t["cams0"].data_ptr(), t["cams1"].data_ptr()
-            s.pts[0], s.pts[1] = t["pts0"].data_ptr(), t["pts1"].data_ptr()
-            s.camrec[0], s.camrec[1] = t["camrec0"].data_ptr(), t["camrec1"].data_ptr()
-            for k in _INDEX_TABLES + ("obs_q", "cpart", "bpart", "sys", "chol", "delta_c",
-                                      "red_part", "small", "state", "ticket") + _MFMA_TABLES:
-                setattr(s, k, t[k].data_ptr())
+            s.cams[0], s.cams[1] = f64p("cams0"), f64p("cams1")
+            s.pts[0], s.pts[1] = f64p("pts0"), f64p("pts1")
+            s.camrec[0], s.camrec[1] = f64p("camrec0"), f64p("camrec1")
+            for k in _INDEX_TABLES + _MFMA_TABLES:
+                setattr(s, k, i32p(k))
+            for k in ("obs_q", "cpart", "bpart", "sys", "chol", "delta_c", "red_part", "small", "state"):
+                setattr(s, k, f64p(k))
+            s.ticket = b32 + 4 * (o32 + nb + 4)
             bp._s = s
-            bp._init = (t["init_c"], t["init_p"])
             out[w] = bp
         it = iter(extra)
         out = [p if p is not None else next(it) for p in out]
