@@ -419,7 +419,7 @@ def run_tracking(args, world, rank):
     # 14.3k vs 15.5-15.7k tracked frames/s, alternating runs, profiles/r5/tracked_leg)
     TRK_LAG = args.tracked_lag
     leg = {"tracked": False}
-    tleg = {"wms": None, "ws": None, "build_s": [], "shapes": [], "modes": {}, "sets": []}
+    tleg = {"wms": None, "ws": None, "build_s": [], "wait_s": [], "shapes": [], "modes": {}, "sets": []}
 
     ba_done = [None]
     step_no, pending = [0], [0]
@@ -439,19 +439,21 @@ def run_tracking(args, world, rank):
             if marks is not None:
                 marks["track"] = tmarks
             return
-        hb = time.perf_counter()
+        hw = time.perf_counter()
         prev.event.synchronize()  # step k-lag's maps are on the host
-        probs = prev.problems(rig.P_l)
+        hb = time.perf_counter()
+        tleg["wait_s"].append(hb - hw)
+        trk._ht("ba_window_wait", hw)
+        # every window's observations, plan, data and descriptor staged by ONE
+        # native call (slam_ba_stage_windows) into pinned buffers, uploaded by
+        # one asynchronous copy per type on the BA stream (BAWindowSet.stage)
+        bps = prev.stage(tleg["ws"], rig.P_l, ba_stream)
         prev.filled = False
-
-        # every window planned natively, staged in one pinned buffer, uploaded by
-        # one asynchronous copy on the BA stream (slam355.ba.BAWindowSet)
-        bps = tleg["ws"].build(probs, ba_stream)
         groups = {}
         for bp in bps:
             groups.setdefault(bp.lin_mode, []).append(bp)
         tleg["build_s"].append(time.perf_counter() - hb)
-        tleg["shapes"].append([(len(pr[0]), len(pr[1]), len(pr[2])) for pr in probs])
+        tleg["shapes"].append([(bp.C, bp.P, bp.O) for bp in bps])
         for mode, g in groups.items():
             tleg["modes"][mode] = tleg["modes"].get(mode, 0) + len(g)
         h0 = trk._ht("ba_window_build", hb)
@@ -597,6 +599,9 @@ def run_tracking(args, world, rank):
                    "window_cams_pts_obs_mean": shp.mean(0).tolist() if len(shp) else None,
                    "window_pts_obs_max": shp.max(0)[1:].tolist() if len(shp) else None,
                    "host_build_ms_per_step": float(np.mean(tleg["build_s"][-args.steps:])) * 1e3,
+                   "host_build_ms_per_window": float(np.mean(tleg["build_s"][-args.steps:])) * 1e3
+                   / max(1, len(tleg["shapes"][-1]) if tleg["shapes"] else 1),
+                   "host_wait_ms_per_step": float(np.mean(tleg["wait_s"][-args.steps:])) * 1e3,
                    "lin_modes": tleg["modes"], "local_ba_ms_per_step": st_t.get("local_ba"),
                    "last_set_cost_mean": float(np.mean([s_["COST"] for s_ in sts])) if sts else None,
                    "last_set_accepted_mean": float(np.mean([s_["NACCEPT"] for s_ in sts])) if sts else None,

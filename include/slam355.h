@@ -227,8 +227,9 @@ int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int M_bound,
  * and fed pairs b = w n + j, j < n, in order -- slam_map_associate of
  * d_abs[b], d_rel[b] ([cap][3]), d_pts2d[b] ([cap][2]), d_count[b] valid
  * points, frame_index j, rows into d_rows[b] ([cap][4]).  One call for the
- * whole batch (the same launches as n_win * n slam_map_associate calls);
- * workspace from slam_map_workspace_bytes(cap, (n - 1) * cap). */
+ * whole batch, the same results as n_win * n slam_map_associate calls: pair j
+ * of every window runs in one launch pair (2n launches instead of 2 n n_win);
+ * workspace n_win * slam_map_workspace_bytes(cap, (n - 1) * cap). */
 int slam_map_windows(double* d_maps, int32_t* d_M, int map_cap, int n_win, int n,
                      const double* d_abs, const double* d_rel, const double* d_pts2d,
                      const int32_t* d_count, int cap, double threshold, double* d_rows,
@@ -440,6 +441,32 @@ int slam_ba_plan_mfma(int n_cams, int n_pts, int n_obs, const int32_t* cam_idx,
                       const int32_t* pt_idx, const int32_t* block_list, int n_block_list,
                       int chunks_per_wg, int32_t* out, long long out_cap,
                       slam_ba_plan_info* info);
+
+/* Host staging of a batch of tracked local-BA windows (the tracked leg's
+ * host side in one call; replaces a Python loop over windows, buffers and plan
+ * tables -- main.py:120-127 / XXXport_files.py:44-64 build the reference's BA
+ * arguments from the local map).  Window w = frames w n .. w n + n - 1 (one
+ * camera each, parameters cams[w n + j][9]); observations = the first cnt[b]
+ * rows (frame j, map point, u, v) of rows[b][cap][4] for its pairs b, q = (u -
+ * u_off, v - v_off); points = maps[w][0 .. M[w])[3].  Each window is planned
+ * (slam_ba_plan_mfma) and, when the plan exists and 9n <= 120, its float64
+ * data (BAProblem's layout: cams0 pts0 cams1 pts1 init_c init_p obs_q, then
+ * zeroed camrec0 camrec1 cpart bpart sys chol delta_c red_part small state,
+ * each 32-double aligned) go to h64 and its plan tables (+ 8 zero int32:
+ * stand-ins, ticket) to h32; probs[w] gets the device addresses of those
+ * buffers at d64 / d32.  meta[w][SLAM_STAGE_META]: staged (0: the caller builds
+ * that window itself), C, P, O, n_grps, n_sgrps, n_cslots, n_bslots, n_blocks,
+ * int32 offset, plan length, sys length, the SLAM_STAGE_NF64 float64 offsets,
+ * the SLAM_PLAN_NTAB table offsets.  need[2] = doubles / int32 used; with
+ * null outputs, or when they exceed cap64 / cap32, only sizes and meta are
+ * produced (grow the buffers and call again). */
+#define SLAM_STAGE_NF64 17
+#define SLAM_STAGE_META (12 + SLAM_STAGE_NF64 + SLAM_PLAN_NTAB)
+int slam_ba_stage_windows(int n_win, int n, int cap, const double* rows, const int32_t* cnt,
+                          const double* maps, int map_cap, const int32_t* M, const double* cams,
+                          double u_off, double v_off, double* h64, long long cap64, int32_t* h32,
+                          long long cap32, const void* d64, const void* d32,
+                          slam_ba_problem* probs, long long* meta, long long* need);
 
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);

@@ -17,18 +17,35 @@
 // sequence of frames runs without host synchronisation.
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int kNnWG = 256;      // queries per workgroup (one per lane)
 constexpr int kNnChunk = 1024;  // map points per workgroup, staged in LDS (24 KiB)
 constexpr int kAssocWG = 1024;
 
+// Window strides (slam_map_windows: one launch for the same pair of every
+// window, window = blockIdx.z here / blockIdx.x in k_map_assoc): map, M,
+// query and count pointers and the workspace advance by these per window;
+// all zero for a single map.
+struct WinStride {
+  size_t map, x, n, part;
+};
+
 __global__ __launch_bounds__(kNnWG) void k_map_nn(const double* __restrict__ map,
                                                   const int32_t* __restrict__ d_M,
                                                   const double* __restrict__ X,
                                                   const int32_t* __restrict__ d_n, int N,
                                                   double* __restrict__ part_d2,
-                                                  int32_t* __restrict__ part_idx) {
+                                                  int32_t* __restrict__ part_idx, WinStride ws) {
+  const size_t wz = blockIdx.z;
+  map += wz * ws.map;
+  d_M += wz;
+  X += wz * ws.x * 3;
+  if (d_n) d_n += wz * ws.n;
+  part_d2 += wz * ws.part;
+  part_idx += wz * ws.part;
   __shared__ double sm[3 * kNnChunk];
   const int M = *d_M;
   const int n = d_n ? min(max(*d_n, 0), N) : N;
@@ -59,7 +76,17 @@ __global__ __launch_bounds__(kAssocWG) void k_map_assoc(
     const double* __restrict__ rel, const double* __restrict__ pts2d,
     const int32_t* __restrict__ d_n, int N, double threshold, int frame,
     const double* __restrict__ part_d2, const int32_t* __restrict__ part_idx,
-    double* __restrict__ rows) {
+    double* __restrict__ rows, WinStride ws) {
+  const size_t wx = blockIdx.x;
+  map += wx * ws.map;
+  d_M += wx;
+  X += wx * ws.x * 3;
+  rel += wx * ws.x * 3;
+  pts2d += wx * ws.x * 2;
+  rows += wx * ws.x * 4;
+  if (d_n) d_n += wx * ws.n;
+  part_d2 += wx * ws.part;
+  part_idx += wx * ws.part;
   __shared__ int wsum[kAssocWG / 64];
   const int M = *d_M;
   const int n = d_n ? min(max(*d_n, 0), N) : N;
@@ -171,11 +198,11 @@ extern "C" int slam_map_associate(double* d_map, int32_t* d_M, int map_cap, int 
   hipStream_t s = slam::as_stream(stream);
   if (nch > 0) {
     dim3 grid((N + kNnWG - 1) / kNnWG, nch);
-    k_map_nn<<<grid, kNnWG, 0, s>>>(d_map, d_M, d_abs, d_n, N, part_d2, part_idx);
+    k_map_nn<<<grid, kNnWG, 0, s>>>(d_map, d_M, d_abs, d_n, N, part_d2, part_idx, WinStride{});
     SLAM_LAUNCHED("k_map_nn");
   }
   k_map_assoc<<<1, kAssocWG, 0, s>>>(d_map, d_M, d_abs, d_rel, d_pts2d, d_n, N, threshold,
-                                     frame_index, part_d2, part_idx, d_rows);
+                                     frame_index, part_d2, part_idx, d_rows, WinStride{});
   SLAM_LAUNCHED("k_map_assoc");
   return SLAM_OK;
 }
@@ -187,20 +214,33 @@ extern "C" int slam_map_windows(double* d_maps, int32_t* d_M, int map_cap, int n
   SLAM_REQUIRE(n_win >= 0 && n >= 1 && cap >= 0 && map_cap >= 0, "slam_map_windows: bad shape");
   SLAM_REQUIRE((long long)n * cap <= map_cap, "slam_map_windows: map capacity %d < %d pairs x %d",
                map_cap, n, cap);
-  SLAM_REQUIRE(ws_size >= ws_bytes(cap, (n - 1) * cap), "slam_map_windows: workspace too small");
+  SLAM_REQUIRE(ws_size >= (size_t)n_win * ws_bytes(cap, (n - 1) * cap),
+               "slam_map_windows: workspace too small (n_win x slam_map_workspace_bytes)");
   if (n_win == 0 || cap == 0) return SLAM_OK;
   SLAM_REQUIRE(d_maps && d_M && d_abs && d_rel && d_pts2d && d_count && d_rows && d_ws,
                "slam_map_windows: null pointer");
   hipStream_t s = slam::as_stream(stream);
   SLAM_HIP(hipMemsetAsync(d_M, 0, sizeof(int32_t) * (size_t)n_win, s));
-  for (int w = 0; w < n_win; ++w)
-    for (int j = 0; j < n; ++j) {
-      const size_t b = (size_t)w * n + j;
-      if (int rc = slam_map_associate(d_maps + (size_t)w * map_cap * 3, d_M + w, map_cap, j * cap,
-                                      d_abs + b * cap * 3, d_rel + b * cap * 3, d_pts2d + b * cap * 2,
-                                      d_count + b, cap, threshold, j, d_rows + b * cap * 4, d_ws,
-                                      ws_size, stream))
-        return rc;
+  // pair j of every window in one launch pair (the windows are independent;
+  // within a window the pairs stay in order): per window its own map, size,
+  // rows and a workspace slice of nch_max x cap partials
+  const int nch_max = ((n - 1) * cap + kNnChunk - 1) / kNnChunk;
+  const size_t part = (size_t)std::max(nch_max, 1) * cap;
+  double* part_d2 = static_cast<double*>(d_ws);
+  int32_t* part_idx = reinterpret_cast<int32_t*>(part_d2 + (size_t)n_win * part);
+  const WinStride wst{(size_t)map_cap * 3, (size_t)n * cap, (size_t)n, part};
+  for (int j = 0; j < n; ++j) {
+    const size_t b = (size_t)j;  // pair j of window 0; window w adds w * n pairs
+    const int nch = (j * cap + kNnChunk - 1) / kNnChunk;
+    if (nch > 0) {
+      k_map_nn<<<dim3((cap + kNnWG - 1) / kNnWG, nch, n_win), kNnWG, 0, s>>>(
+          d_maps, d_M, d_abs + b * cap * 3, d_count + b, cap, part_d2, part_idx, wst);
+      SLAM_LAUNCHED("k_map_nn");
     }
+    k_map_assoc<<<n_win, kAssocWG, 0, s>>>(d_maps, d_M, d_abs + b * cap * 3, d_rel + b * cap * 3,
+                                           d_pts2d + b * cap * 2, d_count + b, cap, threshold, j,
+                                           part_d2, part_idx, d_rows + b * cap * 4, wst);
+    SLAM_LAUNCHED("k_map_assoc");
+  }
   return SLAM_OK;
 }

@@ -143,6 +143,8 @@ SIGNATURES = {
     "slam_ba_plan_bound": [c_int, c_int, c_int, c_int],
     "slam_ba_plan_mfma": [c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_int, c_p, c_longlong,
                           ctypes.POINTER(PlanInfo)],
+    "slam_ba_stage_windows": [c_int, c_int, c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_double,
+                              c_double, c_p, c_longlong, c_p, c_longlong, c_p, c_p, c_p, c_p, c_p],
 }
 _RESTYPE = {"slam_last_error": ctypes.c_char_p, "slam_ba_sys_len": ctypes.c_longlong,
             "slam_ba_plan_bound": ctypes.c_longlong,

@@ -1072,13 +1072,15 @@ class _WindowProblem(BAProblem):
     @property
     def t(self):
         if self._t is None:
+            if self._views is None:  # staged by BAWindowSet.stage: offsets from its meta row
+                self._views = BAWindowSet._views_of(self._d64, self._d32, self._meta)
             d64, d32, o64, o32, nb, offs = self._views
             t = {}
             for k, (o, shp) in o64.items():
                 t[k] = d64[o:o + int(np.prod(shp))].view(shp)
             pb = d32[o32:o32 + nb]
             t["plan_buf"] = pb
-            for k in _INDEX_TABLES + _MFMA_TABLES:
+            for k in _INDEX_TABLES + _MFMA_TABLES + ("perm",):
                 t[k] = pb[offs[k]:] if k in offs else d32[o32 + nb:o32 + nb + 1]
             t["ticket"] = d32[o32 + nb + 4:o32 + nb + 5]
             self._t = t
@@ -1087,6 +1089,16 @@ class _WindowProblem(BAProblem):
     @property
     def _init(self):
         return (self.t["init_c"], self.t["init_p"])
+
+    @property
+    def perm(self):
+        if self._perm is None:
+            self._perm = self.t["perm"][:self.P].cpu().numpy().astype(np.int64)
+        return self._perm
+
+    @perm.setter
+    def perm(self, v):
+        self._perm = v
 
 
 class BAWindowSet:
@@ -1114,6 +1126,111 @@ class BAWindowSet:
     @staticmethod
     def _al(n):
         return (max(int(n), 1) + 31) // 32 * 32
+
+    _F64 = ("cams0", "pts0", "cams1", "pts1", "init_c", "init_p", "obs_q", "camrec0", "camrec1",
+            "cpart", "bpart", "sys", "chol", "delta_c", "red_part", "small", "state")
+    META = 12 + len(_F64) + len(_lib.PLAN_TABLES)  # SLAM_STAGE_META
+
+    @staticmethod
+    def _views_of(d64, d32, m):
+        """(d64, d32, {buffer: (offset, shape)}, int32 offset, plan length,
+        {table: offset}) of a window staged by slam_ba_stage_windows (meta row m)."""
+        C, P, O = int(m[1]), int(m[2]), int(m[3])
+        n_cs, n_bs = int(m[6]), int(m[7])
+        shp = {"cams0": (C, 9), "pts0": (P, 3), "cams1": (C, 9), "pts1": (P, 3), "init_c": (C, 9),
+               "init_p": (P, 3), "obs_q": (max(O, 1), 2), "camrec0": (C * 32,), "camrec1": (C * 32,),
+               "cpart": (max(n_cs * 112, 1),), "bpart": (max(n_bs * 81, 1),), "sys": (int(m[11]),),
+               "chol": (1,), "delta_c": (9 * C,), "red_part": (max(_lib.lib.slam_ba_red_slots(int(m[4])), 1),),
+               "small": (4,), "state": (N_STATE,)}
+        o64 = {k: (int(m[12 + i]), shp[k]) for i, k in enumerate(BAWindowSet._F64)}
+        base = 12 + len(BAWindowSet._F64)
+        offs = {k: int(m[base + i]) for i, k in enumerate(_lib.PLAN_TABLES)}
+        return d64, d32, o64, int(m[9]), int(m[10]), offs
+
+    def stage(self, rows, cnt, maps, M, cams, u_off, v_off, stream, lam0=1e-4):
+        """The tracked windows of one batch, staged by ONE native call
+        (slam_ba_stage_windows: every window's observations from the mapper's
+        rows, its plan, its float64 data and tables into the pinned staging
+        buffers, its descriptor with the device addresses) and uploaded by one
+        copy per type.  rows [B, cap, 4] (frame, map point, u, v), cnt [B],
+        maps [W, map_cap, 3], M [W], cams [B, 9] with B = W n; window w = pairs
+        w n .. w n + n - 1.  Windows the camera-union plan cannot take are
+        built as ordinary BAProblems (from the same host arrays).  Returns the
+        problems in window order (BAProblem interface)."""
+        rows = np.ascontiguousarray(rows, np.float64)
+        cnt = np.ascontiguousarray(cnt, np.int32)
+        maps = np.ascontiguousarray(maps, np.float64)
+        M = np.ascontiguousarray(M, np.int32)
+        cams = np.ascontiguousarray(cams, np.float64).reshape(-1, 9)
+        B, cap = rows.shape[0], rows.shape[1]
+        W, map_cap = maps.shape[0], maps.shape[1]
+        if W == 0 or B % W or len(cams) != B or len(cnt) != B or len(M) != W:
+            raise ValueError("stage: rows / cnt / cams must cover W windows of B / W pairs each")
+        n = B // W
+        meta = np.zeros((W, self.META), np.int64)
+        need = np.zeros(2, np.int64)
+        probs = (_Prob * W)()
+        args = (W, n, cap, rows.ctypes.data, cnt.ctypes.data, maps.ctypes.data, map_cap,
+                M.ctypes.data, cams.ctypes.data, float(u_off), float(v_off))
+        hs = self.h[self.k & 1]
+        if hs is not None:
+            hs[2].synchronize()  # that set's previous upload has run
+        for attempt in range(2):
+            ok64 = hs is not None and self.d_f64 is not None and hs[0].numel() <= self.d_f64.numel()
+            ok32 = hs is not None and self.d_i32 is not None and hs[1].numel() <= self.d_i32.numel()
+            if ok64 and ok32:
+                _lib.call("slam_ba_stage_windows", *args, hs[0].data_ptr(), hs[0].numel(),
+                          hs[1].data_ptr(), hs[1].numel(), self.d_f64.data_ptr(),
+                          self.d_i32.data_ptr(), ctypes.addressof(probs), meta.ctypes.data,
+                          need.ctypes.data)
+            else:
+                _lib.call("slam_ba_stage_windows", *args, None, 0, None, 0, None, None, None,
+                          meta.ctypes.data, need.ctypes.data)
+            n64, n32 = int(need[0]), int(need[1])
+            if ok64 and ok32 and n64 <= hs[0].numel() and n32 <= hs[1].numel():
+                break
+            # grow: pinned staging of this set and the shared device buffers (both
+            # sized alike, so the device addresses written above stay valid)
+            sz64, sz32 = max(n64, 1) * 3 // 2, max(n32, 1) * 3 // 2
+            hs = [torch.zeros(sz64, dtype=torch.float64, pin_memory=True),
+                  torch.zeros(sz32, dtype=torch.int32, pin_memory=True), torch.cuda.Event()]
+            self.h[self.k & 1] = hs
+            with torch.cuda.stream(stream):
+                if self.d_f64 is None or self.d_f64.numel() < sz64:
+                    self.d_f64 = torch.empty(sz64, dtype=torch.float64, device=self.dev)
+                if self.d_i32 is None or self.d_i32.numel() < sz32:
+                    self.d_i32 = torch.empty(sz32, dtype=torch.int32, device=self.dev)
+        else:
+            raise RuntimeError("stage: staging buffers could not be sized")
+        self.k += 1
+        with torch.cuda.stream(stream):
+            if n64:
+                self.d_f64[:n64].copy_(hs[0][:n64], non_blocking=True)
+            if n32:
+                self.d_i32[:n32].copy_(hs[1][:n32], non_blocking=True)
+            hs[2].record(stream)
+        out = []
+        for w in range(W):
+            m = meta[w]
+            if not m[0]:  # not plannable here: an ordinary problem from the same rows
+                om = np.concatenate([rows[b, :max(min(int(cnt[b]), cap), 0)] for b in range(w * n, w * n + n)])
+                qs = np.stack([om[:, 2] - u_off, om[:, 3] - v_off], 1)
+                out.append(BAProblem(cams[w * n:w * n + n].copy(), maps[w, :int(M[w])].copy(),
+                                     om[:, 0].astype(np.int64), om[:, 1].astype(np.int64), qs,
+                                     lam0=lam0, stream=stream))
+                continue
+            bp = _WindowProblem()
+            bp._t, bp._perm, bp._views = None, None, None
+            bp._d64, bp._d32, bp._meta = self.d_f64, self.d_i32, m
+            bp.plan, bp.lin_mode = None, "mfma"
+            bp.C, bp.P, bp.O, bp.stream = int(m[1]), int(m[2]), int(m[3]), stream
+            bp.sys_len, bp.tl_levels = int(m[11]), False
+            bp._s = probs[w]
+            out.append(bp)
+        built = [p for p in out if isinstance(p, _WindowProblem)]
+        for i in range(0, len(built), BABatch.MAX_BATCH):
+            BABatch(built[i:i + BABatch.MAX_BATCH], stream=stream).reset(lam0)
+        return out
 
     def build(self, problems, stream, lam0=1e-4):
         specs, extra = [], []
@@ -1181,7 +1298,7 @@ class BAWindowSet:
             bp = _WindowProblem()
             nb = len(pl["buf"])
             offs = pl["offs"]
-            bp._t = None
+            bp._t, bp._perm = None, None
             bp._views = (self.d_f64, self.d_i32, o64, o32, nb, offs)
             bp.plan, bp.lin_mode, bp.perm = pl, "mfma", pl["perm"]
             bp.C, bp.P, bp.O, bp.stream = C, P, pl["n_obs"], stream

@@ -352,7 +352,8 @@ class WindowMapper:
         self.d_M = torch.zeros((self.n_win,), dtype=torch.int32, device=d)
         nb = ctypes.c_size_t(0)
         _lib.call("slam_map_workspace_bytes", cap, (self.n - 1) * cap, ctypes.byref(nb))
-        self.ws = torch.empty(max(int(nb.value), 1), dtype=torch.uint8, device=d)
+        # one workspace slice per window (slam_map_windows runs a pair of every window per launch)
+        self.ws = torch.empty(max(self.n_win * int(nb.value), 1), dtype=torch.uint8, device=d)
         f64 = dict(dtype=torch.float64, device=d)
         self.abs = torch.zeros((B, cap, 3), **f64)
         self.rows = torch.zeros((B, cap, 4), **f64)
@@ -365,6 +366,7 @@ class WindowMapper:
         self.h_maps = torch.zeros((self.n_win, self.n * cap, 3), dtype=torch.float64, **pin)
         self.h_M = torch.zeros((self.n_win,), dtype=torch.int32, **pin)
         self.event = torch.cuda.Event()
+        self.copy_stream = torch.cuda.Stream()
         self.filled = False
 
     def save_pose0(self, stream):
@@ -373,22 +375,41 @@ class WindowMapper:
 
     def map_batch(self, stream):
         t = self.trk
+        stream.wait_event(self.event)  # this mapper's previous host copies have run
         with torch.cuda.stream(stream):
             _lib.call("slam_rel_to_abs", ptr(t.Q1), ptr(t.t_cnt), t.cap, t.B, ptr(t.poses),
                       ptr(self.abs), stream_ptr(stream))
             # every window's device map in one call (slam_map_windows: the
-            # appendKeyPoints launches of its pairs, in order, maps restarted empty)
+            # appendKeyPoints launches of its pairs, in order, maps restarted
+            # empty; pair j of all windows per launch)
             _lib.call("slam_map_windows", ptr(self.maps), ptr(self.d_M), self.n * t.cap, self.n_win,
                       self.n, ptr(self.abs), ptr(t.Q1), ptr(t.q1), ptr(t.t_cnt), t.cap,
                       self.threshold, ptr(self.rows), ptr(self.ws), self.ws.numel(), stream_ptr(stream))
-            self.h_maps.copy_(self.maps, non_blocking=True)
-            self.h_rows.copy_(self.rows, non_blocking=True)
+            # the tracker's buffers (rewritten by the next batch) are copied on
+            # the tracking stream; the mapper's own maps and rows (~7 MB at 64
+            # pairs) on a copy stream, so the next batch's tracking does not
+            # queue behind them
             self.h_cnt.copy_(t.t_cnt, non_blocking=True)
             self.h_poses.copy_(t.poses, non_blocking=True)
             self.h_pose0.copy_(self.pose0, non_blocking=True)
             self.h_M.copy_(self.d_M, non_blocking=True)
-            self.event.record(stream)
+        self.copy_stream.wait_stream(stream)
+        with torch.cuda.stream(self.copy_stream):
+            self.h_maps.copy_(self.maps, non_blocking=True)
+            self.h_rows.copy_(self.rows, non_blocking=True)
+            self.event.record(self.copy_stream)
         self.filled = True
+
+    def stage(self, ws, P_left, stream, lam0=1e-4):
+        """The batch's windows as BA problems in one native call
+        (BAWindowSet.stage over this mapper's host copies; call after
+        event.synchronize()): the same problems as ws.build(self.problems(P_left))."""
+        from .XXXport_files import U_OFF, V_OFF, make_cam_params
+
+        frames = np.concatenate([self.h_pose0.numpy()[None], self.h_poses.numpy()[:-1]])
+        cams = make_cam_params(frames, P_left).reshape(-1, 9)
+        return ws.stage(self.h_rows.numpy(), self.h_cnt.numpy(), self.h_maps.numpy(),
+                        self.h_M.numpy(), cams, U_OFF, V_OFF, stream, lam0)
 
     def problems(self, P_left):
         """Every window's (cams [n,9], pts [M,3], cam_idx, pt_idx, qs [O,2]) from

@@ -941,6 +941,119 @@ def test_gpu_window_set_equals_separate_problems():
             assert np.array_equal(r[w][0], rc) and np.array_equal(r[w][1], rp), w
 
 
+def _stage_inputs(specs, n, seed, u_off=0.5, v_off=0.25):
+    """Mapper-shaped host arrays (rows [W n, cap, 4] = (frame, point, u, v),
+    counts, maps, M, cams) for synthetic windows of n cameras, each window's
+    observations dealt over its n pairs in order, and the problems they stand
+    for (q = u - u_off: the stager's arithmetic)."""
+    from slam355.synthetic import ba_problem, perturb
+
+    wins = []
+    for w, (P, k) in enumerate(specs):
+        rng = np.random.default_rng(seed + w)
+        cams, pts, ci, pi, qs = ba_problem(rng, n, P, k)
+        c0, p0 = perturb(rng, cams, pts)
+        wins.append((c0, p0, ci, pi, qs))
+    W = len(wins)
+    cap = max(-(-len(w[2]) // n) for w in wins)
+    map_cap = max(len(w[1]) for w in wins)
+    rows = np.zeros((W * n, cap, 4))
+    cnt = np.zeros(W * n, np.int32)
+    maps = np.zeros((W, map_cap, 3))
+    M = np.zeros(W, np.int32)
+    cams = np.zeros((W * n, 9))
+    probs = []
+    for w, (c0, p0, ci, pi, qs) in enumerate(wins):
+        maps[w, :len(p0)] = p0
+        M[w] = len(p0)
+        cams[w * n:(w + 1) * n] = c0
+        parts = np.array_split(np.arange(len(ci)), n)
+        qq = []
+        for j, idx in enumerate(parts):
+            b = w * n + j
+            cnt[b] = len(idx)
+            rows[b, :len(idx)] = np.stack([ci[idx], pi[idx], qs[idx, 0] + u_off, qs[idx, 1] + v_off], 1)
+            qq.append(np.stack([rows[b, :len(idx), 2] - u_off, rows[b, :len(idx), 3] - v_off], 1))
+        probs.append((c0, p0, ci, pi, np.concatenate(qq)))
+    return (rows, cnt, maps, M, cams, u_off, v_off), probs
+
+
+def test_stage_windows_layout_matches_planner():
+    """slam_ba_stage_windows (host only, fake device addresses): per window the
+    native planner's tables, the float64 data in BAProblem's layout (points
+    permuted by the plan, observations in plan order) and descriptor addresses
+    at the staged offsets; a window the camera-union plan cannot take (every
+    point seen by all 8 cameras) is left to the caller."""
+    import ctypes
+
+    from slam355 import _lib, ba
+
+    (rows, cnt, maps, M, cams, uo, vo), probs = _stage_inputs([(800, 3), (300, 8), (1000, 2)], 8, 70)
+    W = len(probs)
+    meta = np.zeros((W, ba.BAWindowSet.META), np.int64)
+    need = np.zeros(2, np.int64)
+    args = (W, 8, rows.shape[1], rows.ctypes.data, cnt.ctypes.data, maps.ctypes.data, maps.shape[1],
+            M.ctypes.data, cams.ctypes.data, uo, vo)
+    _lib.call("slam_ba_stage_windows", *args, None, 0, None, 0, None, None, None, meta.ctypes.data,
+              need.ctypes.data)
+    assert list(meta[:, 0]) == [1, 0, 1]
+    h64 = np.full(int(need[0]), np.nan)
+    h32 = np.full(int(need[1]), -7, np.int32)
+    d64, d32 = 1 << 40, 1 << 41
+    structs = (ba._Prob * W)()
+    _lib.call("slam_ba_stage_windows", *args, h64.ctypes.data, len(h64), h32.ctypes.data, len(h32),
+              d64, d32, ctypes.addressof(structs), meta.ctypes.data, need.ctypes.data)
+    for w in (0, 2):
+        c0, p0, ci, pi, qs = probs[w]
+        pl = ba.plan_mfma_native(8, len(p0), ci, pi)
+        m = meta[w]
+        _, _, o64, o32, nb, offs = ba.BAWindowSet._views_of(h64, h32, m)
+        assert nb == len(pl["buf"]) and np.array_equal(h32[o32:o32 + nb], pl["buf"])
+        assert np.all(h32[o32 + nb:o32 + nb + 8] == 0)
+        get = lambda k: h64[o64[k][0]:o64[k][0] + int(np.prod(o64[k][1]))].reshape(o64[k][1])  # noqa: E731
+        for k in ("cams0", "cams1", "init_c"):
+            assert np.array_equal(get(k), c0)
+        for k in ("pts0", "pts1", "init_p"):
+            assert np.array_equal(get(k), p0[pl["perm"]])
+        assert np.array_equal(get("obs_q"), qs[pl["order"]])
+        for k in ba.BAWindowSet._F64[7:]:
+            assert np.all(get(k) == 0.0), k
+        s = structs[w]
+        assert (s.n_cams, s.n_pts, s.n_obs, s.n_sgrps) == (8, len(p0), len(ci), pl["n_sgrps"])
+        assert s.cams[1] == d64 + 8 * o64["cams1"][0] and s.state == d64 + 8 * o64["state"][0]
+        assert s.obs_meta == d32 + 4 * (o32 + offs["obs_meta"])
+        assert s.ticket == d32 + 4 * (o32 + nb + 4)
+
+
+@pytest.mark.gpu
+def test_gpu_window_stage_equals_separate_problems():
+    """BAWindowSet.stage (the tracked leg's one-call host staging) gives every
+    window the iterates BAProblem gives it alone, bit for bit, twice in a row
+    into the reused buffers; the window the camera-union plan cannot take is
+    an ordinary (slot-mode) problem."""
+    import torch
+    from slam355 import ba
+
+    inp, probs = _stage_inputs([(800, 3), (300, 8), (1000, 2)], 8, 80)
+    s = torch.cuda.Stream()
+    ws = ba.BAWindowSet()
+    runs = []
+    for _ in range(2):
+        got = ws.stage(*inp, stream=s)
+        assert [p.lin_mode for p in got] == ["mfma", "slot", "mfma"]
+        with torch.cuda.stream(s):
+            ba.BABatch([got[0], got[2]], stream=s).iterate(4)
+            got[1].iterate(4)
+        torch.cuda.synchronize()
+        runs.append([p.params() for p in got])
+    for w, pr in enumerate(probs):
+        ref = ba.BAProblem(*pr)
+        ref.iterate(4)
+        rc, rp = ref.params()
+        for r in runs:
+            assert np.array_equal(r[w][0], rc) and np.array_equal(r[w][1], rp), w
+
+
 def test_assembly_table_counts_every_partial_row():
     """The folded assembly's table (slam355.ba.assembly_table): every cpart row
     is counted once at its camera's diagonal block, every bpart row once at its
