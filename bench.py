@@ -387,13 +387,14 @@ def run_tracking(args, world, rank):
     bas = []
     for i, s in enumerate(ba_subs):
         with torch.cuda.stream(s):
-            # 5 chunks per workgroup unless set: the launch set batches 8 windows,
-            # so fewer, fuller workgroups than the single-window auto choice (3)
-            # still cover the chip and write 3/5 of its partial rows; at 64 pairs
-            # per step, alternating runs: 3 / 4 / 5 / 6 / 8 -> 17.7k / 17.8k /
-            # 18.1-18.3k / 18.1-18.3k / 17.6-17.9k frames/s
-            # (round-3 sweep; 8 was best at 32 pairs per step)
-            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 8
+            # 16 chunks per workgroup unless set: the launch set batches 16
+            # windows, so fewer, fuller workgroups still cover the chip and write
+            # fewer partial rows -- round 5, alternating runs of this bench
+            # (profiles/r5/cpw_ab): 8 / 16 / 32 -> 22.0-22.3k / 22.3-22.5k /
+            # 21.1-21.2k frames/s, PMC traffic of a batched iteration 54.8 /
+            # 44.7 / 39.6 MB (the 16-window set alone is faster at 8: 65k vs
+            # 57k window-iterations/s, but beside tracking it is not)
+            cpw = args.chunks_per_wg if args.chunks_per_wg is not None else 16
             bas.append(BABatch([BAProblem(*w, stream=s, chunks_per_wg=cpw,
                                           fold_assembly=args.fold)
                                 for w in windows[i::ns]], stream=s))
