@@ -233,10 +233,19 @@ constexpr int kRc = 4;  // refinement points per lane held in registers (L <= 25
 // sums term j over (s, a) in the oracle's order (H, g, cost), every lane then
 // reads the 28 sums and runs the identical 6x6 solve and decision, so p and
 // lam stay replicated.  Bitwise the operations of oracle lm.
-// t: LDS [2 * kMinSample][28], sums: LDS [28 + kMinSample].  Every lane of the
-// group's wave must call it (wave-level __syncthreads inside).
+// t: LDS [2 * kMinSample][kLmT], sums: LDS [28 + kMinSample].  Every lane of
+// the group's wave must call it (wave-level __syncthreads inside).
+// Row stride 29 doubles: the five point lanes' term stores (16-lane groups of
+// ds_write_b64, bank = dword mod 32) fall on distinct banks (at 28 lanes 0, 2
+// and 4 shared one: 3.3 conflict cycles per LDS instruction).
+constexpr int kLmT = 29;
+// per-group block of t: 10 rows of 29 doubles padded to 304 (608 dwords = 32
+// mod 64), so the sum reads of groups g and g+1 (one 32-lane half of a
+// ds_read_b64, bank = dword mod 64) use the two bank halves
+constexpr int kLmGroup = 304;
+static_assert(kLmGroup >= 2 * kMinSample * kLmT && (2 * kLmGroup) % 64 == 32, "lm_group LDS layout");
 __device__ void lm_group(const double* Q, const double* q, int n, const Cam& K, int iters,
-                         double p[6], int k, double (*t)[28], double* sums) {
+                         double p[6], int k, double (*t)[kLmT], double* sums) {
   double lam = 1e-3;
   double R[9];  // rotation of p: carried over from the trial pose when a step is accepted
   rodrigues(p, R);
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_lm(const double* __restrict__ Qa
 #endif
   __shared__ double spw[kHypGroups][3 * kMinSample], suv[kHypGroups][2 * kMinSample];
   __shared__ int sidx[kHypGroups][kMinSample];
-  __shared__ double lmt[kHypGroups][2 * kMinSample][28], lms[kHypGroups][28 + kMinSample];
+  __shared__ double lmt[kHypGroups * kLmGroup], lms[kHypGroups][28 + kMinSample];
   __shared__ double p0[kHypGroups][6];
   const int b = blockIdx.x, t = threadIdx.x;
   const int g = t >> 4, k = t & 15;
@@ -473,7 +482,8 @@ __global__ __launch_bounds__(64) void k_pnp_hyp_lm(const double* __restrict__ Qa
   __syncthreads();
   double p[6];
   for (int i = 0; i < 6; ++i) p[i] = p0[g][i];
-  lm_group(spw[g], suv[g], kMinSample, K, hyp_iters, p, k, lmt[g], lms[g]);
+  lm_group(spw[g], suv[g], kMinSample, K, hyp_iters, p, k,
+           reinterpret_cast<double (*)[kLmT]>(lmt + g * kLmGroup), lms[g]);
   if (k == 0 && live)
     for (int i = 0; i < 6; ++i) o[i] = p[i];
 }
