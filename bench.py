@@ -711,7 +711,8 @@ def run_tracking(args, world, rank):
                    # the headline's windows are fixed synthetic C3 problems (clean
                    # tracks, sigma 0.5 px), restored and re-solved every launch set;
                    # BA over windows built from the tracked frames is measured
-                   # beside it in "tracked_window_ba" (its per-window build cost there)
+                   # beside it in "tracked_source" (a timed region of its own;
+                   # --ba-source tracked makes it the line's value)
                    "local_ba_source": "synthetic C3",
                    "local_ba_launch_set": (f"{n_launch} windows every {G} steps (pending steps flushed "
                                            "as a whole set at the ends of warmup and timed region)" if G > 1 else
@@ -738,6 +739,17 @@ def run_tracking(args, world, rank):
         rec["pcie_inclusive"] = pcie
     if tracked is not None:
         rec["tracked_source"] = tracked
+    if args.ba_source == "tracked":
+        # the line's value from the tracked-source region (opt-in; the driver's
+        # default stays the BASELINE-named synthetic C3 windows)
+        if tracked is None:
+            raise SystemExit("--ba-source tracked needs the tracked leg (one rank, batch a "
+                             "multiple of --ba-every, no --no-tracked-leg)")
+        rec["synthetic_source"] = {"frames_per_s": rec["value"], "ms_per_step": rec["ms_per_step"]}
+        rec["value"], rec["ms_per_step"] = tracked["frames_per_s"], tracked["ms_per_step"]
+        rec["config"]["local_ba_source"] = (f"tracked: windows of {args.ba_every} tracked frame pairs, "
+                                            "mapped on the device, staged by one native call, solved "
+                                            f"{args.tracked_lag} steps behind tracking (tracked_source)")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_tracking(L_np, R_np, rig, args, C3, windows[0],
                                                     pairs=CPU_PAIRS, lm_iters=CPU_PAIRS)
@@ -1293,6 +1305,10 @@ def main():
     ap.add_argument("--no-pcie-leg", action="store_true",
                     help="tracking: skip the PCIe-inclusive run (frames streamed from pinned host "
                          "memory inside the timed region) reported beside the headline")
+    ap.add_argument("--ba-source", default="synthetic", choices=["synthetic", "tracked"],
+                    help="local-BA windows of the line's value: the BASELINE-named synthetic C3 "
+                         "windows (default; the tracked-source rate beside it) or the windows "
+                         "built from the tracked frames")
     ap.add_argument("--tracked-lag", type=int, default=2,
                     help="steps between a batch's tracking and its tracked-window BA (>= 1)")
     ap.add_argument("--no-tracked-leg", action="store_true",
