@@ -40,6 +40,26 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
               " ".join(f"{PH[i]} {d[i]:6.1f}" for i in range(6)) + f" | x at {rel[J,6]:7.1f}")
         if J > 24:
             break
+    fs = getattr(_lib.lib, "slam_flow_sub_stamps", None)
+    if fs is not None:
+        fs.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        sb = (ctypes.c_ulonglong * (8 * T))()
+        fs(ctypes.cast(sb, ctypes.c_void_p), T)
+        raw = np.array(sb[:], np.uint64).reshape(T, 8).astype(np.float64)
+        sub = np.where((raw > t0) & (raw < t0 + 1e8), (raw - t0) * 10 / 1000.0, np.nan)
+        rs = sched  # rs(J) list at rec[J, 2], count rec[J, 3]; rows at rec[J, 0], count rec[J, 1]
+        print("  row 0 of each column (us, absolute): first child in / last child in / factor end /"
+              " folds done / staged / product / published | parent's last child in")
+        for J in range(min(T, 26)):
+            last_in = ""
+            if rec[J, 1] > 0:
+                P = int(rs[rec[J, 0]])
+                kids = rs[rec[P, 2]:rec[P, 2] + rec[P, 3]]
+                if len(kids) and int(kids[-1]) == J:
+                    last_in = f"{sub[P, 1]:7.1f} (+{sub[P, 1] - sub[J, 5]:.1f})"
+            print(f"  col {J:3d}: " + " ".join(f"{sub[J, i]:7.1f}" for i in (0, 1)) + f" {rel[J, 2]:7.1f} " +
+                  " ".join(f"{sub[J, i]:7.1f}" for i in (2, 3, 4, 5)) + " | " + last_in +
+                  f" | staging at the barrier: wave 0 {sub[J, 6]:7.1f}, waves 1-3 {sub[J, 7]:7.1f}")
     ff = getattr(_lib.lib, "slam_flow_fac_stamps", None)
     if ff is not None:
         fb = (ctypes.c_ulonglong * 16)()

@@ -2753,10 +2753,33 @@ __device__ unsigned long long g_flow_stamp[SLAM_TL_FLOW_MAX_T][8];
   do {                                                            \
     if (threadIdx.x == 0) g_flow_stamp[(col)][i] = wall_clock64(); \
   } while (0)
+// finer stamps of the same column: first child tile in, last child tile in,
+// row 0's deferred folds done, row 0 staged, row 0's product done, row 0 published
+__device__ unsigned long long g_flow_sub[SLAM_TL_FLOW_MAX_T][8];
+// The own column's stamps go to LDS (flow_lds: 0-4 phases, 8-13 sub-stamps)
+// and out to global memory at the end, so that no stamp store is pending at
+// the phases' own s_waitcnt vmcnt(0).
+#define FLOW_LDS(i)                                               \
+  do {                                                            \
+    if (threadIdx.x == 0) flow_lds[i] = wall_clock64();           \
+  } while (0)
+#define FLOW_S(i) FLOW_LDS(8 + (i))
+#define FLOW_T(i) FLOW_LDS(i)
+#define FLOW_FLUSH()                                                             \
+  do {                                                                           \
+    if (threadIdx.x == 0) {                                                      \
+      for (int i_ = 0; i_ < 5; ++i_) g_flow_stamp[J][i_] = flow_lds[i_];         \
+      for (int i_ = 0; i_ < 6; ++i_) g_flow_sub[J][i_] = flow_lds[8 + i_];       \
+      g_flow_sub[J][6] = flow_lds[5];                                            \
+      g_flow_sub[J][7] = max(flow_lds[6], max(flow_lds[7], flow_lds[14]));         \
+    }                                                                            \
+  } while (0)
 #else
 #define FLOW_TC(col, i) (void)0
+#define FLOW_S(i) (void)0
+#define FLOW_T(i) (void)0
+#define FLOW_FLUSH() (void)0
 #endif
-#define FLOW_T(i) FLOW_TC(J, i)
 
 struct FlowPtrs {
   int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt, *dv;
@@ -2891,6 +2914,26 @@ __device__ __forceinline__ void tile_to_frag_sc1(const double* __restrict__ g, i
   for (int q = 0; q < 16; ++q) f[((w + 4 * q) << 6) + lane] = tmp[q];
 }
 
+// two tiles through sc1 loads, all 32 loads of a lane in flight before the LDS stores
+__device__ __forceinline__ void tiles2_to_frag_sc1(const double* __restrict__ g0, const double* __restrict__ g1,
+                                                   int ld, double* f0, double* f1) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r = lane & 15, c = lane >> 4;
+  double t0[16], t1[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int fi = w + 4 * q;
+    const size_t o = (size_t)(16 * (fi >> 4) + r) * ld + 4 * (fi & 15) + c;
+    t0[q] = ld_sc1(g0 + o);
+    t1[q] = ld_sc1(g1 + o);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    f0[((w + 4 * q) << 6) + lane] = t0[q];
+    f1[((w + 4 * q) << 6) + lane] = t1[q];
+  }
+}
+
 // acc[s] += (rows 16w.., cols 16s.. of X Y^T), X and Y in fragment order
 __device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf, d4 acc[4]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -2923,6 +2966,9 @@ void k_tl3_flow(slam_ba_problem p) {
   __shared__ int shf, okf, col_sh;
   __shared__ double VR[kTB * kVR];        // L_JJ^-1 row-major (stride 65): (3), this column's x
   __shared__ int stk[SLAM_TL_FLOW_MAX_T], sp_sh, cur_sh, last_sh, own_sh;
+#ifdef SLAM_FLOW_PROFILE
+  __shared__ unsigned long long flow_lds[16];
+#endif
   // the column: the start ticket hands them out in the order the workgroups start
   if (threadIdx.x == 0)
     col_sh = (int)ticket_add(reinterpret_cast<uint32_t*>(F.start));
@@ -2989,15 +3035,19 @@ void k_tl3_flow(slam_ba_problem p) {
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) racc[q2][s2] = d4{0.0, 0.0, 0.0, 0.0};
   int rptr[2] = {0, 0};  // next entry of row tile q2's k list (uniform)
+  // The buffers alternate so that the LAST child's L_Jk lands in Xf, which the
+  // factor leaves alone: (2) reuses it for that child's deferred row updates.
   if (sc > 0) {
     ok = flow_wait(F.tile + J * T + S[so], epoch, fail, &shf);
-    if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so] * kTB, L.N, Xf);
+    if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so] * kTB, L.N, ((sc - 1) & 1) ? Yf : Xf);
+    FLOW_S(0);
   }
   for (int q = 0; q < sc && ok; ++q) {
-    double* cur = (q & 1) ? Yf : Xf;
-    double* nxt = (q & 1) ? Xf : Yf;
+    double* cur = ((sc - 1 - q) & 1) ? Yf : Xf;
+    double* nxt = ((sc - 1 - q) & 1) ? Xf : Yf;
     const int k = S[so + q];
     __syncthreads();  // cur filled; the previous MFMAs' reads of nxt done
+    if (q == sc - 1) FLOW_S(1);
     bool pre = false;
     if (q + 1 < sc) {
       if (t == 0) shf = ld_flag(F.tile + J * T + S[so + q + 1]) == epoch ? 1 : 0;
@@ -3069,37 +3119,84 @@ void k_tl3_flow(slam_ba_problem p) {
     __syncthreads();
   }
   FLOW_T(2);
-  // (2) row tiles, parent first
-  for (int q = 0; q < rc && ok; ++q) {
+  // (2) row tiles, parent first.  Rows 0 and 1 (the children folded in during
+  // (1), A_IJ in registers) and the rest are separate straight-line instances:
+  // one uniform branch per row tile, not one per element (this code runs once
+  // per solve on a CU whose instruction cache the LM kernels have refilled, so
+  // every taken branch into cold code costs an L2 fetch).
+  auto row_tile = [&](auto QC, int q) {
+    constexpr int qc = decltype(QC)::value;  // 0, 1: rows 0 / 1; 2: any later row
     const int I = S[ro + q];
     const int ko = S[uo + 2 * q], kc = S[uo + 2 * q + 1];
-    // rows 0 and 1: the children folded in during (1), the rest from here
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) acc[s2] = q == 0 ? racc[0][s2] : (q == 1 ? racc[1][s2] : d4{0.0, 0.0, 0.0, 0.0});
-    for (int u = q < 2 ? rptr[q] : 0; u < kc && ok; ++u) {
+    for (int s2 = 0; s2 < 4; ++s2) {
+      if constexpr (qc < 2) acc[s2] = racc[qc][s2];
+      else acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+    // Rows 0 and 1 have at most the last child left (its L_Jk still in Xf from
+    // (1): only L_Ik is loaded, into Yf); the staged A_IJ goes to Yf so that Xf
+    // keeps L_Jk for row 1.  Later rows load both tiles (loads in flight together)
+    // and stage into Xf.
+    double* stg = qc < 2 ? Yf : Xf;
+    int u0 = 0;
+    if constexpr (qc < 2) u0 = rptr[qc];
+    for (int u = u0; u < kc && ok; ++u) {
       const int k = S[ko + u];
       ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);  // (J, k) was waited for in (1)
       if (!ok) break;
-      tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, Xf);
-      tile_to_frag_sc1(A + (size_t)J * kTB * L.N + k * kTB, L.N, Yf);
-      __syncthreads();
-      gemm_xyT_acc(Xf, Yf, acc);
+      if (qc < 2 && k == S[so + sc - 1]) {
+        tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, Yf);
+        __syncthreads();
+        gemm_xyT_acc(Yf, Xf, acc);
+      } else {
+        // (cannot happen for rows 0 and 1 with the schedule's ordered k lists;
+        // kept general: Xf's L_Jk of the last child is then reloaded below)
+        tiles2_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, A + (size_t)J * kTB * L.N + k * kTB, L.N,
+                           Yf, Xf);
+        __syncthreads();
+        gemm_xyT_acc(Yf, Xf, acc);
+        if (qc < 2 && sc > 0) {
+          __syncthreads();
+          const int kl = S[so + sc - 1];
+          tile_to_frag_sc1(A + (size_t)J * kTB * L.N + kl * kTB, L.N, Xf);
+        }
+      }
       __syncthreads();
     }
-    if (!ok) break;
+    if (!ok) return;
+    if (q == 0) FLOW_S(2);
     double* AIJ = A + (size_t)I * kTB * L.N + J * kTB;
+    double a[16];
+    if constexpr (qc < 2) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a[e] = air[qc][e];
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          a[4 * s2 + r] = AIJ[(size_t)(w * 16 + (lane >> 4) + 4 * r) * L.N + s2 * 16 + (lane & 15)];
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
-        const double a = q == 0 ? air[0][4 * s2 + r] : q == 1 ? air[1][4 * s2 + r]
-                                                             : AIJ[(size_t)row * L.N + col];
-        Xf[frag_idx(row, col)] = a - acc[s2][r];
+        stg[frag_idx(row, col)] = a[4 * s2 + r] - acc[s2][r];
       }
+#ifdef SLAM_FLOW_PROFILE
+    if (q == 0 && lane == 0) flow_lds[w < 3 ? 5 + w : 14] = wall_clock64();
+#endif
     __syncthreads();
+    if (q == 0) FLOW_S(3);
     d4 lacc[4];
-    gemm_xyT_lowY(Xf, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+    gemm_xyT_lowY(stg, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+#ifdef SLAM_FLOW_PROFILE
+    if (q == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      FLOW_S(4);
+    }
+#endif
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
@@ -3108,7 +3205,11 @@ void k_tl3_flow(slam_ba_problem p) {
         st_sc1(AIJ + (size_t)row * L.N + col, lacc[s2][r]);
       }
     flow_publish(F.tile + I * T + J, epoch);
-  }
+    if (q == 0) FLOW_S(5);
+  };
+  if (ok && rc > 0) row_tile(std::integral_constant<int, 0>{}, 0);
+  if (ok && rc > 1) row_tile(std::integral_constant<int, 1>{}, 1);
+  for (int q = 2; q < rc && ok; ++q) row_tile(std::integral_constant<int, 2>{}, q);
   FLOW_T(3);
   // (3) forward substitution: r = b_J - sum_{k in rs(J)} L_Jk y_k, the terms
   // pushed by the children (fc[J][k]); y_J = L_JJ^-1 r; then this column's
@@ -3259,6 +3360,7 @@ void k_tl3_flow(slam_ba_problem p) {
     }
     __syncthreads();
   }
+  FLOW_FLUSH();
   // (5) the workgroup that retired the last column runs the epilogue
   if (!last_sh) return;
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
@@ -3277,7 +3379,7 @@ void k_tl3_flow(slam_ba_problem p) {
   const double* gvec = bvec + n;
   solve_epilogue<true>(p, xs, good, &part[0][0],
                  EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n}, fcode);
-  FLOW_T(7);
+  FLOW_TC(J, 7);
 }
 
 // The dataflow solve makes no residency assumption (k_tl3_flow's comment), so it
@@ -3768,6 +3870,11 @@ extern "C" int slam_linm_stamps(unsigned long long* out, int n) {
 #endif
 
 #ifdef SLAM_FLOW_PROFILE
+extern "C" int slam_flow_sub_stamps(unsigned long long* out, int n_cols) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_flow_sub), (size_t)n_cols * 8 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
 extern "C" int slam_flow_fac_stamps(unsigned long long* out16) {
   SLAM_HIP(hipDeviceSynchronize());
   SLAM_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_flow_fac), 16 * sizeof(unsigned long long)));
