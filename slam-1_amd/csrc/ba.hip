@@ -3098,22 +3098,23 @@ void k_tl3_flow(slam_ba_problem p) {
       }
     double* Xb = VX + kTB * kMS;
     ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf);
-    double x[kTB];
-    if (ok && w == 1) {
+    // L_JJ^-1 out of the block store into fragment order (Vf) and row-major
+    // (VR): wave w takes rows [16w, 16w + 16), lane = column
+    double x[16];
+    if (ok) {
       const int cb16 = lane >> 4;
 #pragma unroll
-      for (int m = 0; m < kTB; ++m)
-        x[m] = (m >> 4) >= cb16 ? Xb[blk_id(m >> 4, cb16) * 16 * kBS17 + (m & 15) * kBS17 + (lane & 15)]
-                                : 0.0;
+      for (int m = 0; m < 16; ++m)
+        x[m] = w >= cb16 ? Xb[blk_id(w, cb16) * 16 * kBS17 + m * kBS17 + (lane & 15)] : 0.0;
     }
     __syncthreads();  // VX is reused below
     if (!ok) {
       if (t == 0) st_flag(fail, 1);
-    } else if (w == 1) {
+    } else {
 #pragma unroll
-      for (int m = 0; m < kTB; ++m) {
-        Vf[frag_idx(m, lane)] = x[m];
-        VR[m * kVR + lane] = x[m];
+      for (int m = 0; m < 16; ++m) {
+        Vf[frag_idx(16 * w + m, lane)] = x[m];
+        VR[(16 * w + m) * kVR + lane] = x[m];
       }
     }
     __syncthreads();
