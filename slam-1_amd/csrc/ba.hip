@@ -1949,6 +1949,33 @@ __device__ __forceinline__ void gemm_xyT_lowY(const double* Xf, const double* Yf
   });
 }
 
+// Fragment order with the offset inside each 64-double fragment F rotated by
+// (4 * (c & 3) + (F & 3)) mod 16 within its 16-row quarter: the MFMA result
+// layout (lanes along a row) then stores without LDS bank conflicts (16-way in
+// plain fragment order: a 16-lane group's doubles all sit 32 dwords apart),
+// and a fragment still reads back conflict-free (a permutation of each quarter).
+__device__ __forceinline__ int frag_swz(int r, int c) {
+  const int F = ((r >> 4) << 4) + (c >> 2), hi = c & 3;
+  return (F << 6) + (hi << 4) + (((r & 15) + 4 * hi + (F & 3)) & 15);
+}
+// gemm_xyT_lowY with both operands in frag_swz order (same products, same order)
+__device__ __forceinline__ void gemm_xyT_lowY_swz(const double* Xf, const double* Yf, d4 acc[4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int so[4];
+#pragma unroll
+  for (int k3 = 0; k3 < 4; ++k3) so[k3] = ((lane >> 4) << 4) + (((lane & 15) + 4 * (lane >> 4) + k3) & 15);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
+  static_for<0, 16>([&](auto K) {
+    constexpr int kk = decltype(K)::value;
+    const double a = Xf[((w * 16 + kk) << 6) + so[kk & 3]];
+    static_for<kk / 4, 4>([&](auto S) {
+      constexpr int s = decltype(S)::value;
+      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + so[kk & 3]], acc[s], 0, 0, 0);
+    });
+  });
+}
+
 __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayout& L) {
   return *reinterpret_cast<const volatile int*>(p.chol + L.fail) != 0;
 }
@@ -3098,8 +3125,8 @@ void k_tl3_flow(slam_ba_problem p) {
       }
     double* Xb = VX + kTB * kMS;
     ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf);
-    // L_JJ^-1 out of the block store into fragment order (Vf) and row-major
-    // (VR): wave w takes rows [16w, 16w + 16), lane = column
+    // L_JJ^-1 out of the block store into (swizzled) fragment order (Vf) and
+    // row-major (VR): wave w takes rows [16w, 16w + 16), lane = column
     double x[16];
     if (ok) {
       const int cb16 = lane >> 4;
@@ -3113,7 +3140,7 @@ void k_tl3_flow(slam_ba_problem p) {
     } else {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
-        Vf[frag_idx(16 * w + m, lane)] = x[m];
+        Vf[frag_swz(16 * w + m, lane)] = x[m];
         VR[(16 * w + m) * kVR + lane] = x[m];
       }
     }
@@ -3183,7 +3210,7 @@ void k_tl3_flow(slam_ba_problem p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
-        stg[frag_idx(row, col)] = a[4 * s2 + r] - acc[s2][r];
+        stg[frag_swz(row, col)] = a[4 * s2 + r] - acc[s2][r];
       }
 #ifdef SLAM_FLOW_PROFILE
     if (q == 0 && lane == 0) flow_lds[w < 3 ? 5 + w : 14] = wall_clock64();
@@ -3191,7 +3218,7 @@ void k_tl3_flow(slam_ba_problem p) {
     __syncthreads();
     if (q == 0) FLOW_S(3);
     d4 lacc[4];
-    gemm_xyT_lowY(stg, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+    gemm_xyT_lowY_swz(stg, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
 #ifdef SLAM_FLOW_PROFILE
     if (q == 0) {
       __builtin_amdgcn_s_waitcnt(0);
