@@ -2368,23 +2368,27 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     }
   }
   bool ok = true;
-  int* lflag = reinterpret_cast<int*>(Tb + 3 * 16 * kBS17);  // L_32 published (waves 1-3 wait)
-  if (t == 0) *lflag = 0;
+  // wave-to-wave hand-offs inside the tile (LDS flags, raised once per call):
+  // 0: L_10, 1: L_20, 2: L_30, 3: L_21, 4: L_31, 5: L_32 stored
+  int* fl = reinterpret_cast<int*>(Tb + 3 * 16 * kBS17);
+  if (t < 6) fl[t] = 0;
   __syncthreads();
   TL_STAMP(1);
   FAC_T(0);
   // One loop over the block columns with ONE instance of wave 0's 16x16 code
   // (an instance per block column measured 0.4-1.0 us slower per block: the
   // unrolled factor is ~16 KB of code and the copies missed the instruction
-  // cache).  Block columns 0 and 1: wave 0 factors the diagonal block, then
-  // every wave takes a panel block and trailing blocks (workgroup barriers
-  // between).  Block columns 2 and 3 are wave 0's chain alone (block 2's
-  // factor, the last panel block L_32 and trailing block A_33, block 3's
-  // factor: no workgroup barrier on it).  Waves 1-3 assemble L^-1 beside it,
-  // block by block as its inputs appear, so that after block 3's factor only
-  // X_3p = -X_33 T_3p is left (one 16x16 product per wave):
-  //   X_ip = -X_ii T_ip,  T_ip = sum_{k=p}^{i-1} L_ik X_kp  (k ascending: the
-  //   same sums in the same order as the level-by-level form, bit-identical).
+  // cache).  Wave 0 runs the critical chain with look-ahead: before block p's
+  // factor it forms the panel block L_{p,p-1} and the trailing block A_pp
+  // itself, so the only workgroup barrier per block column is the one that
+  // publishes X_pp.  Waves 1-3 take the other panel and trailing blocks of
+  // block column p-1 beside block p's factor (LDS flags for the blocks one
+  // wave forms and another reads) and assemble L^-1 block by block as its
+  // inputs appear, so that after block 3's factor only X_3p = -X_33 T_3p is
+  // left (one 16x16 product per wave):
+  //   X_ip = -X_ii T_ip,  T_ip = sum_{k=p}^{i-1} L_ik X_kp  (k ascending).
+  // Every block gets the same updates in the same order as the column-by-column
+  // form: bit-identical.
   const d4 z = d4{0.0, 0.0, 0.0, 0.0};
   auto T_of = [&](int i, int p, int k_end) {  // sum_{k=p}^{k_end-1} L_ik X_kp
     d4 acc = z;
@@ -2399,68 +2403,78 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     st16(Xb + blk_id(i, p) * 16 * kBS17, kBS17, mm16_xy(Xb + blk_id(i, i) * 16 * kBS17, kBS17, Tw, kBS17, z, true));
     wave_lds_fence();
   };
+  auto Mb = [&](int i, int j) { return M + (16 * i) * kMS + 16 * j; };
+  auto panel = [&](int i, int p) {  // L_ip = A_ip X_pp^T, in place
+    st16(Mb(i, p), kMS, mm16_xyT(Mb(i, p), kMS, Xb + blk_id(p, p) * 16 * kBS17, kBS17, z, false));
+    wave_lds_fence();
+  };
+  auto trail = [&](int i, int j, int p) {  // A_ij -= L_ip L_jp^T
+    st16(Mb(i, j), kMS, mm16_xyT(Mb(i, p), kMS, Mb(j, p), kMS, ld16(Mb(i, j), kMS), true));
+    wave_lds_fence();
+  };
+  auto put = [&](int f) {  // this wave's LDS stores before it, then flag f
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (l == 0) __hip_atomic_store(fl + f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto get = [&](int f) {
+    while (__hip_atomic_load(fl + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
   d4 T3 = z;
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
-      if (p == 3) {  // the last panel and trailing blocks, then block 3's factor
-        double* A32 = M + 48 * kMS + 32;
-        st16(A32, kMS, mm16_xyT(A32, kMS, Xb + blk_id(2, 2) * 16 * kBS17, kBS17, z, false));
-        wave_lds_fence();
-        FAC_T(8);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (l == 0) __hip_atomic_store(lflag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        double* A33 = M + 48 * kMS + 48;
-        st16(A33, kMS, mm16_xyT(A32, kMS, A32, kMS, ld16(A33, kMS), true));
-        wave_lds_fence();
-        FAC_T(9);
+      if (p > 0) {  // look-ahead: L_{p,p-1}, then A_pp's last update
+        panel(p, p - 1);
+        put(p == 1 ? 0 : (p == 2 ? 3 : 5));
+        trail(p, p, p - 1);
       }
       blk_factor_w0(M, Xb, p, ok);
-    } else if (p == 2) {
-      if (w == 1) X_from(1, 0, T_of(1, 0, 1));  // X_10 (X_00, X_11, L_10 final after block column 1)
+    } else if (p == 1) {  // block column 0's other panel and trailing blocks
+      if (w == 1) {
+        panel(2, 0);
+        put(1);
+        trail(2, 2, 0);
+        get(0);
+        trail(2, 1, 0);
+      } else if (w == 2) {
+        panel(3, 0);
+        put(2);
+        trail(3, 3, 0);
+        get(0);
+        trail(3, 1, 0);
+      } else {
+        get(1);
+        get(2);
+        trail(3, 2, 0);
+      }
+    } else if (p == 2) {  // block column 1's, and X_10
+      if (w == 1) {
+        panel(3, 1);
+        put(4);
+        trail(3, 3, 1);
+      } else if (w == 2) {
+        get(3);
+        get(4);
+        trail(3, 2, 1);
+      } else {
+        X_from(1, 0, T_of(1, 0, 1));  // X_10 (X_00, X_11: published by the barriers)
+      }
     } else if (p == 3) {
       if (w == 1) X_from(2, 1, T_of(2, 1, 2));  // X_21
       if (w == 2) X_from(2, 0, T_of(2, 0, 2));  // X_20 (needs X_10: published by the barrier)
-      // T_3p needs L_32 (wave 0's panel block above)
-      while (__hip_atomic_load(lflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
-        __builtin_amdgcn_s_sleep(1);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       // wave 1: T_31, wave 2: T_30, wave 3: T_32 (each wave reads only the X
-      // blocks it formed itself or that the barrier published)
+      // blocks it formed itself or that the barrier published), after L_32
+      get(5);
       T3 = T_of(3, w == 1 ? 1 : (w == 2 ? 0 : 2), 3);
     }
-    if (p == 2) {
-      __syncthreads();  // X_22 (and X_10) published
-      FAC_T(7);
+    if (p < 3) {
+      __syncthreads();  // X_pp and block column p-1's blocks published
+      FAC_T(1 + 3 * p);
+      FAC_T(2 + 3 * p);
+      FAC_T(3 + 3 * p);
     }
-    if (p >= 2) continue;  // (uniform)
-    __syncthreads();
-    FAC_T(1 + 3 * p);
-    // panel: L_ip = A_ip X_pp^T (one block per wave)
-    const int ip = p + 1 + w;
-    if (ip < 4) {
-      double* Aip = M + (16 * ip) * kMS + 16 * p;
-      const d4 acc = mm16_xyT(Aip, kMS, Xb + blk_id(p, p) * 16 * kBS17, kBS17, z, false);
-      st16(Aip, kMS, acc);
-    }
-    __syncthreads();
-    FAC_T(2 + 3 * p);
-    // trailing: A_ij -= L_ip L_jp^T for p < j <= i <= 3
-    const int nt = (3 - p) * (4 - p) / 2;
-    for (int q = w; q < nt; q += 4) {
-      int i = p + 1, rem = q;
-      while (rem >= i - p) {
-        rem -= i - p;
-        ++i;
-      }
-      const int j = p + 1 + rem;
-      double* Aij = M + (16 * i) * kMS + 16 * j;
-      d4 acc = ld16(Aij, kMS);
-      acc = mm16_xyT(M + (16 * i) * kMS + 16 * p, kMS, M + (16 * j) * kMS + 16 * p, kMS, acc, true);
-      st16(Aij, kMS, acc);
-    }
-    __syncthreads();
-    FAC_T(3 + 3 * p);
   }
   FAC_T(10);
   FAC_T(11);
