@@ -3391,14 +3391,32 @@ void k_tl3_flow(slam_ba_problem p) {
     // still complete; the epilogue sees the fail code)
     flow_publish(F.xf + k, epoch);
     FLOW_TC(k, 6);
-    if (t == 0) {
-      for (int u = 0; u < ksc; ++u) {
-        const int c = S[kso + u];  // k is a row tile of column c
-        const int rcc = S[S[5] + 5 * c + 1];
-        const unsigned old = ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c));
-        if ((int)(old & 0xffffu) == rcc - 1 && (old >> 16) == 0) stk[sp_sh++] = c;
+    // the parent counters (one lane each) and the retire ticket in flight
+    // together -- they are independent, and a chain of returning atomics cost
+    // a device round trip each on the back substitution's critical path; the
+    // columns this retire completes go on the stack in u order as before
+    if (t < 64) {
+      for (int u0 = 0; u0 == 0 || u0 < ksc; u0 += 64) {
+        const int u = u0 + t;
+        int c = 0, rcc = 0;
+        unsigned old = 0, oldt = 0;
+        if (u < ksc) {
+          c = S[kso + u];  // k is a row tile of column c
+          rcc = S[S[5] + 5 * c + 1];
+          old = ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c));
+        }
+        if (u0 == 0 && t == 0) oldt = ticket_add(reinterpret_cast<uint32_t*>(F.ticket));
+        const bool push = u < ksc && (int)(old & 0xffffu) == rcc - 1 && (old >> 16) == 0;
+        const unsigned long long m = __ballot(push);
+        const int base = sp_sh;
+        if (push) stk[base + __popcll(m & ((1ull << t) - 1ull))] = c;
+        wave_lds_fence();
+        if (t == 0) {
+          sp_sh = base + __popcll(m);
+          if (u0 == 0 && oldt == (unsigned)(T - 1)) last_sh = 1;
+        }
+        wave_lds_fence();
       }
-      if (ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1)) last_sh = 1;
     }
     __syncthreads();
   }
