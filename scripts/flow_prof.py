@@ -60,6 +60,14 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
             print(f"  col {J:3d}: " + " ".join(f"{sub[J, i]:7.1f}" for i in (0, 1)) + f" {rel[J, 2]:7.1f} " +
                   " ".join(f"{sub[J, i]:7.1f}" for i in (2, 3, 4, 5)) + " | " + last_in +
                   f" | staging at the barrier: wave 0 {sub[J, 6]:7.1f}, waves 1-3 {sub[J, 7]:7.1f}")
+    fe = getattr(_lib.lib, "slam_flow_epi_stamps", None)
+    if fe is not None:
+        fe.argtypes = [ctypes.c_void_p]
+        eb = (ctypes.c_ulonglong * 4)()
+        fe(ctypes.cast(eb, ctypes.c_void_p))
+        ev = (np.array(eb[:], np.float64) - float(t0)) * 10 / 1000.0
+        print(f"  epilogue (us, absolute): start {ev[0]:.1f}, x staged {ev[1]:.1f}, pc / cost reduced {ev[2]:.1f},"
+              f" cameras prepared {ev[3]:.1f}")
     ff = getattr(_lib.lib, "slam_flow_fac_stamps", None)
     if ff is not None:
         fb = (ctypes.c_ulonglong * 16)()

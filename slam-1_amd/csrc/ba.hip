@@ -1323,6 +1323,10 @@ constexpr int kSolveHdr = 32;   // doubles of LDS header in k_solve_blk
 struct EpiSrc {
   const double *g, *dU, *cam, *costc;
 };
+#ifdef SLAM_FLOW_PROFILE
+// the dataflow solve's epilogue: start, x staged, pc / cost reduced, cameras prepared
+__device__ unsigned long long g_flow_epi[4];
+#endif
 
 // Shared epilogue: camera step, trial cameras, predicted reduction of the camera
 // part, LM cost at the live parameters.  GLOBAL (the tiled solves, 9C up to
@@ -1389,6 +1393,9 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
     }
     for (int c = t; c < p.n_cams; c += nt) cost += e.costc[c];
     block_sum2(pc, cost, red);  // (its barriers also publish the trial cameras to the WG)
+#ifdef SLAM_FLOW_PROFILE
+    if (t == 0) g_flow_epi[2] = wall_clock64();
+#endif
   } else {
     for (int i = t; i < C9; i += blockDim.x) {
       const double d = ok ? x[i] : 0.0;
@@ -1402,6 +1409,13 @@ __device__ void solve_epilogue(const slam_ba_problem& p, const double* x, bool o
   }
   for (int c = t; c < p.n_cams; c += blockDim.x)
     cam_prep(p.cams[1 - cur] + 9 * c, p.camrec[1 - cur] + kCamRec * c);
+#ifdef SLAM_FLOW_PROFILE
+  if (GLOBAL) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (t == 0) g_flow_epi[3] = wall_clock64();
+  }
+#endif
   if (t == 0) {
     state[SLAM_BA_ST_COST] = 0.5 * cost;
     state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
@@ -3423,6 +3437,9 @@ void k_tl3_flow(slam_ba_problem p) {
   FLOW_FLUSH();
   // (5) the workgroup that retired the last column runs the epilogue
   if (!last_sh) return;
+#ifdef SLAM_FLOW_PROFILE
+  if (t == 0) g_flow_epi[0] = wall_clock64();
+#endif
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
   const bool good = fcode == 0;
   double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
@@ -3435,6 +3452,9 @@ void k_tl3_flow(slam_ba_problem p) {
       if (i0 + q * kTlWG < n) xs[i0 + q * kTlWG] = xv[q];
   }
   __syncthreads();
+#ifdef SLAM_FLOW_PROFILE
+  if (t == 0) g_flow_epi[1] = wall_clock64();
+#endif
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
   const double* gvec = bvec + n;
   solve_epilogue<true>(p, xs, good, &part[0][0],
@@ -3930,6 +3950,11 @@ extern "C" int slam_linm_stamps(unsigned long long* out, int n) {
 #endif
 
 #ifdef SLAM_FLOW_PROFILE
+extern "C" int slam_flow_epi_stamps(unsigned long long* out4) {
+  SLAM_HIP(hipDeviceSynchronize());
+  SLAM_HIP(hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_flow_epi), 4 * sizeof(unsigned long long)));
+  return SLAM_OK;
+}
 extern "C" int slam_flow_sub_stamps(unsigned long long* out, int n_cols) {
   SLAM_HIP(hipDeviceSynchronize());
   SLAM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_flow_sub), (size_t)n_cols * 8 * sizeof(unsigned long long)));
