@@ -420,7 +420,7 @@ def run_tracking(args, world, rank):
     # 14.3k vs 15.5-15.7k tracked frames/s, alternating runs, profiles/r5/tracked_leg)
     TRK_LAG = args.tracked_lag
     leg = {"tracked": False}
-    tleg = {"wms": None, "ws": None, "build_s": [], "wait_s": [], "shapes": [], "modes": {}, "sets": []}
+    tleg = {"wms": None, "ws": None, "build_s": [], "wait_s": [], "shapes": [], "modes": {}}
 
     ba_done = [None]
     step_no, pending = [0], [0]
@@ -463,14 +463,9 @@ def run_tracking(args, world, rank):
             for g in groups.values():
                 for i in range(0, len(g), BABatch.MAX_BATCH):
                     BABatch(g[i:i + BABatch.MAX_BATCH], stream=ba_stream).iterate(args.ba_iters)
-        # the sets' device memory was allocated on the upload stream and is read on
-        # the BA stream: a set is released only once the BA stream has finished it
-        done = torch.cuda.Event()
-        done.record(ba_stream)
-        tleg["sets"].append((bps, done))
-        while len(tleg["sets"]) > 2:
-            tleg["sets"][0][1].synchronize()  # (finished long ago: two steps back)
-            tleg["sets"].pop(0)
+        # BAWindowSet double-buffers its device memory: these problems stay valid
+        # through the next stage() call (the one after reuses their buffers and
+        # they raise from then on); the last set's states are read after the loop
         tleg["last"] = bps
         if bmarks is not None:
             bmarks.append(("local_ba", ev_on(ba_stream)))
@@ -609,7 +604,7 @@ def run_tracking(args, world, rank):
                    "note": ("local BA on windows built from the bench's own tracked frames (lag 2: "
                             "host build of step k-2's windows overlaps step k's tracking); not the headline")}
         torch.cuda.synchronize()
-        tleg["wms"], tleg["sets"], tleg["last"] = None, [], None
+        tleg["wms"], tleg["last"] = None, None
     frames = reduce_scalar(float(B * args.steps), world, "sum")
     cnt = trk.counters()  # raises on any ORB workspace overflow since the start
     # accuracy of the tracked trajectory (the last tracked window; the device
@@ -1249,10 +1244,10 @@ def main():
     ap.add_argument("--lin-mode", default="auto", choices=["auto", "mfma", "slot"],
                     help="BA linearisation: camera-union MFMA kernel or the slot kernel")
     ap.add_argument("--chunks-per-wg", type=int, default=None,
-                    help="camera-union linearisation: chunks per workgroup (default: 8 for the "
-                         "tracking workload's batched windows -- 3 / 4 / 5 / 6 / 8 / 12 / 16 "
-                         "measured 20.2k / 20.4k / 20.5k / 20.5k / 20.6k / 20.6k / 20.5k "
-                         "frames/s, round-4 sweep in git history at f26058c; auto elsewhere)")
+                    help="camera-union linearisation: chunks per workgroup (default: 16 for the "
+                         "tracking workload's batched windows -- 8 / 16 / 32 measured 22.0-22.3k "
+                         "/ 22.3-22.5k / 21.1-21.2k frames/s, round-5 sweep profiles/r5/cpw_ab; "
+                         "auto elsewhere)")
     ap.add_argument("--ba-streams", type=int, default=1,
                     help="split the local-BA windows over this many streams (tracking, and "
                          "--workload ba --ba-batch N)")
@@ -1318,6 +1313,8 @@ def main():
     ap.add_argument("--ba-cus", type=int, default=0,
                     help="disjoint CU partition: local BA on the last N CUs, tracking on the rest")
     args = ap.parse_args()
+    if args.tracked_lag < 1:
+        ap.error("--tracked-lag must be >= 1 (0 would stage the window mapper the same step fills)")
     if args.batch is None:
         args.batch = 64 if args.workload == "tracking" else 32
     if args.windows is None:  # global steps in the sequence (each world * batch pairs)

@@ -2008,7 +2008,8 @@ __device__ __forceinline__ bool tl_failed(const slam_ba_problem& p, const TlLayo
 // the last pivot only one 16x16 product per wave is left (the assembly after
 // the factor was 2.2 us of 13.0 per tile; 0.44 now).  M: LDS [64][65] (A, then
 // L's off-diagonal blocks), Xb: LDS [10][16][17] (lower blocks of L^-1), Tb:
-// LDS [3][16][17] scratch + one int (L_32 published).  Every wave must call
+// LDS [3][16][17] scratch + six int flags (the wave-to-wave hand-offs of
+// L_10 .. L_32, right after the scratch).  Every wave must call
 // it; returns false (uniform) on a non-positive or non-finite pivot.
 constexpr int kMS = 65;   // row stride of M (odd: MFMA operand reads spread over banks)
 constexpr int kVR = 65;   // row stride of k_tl3_flow's row-major L_JJ^-1
@@ -2384,6 +2385,9 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
   bool ok = true;
   // wave-to-wave hand-offs inside the tile (LDS flags, raised once per call):
   // 0: L_10, 1: L_20, 2: L_30, 3: L_21, 4: L_31, 5: L_32 stored
+  // callers pass M = VX, Xb = VX + kTB * kMS, Tb = Xb + 10 * 16 * kBS17 of a
+  // VX[2 * kTB * kTB]: M + Xb + Tb + the six flags (3 doubles) must fit in it
+  static_assert(kTB * kMS + 13 * 16 * kBS17 + 3 <= 2 * kTB * kTB, "tile factor LDS layout overflows VX");
   int* fl = reinterpret_cast<int*>(Tb + 3 * 16 * kBS17);
   if (t < 6) fl[t] = 0;
   __syncthreads();

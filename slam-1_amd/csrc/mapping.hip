@@ -223,9 +223,11 @@ extern "C" int slam_map_windows(double* d_maps, int32_t* d_M, int map_cap, int n
   SLAM_HIP(hipMemsetAsync(d_M, 0, sizeof(int32_t) * (size_t)n_win, s));
   // pair j of every window in one launch pair (the windows are independent;
   // within a window the pairs stay in order): per window its own map, size,
-  // rows and a workspace slice of nch_max x cap partials
+  // rows and a workspace slice of nch_max x cap partials -- the slice ws_bytes
+  // sizes per window (none when n == 1: pair 0 meets an empty map, k_map_nn
+  // never runs and k_map_assoc reads no partials)
   const int nch_max = ((n - 1) * cap + kNnChunk - 1) / kNnChunk;
-  const size_t part = (size_t)std::max(nch_max, 1) * cap;
+  const size_t part = (size_t)nch_max * cap;
   double* part_d2 = static_cast<double*>(d_ws);
   int32_t* part_idx = reinterpret_cast<int32_t*>(part_d2 + (size_t)n_win * part);
   const WinStride wst{(size_t)map_cap * 3, (size_t)n * cap, (size_t)n, part};

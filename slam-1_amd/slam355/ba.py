@@ -988,6 +988,9 @@ class BABatch:
             ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(p._s), ctypes.sizeof(_Prob))
         self._arr = arr
         self._graphs = {}
+        # BAWindowSet problems: checked before every launch (their buffers are
+        # reused two stage()/build() calls later)
+        self._win = [p for p in self.problems if hasattr(p, "_live")]
 
     def _sp(self):
         return stream_ptr(self.stream)
@@ -1007,11 +1010,15 @@ class BABatch:
         self.reset(lam0)
 
     def iterate(self, n: int = 1):
+        for p in self._win:
+            p._live()
         _lib.call("slam_ba_iterate_batch", self._arr, len(self.problems), int(n), self._sp())
 
     def iterate_graphed(self, n: int = 1, with_restore=False):
         """n LM iterations of every problem (optionally preceded by restore())
         replayed from one captured HIP graph."""
+        for p in self._win:
+            p._live()
         key = (n, with_restore)
         if key not in self._graphs:
             g = torch.cuda.CUDAGraph()
@@ -1061,16 +1068,33 @@ def residuals(cams, pts, cam_idx, pt_idx, qs, *, jacobian=False):
 
 
 class _WindowProblem(BAProblem):
-    """A BAProblem whose buffers are views into a BAWindowSet's shared device
-    memory (built by BAWindowSet.build, not by __init__).  The kernels see raw
+    """A BAProblem whose buffers are views into a BAWindowSet's device memory
+    (built by BAWindowSet.build / stage, not by __init__).  The kernels see raw
     pointers set at build time; the torch views (`t`, `_init`) that the
-    BAProblem methods read are made on first use only."""
+    BAProblem methods read are made on first use only.
+
+    Lifetime: the set double-buffers its device memory, so the problems of one
+    call stay valid through the next call; the call after that reuses their
+    buffers, and from then on every use of them (launches, `state()`,
+    `params()`, a new BABatch over them) raises RuntimeError instead of
+    silently reading another batch's data."""
 
     def __init__(self):  # noqa: D107 (constructed by BAWindowSet only)
         pass
 
+    def _live(self):
+        if self._ws.gen[self._slot] != self._gen:
+            raise RuntimeError("BAWindowSet problem used after its device buffers were reused "
+                               "(problems stay valid for one further stage()/build() call)")
+
+    @property
+    def _s(self):
+        self._live()
+        return self._s_raw
+
     @property
     def t(self):
+        self._live()
         if self._t is None:
             if self._views is None:  # staged by BAWindowSet.stage: offsets from its meta row
                 self._views = BAWindowSet._views_of(self._d64, self._d32, self._meta)
@@ -1112,16 +1136,33 @@ class BAWindowSet:
     that need the slot linearisation (a point seen by more than MF_CAMS
     cameras) or the tiled solve (9C > 120) are built as ordinary BAProblems.
 
-    The device buffers are reused call after call: a call's upload is ordered on
-    `stream` after the launches of the previous call's problems (same stream),
-    and the host staging buffers alternate between two sets, each reused only
-    after its previous upload has run (an event)."""
+    Two sets of buffers alternate call by call -- pinned host staging and
+    device memory alike -- so a call's problems stay valid through the next
+    call (the bench's lag-2 pipeline launches step k's set while step k+1's
+    is staged).  Set s is reused two calls later: its upload is ordered on
+    `stream` after the launches of the problems it held (same stream), its
+    host staging only after its previous upload has run (an event), and its
+    generation is bumped, so the old problems then raise on any use
+    (_WindowProblem._live) rather than read the new batch's data."""
 
     def __init__(self):
         self.dev = require_gpu()
-        self.d_f64 = self.d_i32 = None
-        self.h = [None, None]  # (f64, i32, event) per staging set
+        self.d = [[None, None], [None, None]]  # (f64, i32) device buffers per set
+        self.h = [None, None]  # (f64, i32, event) host staging per set
+        self.gen = [0, 0]  # calls that have filled each set
         self.k = 0
+
+    def _claim(self):
+        """The set this call fills: its generation bumped (the problems of its
+        previous fill are dead from here on)."""
+        slot = self.k & 1
+        self.gen[slot] += 1
+        return slot
+
+    def _window(self, slot):
+        bp = _WindowProblem()
+        bp._ws, bp._slot, bp._gen = self, slot, self.gen[slot]
+        return bp
 
     @staticmethod
     def _al(n):
@@ -1172,16 +1213,18 @@ class BAWindowSet:
         probs = (_Prob * W)()
         args = (W, n, cap, rows.ctypes.data, cnt.ctypes.data, maps.ctypes.data, map_cap,
                 M.ctypes.data, cams.ctypes.data, float(u_off), float(v_off))
-        hs = self.h[self.k & 1]
+        slot = self._claim()
+        d = self.d[slot]
+        hs = self.h[slot]
         if hs is not None:
             hs[2].synchronize()  # that set's previous upload has run
         for attempt in range(2):
-            ok64 = hs is not None and self.d_f64 is not None and hs[0].numel() <= self.d_f64.numel()
-            ok32 = hs is not None and self.d_i32 is not None and hs[1].numel() <= self.d_i32.numel()
+            ok64 = hs is not None and d[0] is not None and hs[0].numel() <= d[0].numel()
+            ok32 = hs is not None and d[1] is not None and hs[1].numel() <= d[1].numel()
             if ok64 and ok32:
                 _lib.call("slam_ba_stage_windows", *args, hs[0].data_ptr(), hs[0].numel(),
-                          hs[1].data_ptr(), hs[1].numel(), self.d_f64.data_ptr(),
-                          self.d_i32.data_ptr(), ctypes.addressof(probs), meta.ctypes.data,
+                          hs[1].data_ptr(), hs[1].numel(), d[0].data_ptr(),
+                          d[1].data_ptr(), ctypes.addressof(probs), meta.ctypes.data,
                           need.ctypes.data)
             else:
                 _lib.call("slam_ba_stage_windows", *args, None, 0, None, 0, None, None, None,
@@ -1189,25 +1232,25 @@ class BAWindowSet:
             n64, n32 = int(need[0]), int(need[1])
             if ok64 and ok32 and n64 <= hs[0].numel() and n32 <= hs[1].numel():
                 break
-            # grow: pinned staging of this set and the shared device buffers (both
-            # sized alike, so the device addresses written above stay valid)
+            # grow: pinned staging of this set and its device buffers (both sized
+            # alike, so the device addresses written above stay valid)
             sz64, sz32 = max(n64, 1) * 3 // 2, max(n32, 1) * 3 // 2
             hs = [torch.zeros(sz64, dtype=torch.float64, pin_memory=True),
                   torch.zeros(sz32, dtype=torch.int32, pin_memory=True), torch.cuda.Event()]
-            self.h[self.k & 1] = hs
+            self.h[slot] = hs
             with torch.cuda.stream(stream):
-                if self.d_f64 is None or self.d_f64.numel() < sz64:
-                    self.d_f64 = torch.empty(sz64, dtype=torch.float64, device=self.dev)
-                if self.d_i32 is None or self.d_i32.numel() < sz32:
-                    self.d_i32 = torch.empty(sz32, dtype=torch.int32, device=self.dev)
+                if d[0] is None or d[0].numel() < sz64:
+                    d[0] = torch.empty(sz64, dtype=torch.float64, device=self.dev)
+                if d[1] is None or d[1].numel() < sz32:
+                    d[1] = torch.empty(sz32, dtype=torch.int32, device=self.dev)
         else:
             raise RuntimeError("stage: staging buffers could not be sized")
         self.k += 1
         with torch.cuda.stream(stream):
             if n64:
-                self.d_f64[:n64].copy_(hs[0][:n64], non_blocking=True)
+                d[0][:n64].copy_(hs[0][:n64], non_blocking=True)
             if n32:
-                self.d_i32[:n32].copy_(hs[1][:n32], non_blocking=True)
+                d[1][:n32].copy_(hs[1][:n32], non_blocking=True)
             hs[2].record(stream)
         out = []
         for w in range(W):
@@ -1219,13 +1262,13 @@ class BAWindowSet:
                                      om[:, 0].astype(np.int64), om[:, 1].astype(np.int64), qs,
                                      lam0=lam0, stream=stream))
                 continue
-            bp = _WindowProblem()
+            bp = self._window(slot)
             bp._t, bp._perm, bp._views = None, None, None
-            bp._d64, bp._d32, bp._meta = self.d_f64, self.d_i32, m
+            bp._d64, bp._d32, bp._meta = d[0], d[1], m
             bp.plan, bp.lin_mode = None, "mfma"
             bp.C, bp.P, bp.O, bp.stream = int(m[1]), int(m[2]), int(m[3]), stream
             bp.sys_len, bp.tl_levels = int(m[11]), False
-            bp._s = probs[w]
+            bp._s_raw = probs[w]
             out.append(bp)
         built = [p for p in out if isinstance(p, _WindowProblem)]
         for i in range(0, len(built), BABatch.MAX_BATCH):
@@ -1265,14 +1308,16 @@ class BAWindowSet:
             n32 += self._al(len(pl["buf"]) + 8)  # plan tables, 4 one-element stand-ins, ticket
             specs.append((w, C, P, pl, up, o64, o32))
         # staging (pinned, alternating sets) and device buffers (grown as needed)
-        hs = self.h[self.k & 1]
+        slot = self._claim()
+        d = self.d[slot]
+        hs = self.h[slot]
         if hs is not None:
             hs[2].synchronize()  # that set's previous upload has run
         if hs is None or hs[0].numel() < n64 or hs[1].numel() < n32:
             hs = [torch.zeros(max(n64, 1) * 3 // 2, dtype=torch.float64, pin_memory=True),
                   torch.zeros(max(n32, 1) * 3 // 2, dtype=torch.int32, pin_memory=True),
                   torch.cuda.Event()]
-            self.h[self.k & 1] = hs
+            self.h[slot] = hs
         self.k += 1
         h64, h32 = hs[0].numpy(), hs[1].numpy()
         h64[:n64] = 0.0
@@ -1283,23 +1328,23 @@ class BAWindowSet:
             h32[o32:o32 + nb] = pl["buf"]
             h32[o32 + nb:o32 + nb + 8] = 0
         with torch.cuda.stream(stream):
-            if self.d_f64 is None or self.d_f64.numel() < n64:
-                self.d_f64 = torch.empty(max(n64, 1) * 3 // 2, dtype=torch.float64, device=self.dev)
-            if self.d_i32 is None or self.d_i32.numel() < n32:
-                self.d_i32 = torch.empty(max(n32, 1) * 3 // 2, dtype=torch.int32, device=self.dev)
-            self.d_f64[:n64].copy_(hs[0][:n64], non_blocking=True)
-            self.d_i32[:n32].copy_(hs[1][:n32], non_blocking=True)
+            if d[0] is None or d[0].numel() < n64:
+                d[0] = torch.empty(max(n64, 1) * 3 // 2, dtype=torch.float64, device=self.dev)
+            if d[1] is None or d[1].numel() < n32:
+                d[1] = torch.empty(max(n32, 1) * 3 // 2, dtype=torch.int32, device=self.dev)
+            d[0][:n64].copy_(hs[0][:n64], non_blocking=True)
+            d[1][:n32].copy_(hs[1][:n32], non_blocking=True)
             hs[2].record(stream)
         out = [None] * len(problems)
-        b64, b32 = self.d_f64.data_ptr(), self.d_i32.data_ptr()
+        b64, b32 = d[0].data_ptr(), d[1].data_ptr()
         for w, C, P, pl, up, o64, o32 in specs:
             # raw pointers from the offsets (no torch view per buffer: ~30 per
             # window were most of the host build); the views are made on demand
-            bp = _WindowProblem()
+            bp = self._window(slot)
             nb = len(pl["buf"])
             offs = pl["offs"]
             bp._t, bp._perm = None, None
-            bp._views = (self.d_f64, self.d_i32, o64, o32, nb, offs)
+            bp._views = (d[0], d[1], o64, o32, nb, offs)
             bp.plan, bp.lin_mode, bp.perm = pl, "mfma", pl["perm"]
             bp.C, bp.P, bp.O, bp.stream = C, P, pl["n_obs"], stream
             bp.sys_len, bp.tl_levels = int(o64["sys"][1][0]), False
@@ -1318,7 +1363,7 @@ class BAWindowSet:
             for k in ("obs_q", "cpart", "bpart", "sys", "chol", "delta_c", "red_part", "small", "state"):
                 setattr(s, k, f64p(k))
             s.ticket = b32 + 4 * (o32 + nb + 4)
-            bp._s = s
+            bp._s_raw = s
             out[w] = bp
         it = iter(extra)
         out = [p if p is not None else next(it) for p in out]

@@ -924,15 +924,27 @@ def test_gpu_window_set_equals_separate_problems():
         probs.append((c0, p0, ci, pi, qs))
     s = torch.cuda.Stream()
     ws = ba.BAWindowSet()
-    runs = []
+    runs, sets = [], []
     for _ in range(2):
         got = ws.build(probs, s)
+        sets.append(got)
         assert [p.lin_mode for p in got] == ["mfma", "mfma", "mfma", "slot"]
         with torch.cuda.stream(s):
             ba.BABatch(got[:3], stream=s).iterate(4)
             got[3].iterate(4)
         torch.cuda.synchronize()
         runs.append([p.params() for p in got])
+    # double-buffered device memory: the first call's problems are still valid
+    # after the second call, and dead (they raise) once a third call reuses them
+    assert all(np.array_equal(a[0], b[0]) for a, b in zip(runs[0], [p.params() for p in sets[0]]))
+    b0 = ba.BABatch(sets[0][:3], stream=s)
+    ws.build(probs, s)
+    for bad in (lambda: sets[0][0].params(), lambda: sets[0][1].state(), lambda: b0.iterate(1),
+                lambda: ba.BABatch(sets[0][:3], stream=s)):
+        with pytest.raises(RuntimeError, match="reused"):
+            bad()
+    assert sets[0][3].params() is not None  # an ordinary BAProblem owns its buffers
+    sets[1][0].params()  # the second call's set is still live
     for w, pr in enumerate(probs):
         ref = ba.BAProblem(*pr)
         ref.iterate(4)

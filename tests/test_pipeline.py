@@ -180,19 +180,21 @@ def corridor9():
 
 
 @pytest.mark.gpu
-def test_gpu_window_mapper_equals_per_frame_maps(corridor9):
+@pytest.mark.parametrize("n", [4, 1])
+def test_gpu_window_mapper_equals_per_frame_maps(corridor9, n):
     """WindowMapper (the bench's tracked leg): one slam_map_windows call maps
     every window of the batch exactly as MapStore.append frame by frame does
     (rows and map points bit for bit, frame index = pair index in the window);
     problems() gives each window the export_data / read_bal_data problem of its
-    frames (make_cam_params of the window's first n poses)."""
+    frames (make_cam_params of the window's first n poses).  n = 1: one pair per
+    window, no nearest-landmark partials at all (an empty workspace slice)."""
     import torch
     from slam355.mapping import MapStore
     from slam355.pipeline import Tracker, WindowMapper
     from slam355.XXXport_files import U_OFF, V_OFF, make_cam_params
 
     L, R, poses, rig = corridor9
-    B, n = 8, 4
+    B = 8
     trk = Tracker(B, 720, 1280, rig.P_l, rig.P_r, max_kp_per_tile=64, seed=6)
     wm = WindowMapper(trk, n)
     trk.imgs.copy_(torch.from_numpy(np.concatenate([L[:B + 1], R[:B]])))
