@@ -375,9 +375,11 @@ typedef struct slam_ba_problem {
                                    chunk (= pt_ptr[grp_ptr]); required in both modes */
   const int32_t* chk_cptr;      /* [n_grps][8] start of each camera's run in chk_cobs */
   const int32_t* bslot_ab;      /* [n_bslots] camera pair a | b << 8 (a < b) of a block slot */
-  /* Optional level schedule of the tiled solve (9C > 120), built by
-   * slam355/ba.py tl_schedule: tiles renumbered by nested dissection, columns
-   * grouped by elimination-tree level.  Null: one panel step per tile column.
+  /* Level schedule of the tiled solve (required when 9C > 120), built by
+   * slam355/ba.py tl_schedule: tiles of whole cameras (64-row tiles, the rows
+   * past a tile's cameras padding) in nested-dissection order, with the row
+   * maps between S and the tiled system, columns grouped by elimination-tree
+   * level and the dataflow solve's column table.
    * tl_sched is the device copy, tl_sched_host the same array in host memory
    * (the launcher reads the level counts from it); both or neither. */
   const int32_t* tl_sched;
@@ -392,9 +394,9 @@ typedef struct slam_ba_problem {
   int32_t* asm_tab;
 } slam_ba_problem;
 
-/* Largest tile count (9C / 64, rounded up) the dataflow tiled solve takes:
- * one persistent workgroup per tile column, all resident at once (<= 1 per CU). */
-#define SLAM_TL_FLOW_MAX_T 128
+/* Largest tile count (tl_sched[1]) the dataflow tiled solve takes: one
+ * persistent workgroup per tile column (they need not all be resident). */
+#define SLAM_TL_FLOW_MAX_T 256
 
 /* Problems per batched launch (slam_ba_iterate_batch splits larger batches).
  * The descriptors travel by value in the kernel arguments: 16 x 376 B
@@ -470,8 +472,11 @@ int slam_ba_stage_windows(int n_win, int n, int cap, const double* rows, const i
 
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);
-/* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120). */
-long long slam_ba_chol_len(int n_cams);
+/* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120)
+ * for a tile schedule of n_tiles tiles (tl_sched[1]; slam355/ba.py
+ * tl_schedule cuts the system into tiles of whole cameras, so a schedule may
+ * have more tiles than 9C / 64); n_tiles <= 0: ceil(9C / 64). */
+long long slam_ba_chol_len(int n_cams, int n_tiles);
 /* Doubles in the all-reduced system buffer `sys`: dense (9C <= 120) (9C)^2,
  * packed (9C > 120) 81 * n_blocks (the listed upper camera blocks), then
  * b, g, diag U (9C each) and the per-camera cost (C). */

@@ -1893,14 +1893,21 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
 // end in solve_epilogue.  The diagonal-tile factor + inverse is
 // tile_chol_inv_blk (16x16 diagonal blocks in wave 0's registers, the rest on
 // the f64 matrix cores).
+#ifndef SLAM_TL_KSKIP
+#define SLAM_TL_KSKIP 0    // 1: the flow kernel's products skip a tile's padding k-blocks
+#endif
+#ifndef SLAM_TL_PADSKIP
+#define SLAM_TL_PADSKIP 1  // the tile factor skips the pivot chain of padding blocks
+#endif
 constexpr int kTB = 64;        // tile edge
+constexpr int kTlHdr = 8;      // ints of the tile schedule's header
 constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
 
-struct TlLayout {  // doubles inside p.chol
+struct TlLayout {  // doubles inside p.chol; T = the schedule's tile count (ba.tl_schedule)
   int T, N;
   long long a, dinv, b, y, x, nz, fail, xo, fc, flow, total;
-  __host__ __device__ explicit TlLayout(int n) {
-    T = (n + kTB - 1) / kTB;
+  __host__ __device__ TlLayout(int n, int n_tiles) {
+    T = n_tiles;
     N = T * kTB;
     a = 0;
     dinv = a + (long long)N * N;         // T tiles L_kk^-1 (row-major 64x64 each)
@@ -1972,8 +1979,11 @@ __device__ __forceinline__ int frag_swz(int r, int c) {
   const int F = ((r >> 4) << 4) + (c >> 2), hi = c & 3;
   return (F << 6) + (hi << 4) + (((r & 15) + 4 * hi + (F & 3)) & 15);
 }
-// gemm_xyT_lowY with both operands in frag_swz order (same products, same order)
-__device__ __forceinline__ void gemm_xyT_lowY_swz(const double* Xf, const double* Yf, d4 acc[4]) {
+// gemm_xyT_lowY with both operands in frag_swz order (same products, same order);
+// only the k-steps kk < kmax (Y's columns past a tile's camera rows are padding:
+// X's entries there are exact zeros)
+__device__ __forceinline__ void gemm_xyT_lowY_swz(const double* Xf, const double* Yf, d4 acc[4],
+                                                  int kmax = 16) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int so[4];
 #pragma unroll
@@ -1982,6 +1992,7 @@ __device__ __forceinline__ void gemm_xyT_lowY_swz(const double* Xf, const double
   for (int s = 0; s < 4; ++s) acc[s] = d4{0.0, 0.0, 0.0, 0.0};
   static_for<0, 16>([&](auto K) {
     constexpr int kk = decltype(K)::value;
+    if (SLAM_TL_KSKIP && kk >= kmax) return;  // (uniform)
     const double a = Xf[((w * 16 + kk) << 6) + so[kk & 3]];
     static_for<kk / 4, 4>([&](auto S) {
       constexpr int s = decltype(S)::value;
@@ -2363,9 +2374,24 @@ __device__ __forceinline__ void blk_factor_w0(double* M, double* Xb, int p, bool
   }
 }
 
+// nb: the tile's 16-row blocks that hold rows of S (ba.tl_schedule: a tile of
+// c whole cameras has 9c rows, the rest padding with a unit diagonal and no
+// coupling); wave 0 skips the pivot chain of every block p >= nb, whose factor
+// and inverse are the identity (X_pp = I written directly), so a 45-row tile
+// runs three 16x16 factors instead of four.  Waves 1-3 still form the blocks of
+// L / L^-1 in the padding rows (exact zeros) beside the chain.
+__device__ __forceinline__ void blk_identity_w0(double* Xb, int p) {
+  const int l = threadIdx.x & 63;
+  if (l < 16) {
+    double* X = Xb + blk_id(p, p) * 16 * kBS17;
+#pragma unroll
+    for (int ii = 0; ii < 16; ++ii) X[ii * kBS17 + l] = ii == l ? 1.0 : 0.0;
+  }
+}
+
 __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk, int ld,
                                                   double* M, double* Xb, double* Tb, int* okp,
-                                                  bool tl_prof_on = false) {
+                                                  int nb = 4, bool tl_prof_on = false) {
   const int t = threadIdx.x, l = t & 63, w = t >> 6;
   TL_STAMP(0);
   if (Akk != nullptr) {
@@ -2443,12 +2469,17 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
 #pragma unroll 1
   for (int p = 0; p < 4; ++p) {
     if (w == 0) {
-      if (p > 0) {  // look-ahead: L_{p,p-1}, then A_pp's last update
-        panel(p, p - 1);
+      if (SLAM_TL_PADSKIP && p >= nb) {  // a padding block: L_{p,p-1} = 0, L_pp = X_pp = I
         put(p == 1 ? 0 : (p == 2 ? 3 : 5));
-        trail(p, p, p - 1);
+        blk_identity_w0(Xb, p);
+      } else {
+        if (p > 0) {  // look-ahead: L_{p,p-1}, then A_pp's last update
+          panel(p, p - 1);
+          put(p == 1 ? 0 : (p == 2 ? 3 : 5));
+          trail(p, p, p - 1);
+        }
+        blk_factor_w0(M, Xb, p, ok);
       }
-      blk_factor_w0(M, Xb, p, ok);
     } else if (p == 1) {  // block column 0's other panel and trailing blocks
       if (w == 1) {
         panel(2, 0);
@@ -2520,8 +2551,15 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
 // k_tl2_unperm moves x back to the camera order (into the y region, which the
 // epilogue reads).  A banded window of T tiles runs ~log2 T levels instead of
 // T panel steps (C4: 4 levels for 9 tiles; C5: 8 for 71).
-__device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) {
-  return sched[sched[2] + (r >> 6)] * kTB + (r & 63);
+// The schedule's row maps sit at fixed offsets after its 8-int header (ba.tl_schedule;
+// checked on the host in tl_check_sched), so no lookup waits on a header load:
+// row r of S (camera order) -> its row in the tiled system
+__device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) { return sched[kTlHdr + r]; }
+// row of the tiled system -> row of S, -1 on a tile's padding rows
+__device__ __forceinline__ int tl_old_row(const int32_t* sched, int n, int rn) { return sched[kTlHdr + n + rn]; }
+// rows of S in tile k (they come first, padding after them)
+__device__ __forceinline__ const int32_t* tl_tile_rows(const int32_t* sched, int n, int T) {
+  return sched + kTlHdr + n + T * kTB;
 }
 
 // Zero the lower tiles (identity on the padded rows' diagonal), b in the new order.
@@ -2529,10 +2567,10 @@ __device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) {
 // for the rows I of column J (column table; grid T x (1 + max rows)); every
 // other lower tile is never read by either solve form (C5: 71 diagonal + row
 // tiles of 2556 lower tiles).  Otherwise all T (T + 1) / 2 lower tiles.
-__global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p, int struct_only) {
+__global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p, int T_, int struct_only) {
   lm_wave_priority();
   const int n = 9 * p.n_cams;
-  const TlLayout L(n);
+  const TlLayout L(n, T_);
   const int32_t* S = p.tl_sched;
   int I, J;
   bool first;
@@ -2552,15 +2590,13 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p, int struc
     first = idx == 0;
   }
   double* A = p.chol + L.a;
-  const int oldI = S[S[3] + I];  // padded rows live in the old last tile
   for (int e = threadIdx.x; e < kTB * kTB; e += kTlWG) {
     const int i = I * kTB + (e >> 6), j = J * kTB + (e & 63);
-    A[(size_t)i * L.N + j] = (i == j && oldI * kTB + (e >> 6) >= n) ? 1.0 : 0.0;
+    A[(size_t)i * L.N + j] = (i == j && tl_old_row(S, n, i) < 0) ? 1.0 : 0.0;  // identity on padding
   }
   if (I == J && threadIdx.x < kTB) {
-    const int r = oldI * kTB + threadIdx.x;  // old row landing at new row I*64 + t
-    p.chol[L.b + I * kTB + threadIdx.x] =
-        r < n ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
+    const int r = tl_old_row(S, n, I * kTB + threadIdx.x);  // row of S landing at new row I*64 + t
+    p.chol[L.b + I * kTB + threadIdx.x] = r >= 0 ? p.sys[sys_vec_off(p.n_cams, p.n_blocks) + r] : 0.0;
   }
   if (first) {
     // k_tl3_flow: a new solve epoch (its flags compare against it); the retire
@@ -2578,10 +2614,10 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_load(slam_ba_problem p, int struc
 
 // One WG per packed block: its values at their renumbered positions (lower
 // tiles, full symmetric inside diagonal tiles), camera damping on the diagonal.
-__global__ __launch_bounds__(128) void k_tl2_scatter(slam_ba_problem p) {
+__global__ __launch_bounds__(128) void k_tl2_scatter(slam_ba_problem p, int T_) {
   lm_wave_priority();
   const int n = 9 * p.n_cams;
-  const TlLayout L(n);
+  const TlLayout L(n, T_);
   const int32_t* S = p.tl_sched;
   const int blk = blockIdx.x, t = threadIdx.x;
   if (t >= 81) return;
@@ -2599,9 +2635,9 @@ __global__ __launch_bounds__(128) void k_tl2_scatter(slam_ba_problem p) {
 }
 
 __global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_tl2_panel(slam_ba_problem p, int eoff) {
+void k_tl2_panel(slam_ba_problem p, int T_, int eoff) {
   lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
+  const TlLayout L(9 * p.n_cams, T_);
   if (tl_failed(p, L)) return;
   const int32_t* S = p.tl_sched;
   const int k = S[eoff + 2 * blockIdx.x], I = S[eoff + 2 * blockIdx.x + 1];
@@ -2618,7 +2654,7 @@ void k_tl2_panel(slam_ba_problem p, int eoff) {
   double* Mb = VX;
   double* Xb = VX + kTB * kMS;
   double* Tb = Xb + 10 * 16 * kBS17;
-  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf);
+  const bool ok = tile_chol_inv_blk(Akk, L.N, Mb, Xb, Tb, &okf, (tl_tile_rows(S, 9 * p.n_cams, T_)[k] + 15) >> 4);
   if (w == 1) {
     const int cb16 = lane >> 4;
 #pragma unroll
@@ -2660,9 +2696,9 @@ void k_tl2_panel(slam_ba_problem p, int eoff) {
     }
 }
 
-__global__ __launch_bounds__(kTlWG) void k_tl2_update(slam_ba_problem p, int eoff) {
+__global__ __launch_bounds__(kTlWG) void k_tl2_update(slam_ba_problem p, int T_, int eoff) {
   lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
+  const TlLayout L(9 * p.n_cams, T_);
   if (tl_failed(p, L)) return;
   const int32_t* S = p.tl_sched;
   const int32_t* e = S + eoff + 4 * blockIdx.x;
@@ -2714,9 +2750,9 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_update(slam_ba_problem p, int eof
 }
 
 // x_k = L_kk^-T (y_k - sum_I L_Ik^T x_I), I over the column's structure (ancestors).
-__global__ __launch_bounds__(kTlWG) void k_tl2_back(slam_ba_problem p, int eoff) {
+__global__ __launch_bounds__(kTlWG) void k_tl2_back(slam_ba_problem p, int T_, int eoff) {
   lm_wave_priority();
-  const TlLayout L(9 * p.n_cams);
+  const TlLayout L(9 * p.n_cams, T_);
   if (tl_failed(p, L)) return;
   const int32_t* S = p.tl_sched;
   const int32_t* e = S + eoff + 3 * blockIdx.x;
@@ -2746,18 +2782,18 @@ __global__ __launch_bounds__(kTlWG) void k_tl2_back(slam_ba_problem p, int eoff)
 }
 
 // x (new tile order, L.x) -> camera order in the y region (read by the epilogue)
-__global__ __launch_bounds__(kTB) void k_tl2_unperm(slam_ba_problem p) {
-  const TlLayout L(9 * p.n_cams);
+__global__ __launch_bounds__(kTB) void k_tl2_unperm(slam_ba_problem p, int T_) {
+  const TlLayout L(9 * p.n_cams, T_);
   const int I = blockIdx.x;  // new tile
-  const int oldI = p.tl_sched[p.tl_sched[3] + I];
-  p.chol[L.y + oldI * kTB + threadIdx.x] = p.chol[L.x + I * kTB + threadIdx.x];
+  const int r = tl_old_row(p.tl_sched, 9 * p.n_cams, I * kTB + threadIdx.x);
+  if (r >= 0) p.chol[L.y + r] = p.chol[L.x + I * kTB + threadIdx.x];
 }
 
-__global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p) {
+__global__ __launch_bounds__(1024) void k_tl2_epilogue(slam_ba_problem p, int T_) {
   lm_wave_priority();
   __shared__ double red[32];
   const int n = 9 * p.n_cams;
-  const TlLayout L(n);
+  const TlLayout L(n, T_);
   const bool ok = !tl_failed(p, L);
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
   const double* gvec = bvec + n;
@@ -2993,15 +3029,28 @@ __device__ __forceinline__ void tiles2_to_frag_sc1(const double* __restrict__ g0
   }
 }
 
-// acc[s] += (rows 16w.., cols 16s.. of X Y^T), X and Y in fragment order
-__device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf, d4 acc[4]) {
+// acc[s] += (rows 16w.., cols 16s.. of X Y^T), X and Y in fragment order, over
+// the first nbk 16-column blocks of k (the columns of a child tile past its
+// camera rows' blocks are exact zeros in both operands)
+__device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf, d4 acc[4],
+                                             int nbk = 4) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll 4
-  for (int kk = 0; kk < 16; ++kk) {
-    const double a = Xf[((w * 16 + kk) << 6) + lane];
+#if SLAM_TL_KSKIP
+  for (int kb = 0; kb < nbk; ++kb) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
-      acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + lane], acc[s], 0, 0, 0);
+    for (int k4 = 0; k4 < 4; ++k4) {
+      const int kk = 4 * kb + k4;
+#else
+  (void)nbk;
+  {
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk) {
+#endif
+      const double a = Xf[((w * 16 + kk) << 6) + lane];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Yf[((s * 16 + kk) << 6) + lane], acc[s], 0, 0, 0);
+    }
   }
 }
 
@@ -3010,10 +3059,10 @@ __constant__ int kDiagBlk[4][3][2] = {{{0, 0}, {3, 0}, {3, 1}}, {{1, 0}, {1, 1},
                                       {{2, 0}, {2, 1}, {2, 0}}, {{2, 2}, {3, 3}, {2, 2}}};
 
 __global__ __launch_bounds__(kTlWG) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_tl3_flow(slam_ba_problem p) {
+void k_tl3_flow(slam_ba_problem p, int T_) {
   lm_wave_priority();
   const int n = 9 * p.n_cams;
-  const TlLayout L(n);
+  const TlLayout L(n, T_);
   const int32_t* S = p.tl_sched;
   const int T = L.T;
   const FlowPtrs F(p, L);
@@ -3035,6 +3084,11 @@ void k_tl3_flow(slam_ba_problem p) {
   const int J = col_sh;
   const int32_t* rec = S + S[5] + 5 * J;
   const int ro = rec[0], rc = rec[1], so = rec[2], sc = rec[3], uo = rec[4];
+  // rows of a tile (its rows of S first, padding after them): the 16-row
+  // blocks of the factor and of the products over its columns
+  const int32_t* trows = tl_tile_rows(S, n, T);
+  auto nblk = [&](int k) { return (trows[k] + 15) >> 4; };
+  const int nbJ = nblk(J);
   int* fail = reinterpret_cast<int*>(p.chol + L.fail);
   const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
   double* A = p.chol + L.a;
@@ -3115,12 +3169,25 @@ void k_tl3_flow(slam_ba_problem p) {
       __syncthreads();
       if (pre) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
     }
+    const int kmk = nblk(k);  // child k's column blocks past its rows: zeros
+#if SLAM_TL_KSKIP
+    for (int kb = 0; kb < kmk; ++kb)
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+          const int kk = 4 * kb + k4;
+          acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[((dR[b] * 16 + kk) << 6) + lane],
+                                                        cur[((dC[b] * 16 + kk) << 6) + lane], acc[b], 0, 0, 0);
+        }
+#else
 #pragma unroll 4
     for (int kk = 0; kk < 16; ++kk)
 #pragma unroll
       for (int b = 0; b < 3; ++b)
         acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(cur[((dR[b] * 16 + kk) << 6) + lane],
                                                       cur[((dC[b] * 16 + kk) << 6) + lane], acc[b], 0, 0, 0);
+#endif
     if (q + 1 < sc) {
 #pragma unroll
       for (int q2 = 0; q2 < 2; ++q2) {
@@ -3133,7 +3200,7 @@ void k_tl3_flow(slam_ba_problem p) {
         if (!ok) break;
         tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, VR);
         __syncthreads();  // VR filled
-        gemm_xyT_acc(VR, cur, racc[q2]);
+        gemm_xyT_acc(VR, cur, racc[q2], kmk);
         __syncthreads();  // VR reads done
       }
       if (ok && !pre) {
@@ -3156,7 +3223,7 @@ void k_tl3_flow(slam_ba_problem p) {
         }
       }
     double* Xb = VX + kTB * kMS;
-    ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf);
+    ok = tile_chol_inv_blk(nullptr, 0, M, Xb, Xb + 10 * 16 * kBS17, &okf, nbJ);
     // L_JJ^-1 out of the block store into (swizzled) fragment order (Vf) and
     // row-major (VR): wave w takes rows [16w, 16w + 16), lane = column
     double x[16];
@@ -3207,14 +3274,14 @@ void k_tl3_flow(slam_ba_problem p) {
       if (qc < 2 && k == S[so + sc - 1]) {
         tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, Yf);
         __syncthreads();
-        gemm_xyT_acc(Yf, Xf, acc);
+        gemm_xyT_acc(Yf, Xf, acc, nblk(k));
       } else {
         // (cannot happen for rows 0 and 1 with the schedule's ordered k lists;
         // kept general: Xf's L_Jk of the last child is then reloaded below)
         tiles2_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, A + (size_t)J * kTB * L.N + k * kTB, L.N,
                            Yf, Xf);
         __syncthreads();
-        gemm_xyT_acc(Yf, Xf, acc);
+        gemm_xyT_acc(Yf, Xf, acc, nblk(k));
         if (qc < 2 && sc > 0) {
           __syncthreads();
           const int kl = S[so + sc - 1];
@@ -3250,7 +3317,7 @@ void k_tl3_flow(slam_ba_problem p) {
     __syncthreads();
     if (q == 0) FLOW_S(3);
     d4 lacc[4];
-    gemm_xyT_lowY_swz(stg, Vf, lacc);  // L_IJ = A_IJ (L_JJ^-1)^T
+    gemm_xyT_lowY_swz(stg, Vf, lacc, 4 * nbJ);  // L_IJ = A_IJ (L_JJ^-1)^T
 #ifdef SLAM_FLOW_PROFILE
     if (q == 0) {
       __builtin_amdgcn_s_waitcnt(0);
@@ -3401,8 +3468,8 @@ void k_tl3_flow(slam_ba_problem p) {
       if (t < kTB) {
         const double xv = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
         st_sc1(p.chol + L.x + k * kTB + t, xv);
-        const int orow = S[S[3] + k] * kTB + t;  // camera order (padded rows dropped)
-        if (orow < n) st_sc1(p.chol + L.xo + orow, xv);
+        const int orow = tl_old_row(S, n, k * kTB + t);  // camera order (padding rows dropped)
+        if (orow >= 0) st_sc1(p.chol + L.xo + orow, xv);
       }
     }
     // retire column k even when the solve failed (the counters and the ticket
@@ -3473,7 +3540,7 @@ void k_tl3_flow(slam_ba_problem p) {
 // otherwise (or with tl_mode "levels") the level-scheduled launches run.
 static bool tl_flow_ok(const slam_ba_problem& p, hipStream_t) {
   if (p.tl_mode != 0 || p.tl_sched_host == nullptr || p.tl_sched_host[5] <= 0) return false;
-  const TlLayout L(9 * p.n_cams);
+  const TlLayout L(9 * p.n_cams, p.tl_sched_host[1]);
   return L.T <= SLAM_TL_FLOW_MAX_T && 9 * p.n_cams <= 2 * kTB * kTB;
 }
 
@@ -3484,42 +3551,53 @@ static void tl_load(const slam_ba_problem& p, hipStream_t s) {
   if (h[5] > 0) {
     int maxrc = 0;
     for (int J = 0; J < T; ++J) maxrc = std::max(maxrc, (int)h[h[5] + 5 * J + 1]);
-    k_tl2_load<<<dim3(T, 1 + maxrc), kTlWG, 0, s>>>(p, 1);
+    k_tl2_load<<<dim3(T, 1 + maxrc), kTlWG, 0, s>>>(p, T, 1);
   } else {
-    k_tl2_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p, 0);
+    k_tl2_load<<<T * (T + 1) / 2, kTlWG, 0, s>>>(p, T, 0);
   }
 }
 
+// the layout the kernels assume (row maps at fixed offsets after the header,
+// every row of S in some tile)
+static int tl_check_sched(const slam_ba_problem& p) {
+  const int32_t* h = p.tl_sched_host;
+  const int n = 9 * p.n_cams, T = h[1];
+  SLAM_REQUIRE(T >= (n + kTB - 1) / kTB && h[2] == kTlHdr && h[3] == kTlHdr + n &&
+                   h[6] == kTlHdr + n + T * kTB,
+               "slam_ba: tl_sched layout is not ba.tl_schedule's (T %d, offsets %d %d %d for n %d)", T,
+               h[2], h[3], h[6], n);
+  return SLAM_OK;
+}
+
 static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
-  const TlLayout L(9 * p.n_cams);
-  SLAM_REQUIRE(p.tl_sched_host[1] == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d",
-               p.tl_sched_host[1], L.T);
+  const TlLayout L(9 * p.n_cams, p.tl_sched_host[1]);
+  if (int rc = tl_check_sched(p)) return rc;
   tl_load(p, s);
-  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
-  k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p);
+  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p, L.T);
+  k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p, L.T);
   SLAM_LAUNCHED("k_tl3_flow");
   return SLAM_OK;
 }
 
 static int tl_solve_levels(const slam_ba_problem& p, hipStream_t s) {
-  const TlLayout L(9 * p.n_cams);
+  const TlLayout L(9 * p.n_cams, p.tl_sched_host[1]);
   const int32_t* h = p.tl_sched_host;
   const int nlev = h[0], T = h[1];
-  SLAM_REQUIRE(T == L.T, "slam_ba: tl_sched is for %d tiles, the system has %d", T, L.T);
+  if (int rc = tl_check_sched(p)) return rc;
   const int32_t* tab = h + h[4];
   tl_load(p, s);
-  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p);
+  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p, L.T);
   for (int lv = 0; lv < nlev; ++lv) {
     const int32_t* e = tab + 6 * lv;
-    if (e[1] > 0) k_tl2_panel<<<e[1], kTlWG, 0, s>>>(p, e[0]);
-    if (e[3] > 0) k_tl2_update<<<e[3], kTlWG, 0, s>>>(p, e[2]);
+    if (e[1] > 0) k_tl2_panel<<<e[1], kTlWG, 0, s>>>(p, T, e[0]);
+    if (e[3] > 0) k_tl2_update<<<e[3], kTlWG, 0, s>>>(p, T, e[2]);
   }
   for (int lv = nlev - 1; lv >= 0; --lv) {
     const int32_t* e = tab + 6 * lv;
-    if (e[5] > 0) k_tl2_back<<<e[5], kTlWG, 0, s>>>(p, e[4]);
+    if (e[5] > 0) k_tl2_back<<<e[5], kTlWG, 0, s>>>(p, T, e[4]);
   }
-  k_tl2_unperm<<<T, kTB, 0, s>>>(p);
-  k_tl2_epilogue<<<1, 1024, 0, s>>>(p);
+  k_tl2_unperm<<<T, kTB, 0, s>>>(p, T);
+  k_tl2_epilogue<<<1, 1024, 0, s>>>(p, T);
   SLAM_LAUNCHED("k_tl2_*");
   return SLAM_OK;
 }
@@ -3738,8 +3816,12 @@ int check_problem(const slam_ba_problem* p) {
 
 extern "C" int slam_ba_red_slots(int n_grps) { return 2 * n_grps; }
 
-extern "C" long long slam_ba_chol_len(int n_cams) {
-  return TlLayout(9 * n_cams).total;  // tiled factor workspace (9C > kLdsMaxN)
+extern "C" long long slam_ba_chol_len(int n_cams, int n_tiles) {
+  // tiled factor workspace (9C > kLdsMaxN) for a schedule of n_tiles tiles
+  // (tl_sched[1]); n_tiles <= 0: the fewest 64-row tiles that hold 9C rows
+  if (n_cams <= 0) return 0;
+  const int n = 9 * n_cams;
+  return TlLayout(n, n_tiles > 0 ? n_tiles : (n + kTB - 1) / kTB).total;
 }
 
 extern "C" long long slam_ba_sys_len(int n_cams, int n_blocks) {

@@ -12,6 +12,7 @@ iteration.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -92,16 +93,14 @@ def upper_blocks(n_cams, cam_idx, pt_idx):
 
 
 TB = 64  # tile edge of the tiled solver (csrc/ba.hip kTB)
+TILE_MODE = "rows64"  # default tiling of the camera solve (tl_schedule; measured best)
 
 
-def _nd_order(adj, nodes):
-    """Nested-dissection order of `nodes` in the tile graph `adj` (list of
-    sets): each connected component separately; a component whose BFS level
-    structure (from a pseudo-peripheral node) has >= 3 levels is split by its
-    middle level, the separator numbered last."""
+def _components(adj, nodes):
+    """Connected components of `nodes` in `adj` (list of sets), lowest node first."""
     nodes = set(nodes)
     out = []
-    while nodes:  # components, lowest node first
+    while nodes:
         root = min(nodes)
         comp, stack = {root}, [root]
         while stack:
@@ -111,7 +110,7 @@ def _nd_order(adj, nodes):
                     comp.add(v)
                     stack.append(v)
         nodes -= comp
-        out += _nd_component(adj, comp)
+        out.append(comp)
     return out
 
 
@@ -125,9 +124,9 @@ def _bfs_levels(adj, comp, root):
         levels.append(nxt)
 
 
-def _nd_component(adj, comp):
-    if len(comp) <= 2:
-        return sorted(comp)
+def _bfs_order(adj, comp):
+    """comp in BFS order from a pseudo-peripheral node (camera order for a
+    keyframe window; the two arcs outward for a loop)."""
     levels = _bfs_levels(adj, comp, min(comp))
     for _ in range(2):  # pseudo-peripheral: restart from the far end
         far = min(levels[-1])
@@ -135,24 +134,143 @@ def _nd_component(adj, comp):
         if len(lv2) <= len(levels):
             break
         levels = lv2
-    if len(levels) < 3:
-        return sorted(comp)
-    sep = set(levels[len(levels) // 2])
-    return _nd_order(adj, comp - sep) + sorted(sep)
+    return [v for lv in levels for v in lv]
 
 
-def tl_schedule(n_cams, blocks):
+def _chunk(adj, nodes, cap):
+    """Tiles of at most `cap` nodes over the connected pieces of `nodes` (each
+    piece in BFS order, so a chain of tiles follows the band): pieces that
+    share no block stay in separate tiles -- independent columns."""
+    out = []
+    for comp in _components(adj, nodes):
+        c = _bfs_order(adj, comp)
+        out += [sorted(c[i:i + cap]) for i in range(0, len(c), cap)]
+    return out
+
+
+def _nd_tiles(adj, comp, cap, chain):
+    """Nested dissection of a graph into tiles of <= cap nodes, in elimination
+    order.  A component of <= cap nodes is a leaf; with `chain`, one of <=
+    chain * cap nodes is a chain of tiles along its BFS order (no separator:
+    fewer tiles, fewer children per column).  Otherwise its nodes are put in
+    BFS order, and for every cut i of that order the separator is order[i ..
+    reach(i)], reach(i) = the furthest position any node before i is coupled
+    to: the nodes before and after it share no block.  The cut minimising the
+    larger side plus twice the separator is taken (a band of 6-keyframe
+    tracks: 5-camera separators anywhere, so the sides balance exactly; a
+    loop: a BFS level's two arcs); its separator's tiles are eliminated after
+    both sides."""
+    if len(comp) <= cap * max(chain, 1):
+        return _chunk(adj, comp, cap)
+    order = _bfs_order(adj, comp)
+    pos = {v: i for i, v in enumerate(order)}
+    n = len(order)
+    best, reach = None, -1
+    for i in range(1, n):
+        reach = max(reach, max((pos[w] for w in adj[order[i - 1]] if w in pos), default=i - 1))
+        if reach < i or reach >= n - 1:
+            continue  # order[:i] is a component of its own, or no right side
+        cost = max(i, n - 1 - reach) + 2 * (reach - i + 1)
+        if best is None or cost < best[0]:
+            best = (cost, i, reach)
+    if best is None:  # no separator: a dense chain of tiles
+        return _chunk(adj, comp, cap)
+    _, i, r = best
+    out = []
+    for side in (order[:i], order[r + 1:]):
+        for sub in _components(adj, side):
+            out += _nd_tiles(adj, sub, cap, chain)
+    return out + _chunk(adj, order[i:r + 1], cap)
+
+
+def _nd_order(adj, nodes):
+    """Nested-dissection order of `nodes` in the 64-row tile graph (the
+    "rows64" tiling): each connected component separately; a component whose
+    BFS level structure has >= 3 levels is split by its middle level, the
+    separator numbered last."""
+    out = []
+    for comp in _components(adj, nodes):
+        if len(comp) <= 2:
+            out += sorted(comp)
+            continue
+        levels = _bfs_levels(adj, comp, min(comp))
+        for _ in range(2):
+            far = min(levels[-1])
+            lv2 = _bfs_levels(adj, comp, far)
+            if len(lv2) <= len(levels):
+                break
+            levels = lv2
+        if len(levels) < 3:
+            out += sorted(comp)
+            continue
+        sep = set(levels[len(levels) // 2])
+        out += _nd_order(adj, comp - sep) + sorted(sep)
+    return out
+
+
+def _parse_tile_mode(mode):
+    mode = mode or os.environ.get("SLAM_TL_TILES") or TILE_MODE
+    if mode == "rows64":
+        return mode, 0, 0
+    parts = mode.split(":")
+    if parts[0] != "cams" or len(parts) not in (2, 3):
+        raise ValueError(f"tile mode must be 'rows64' or 'cams:CAP[:CHAIN]', not {mode!r}")
+    cap, chain = int(parts[1]), int(parts[2]) if len(parts) == 3 else 0
+    if not 1 <= cap <= TB // 9:
+        raise ValueError(f"tile mode {mode!r}: 1 <= CAP <= {TB // 9} cameras per tile")
+    return "cams", cap, chain
+
+
+def tile_rows(n_cams, blocks, mode=None):
+    """The tiles of the camera solve as lists of rows of S (<= 64 each), in
+    elimination order.  mode (default TILE_MODE, or $SLAM_TL_TILES):
+      "rows64"          64 consecutive rows per tile (a camera may straddle two
+                        tiles), tiles in nested-dissection order of the tile graph;
+      "cams:CAP[:CH]"   whole cameras, <= CAP per tile (9 CAP rows: the rest of
+                        the 64-row tile is padding, whose 16-row blocks the
+                        factor skips), nested dissection of the camera graph
+                        (_nd_tiles; CH: components of <= CH CAP cameras become a
+                        chain of tiles instead of being split)."""
+    kind, cap, chain = _parse_tile_mode(mode)
+    blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
+    n = 9 * int(n_cams)
+    if kind == "rows64":
+        T = (n + TB - 1) // TB
+        adj = [set() for _ in range(T)]
+        for c1, c2 in blocks:
+            t1 = range((9 * c1) // TB, (9 * c1 + 8) // TB + 1)
+            t2 = range((9 * c2) // TB, (9 * c2 + 8) // TB + 1)
+            for a_ in t1:
+                for b_ in t2:
+                    if a_ != b_:
+                        adj[a_].add(b_)
+                        adj[b_].add(a_)
+        return [list(range(TB * t, min(TB * t + TB, n))) for t in _nd_order(adj, range(T))]
+    adj = [set() for _ in range(int(n_cams))]
+    for c1, c2 in blocks:
+        if c1 != c2:
+            adj[c1].add(int(c2))
+            adj[c2].add(int(c1))
+    out = []
+    for comp in _components(adj, range(int(n_cams))):
+        out += _nd_tiles(adj, comp, cap, chain)
+    return [[9 * c + i for c in cams for i in range(9)] for cams in out]
+
+
+def tl_schedule(n_cams, blocks, mode=None):
     """Level schedule of the tiled camera solve (csrc/ba.hip tl_solve_levels).
 
-    The 64-row tiles of the 9C-row camera system are renumbered by nested
-    dissection of their adjacency graph (tiles sharing a camera block), the
-    tile-level Cholesky structure and elimination tree are computed
-    symbolically, and the columns are grouped by their height in the tree:
-    the columns of one level are mutually independent, so each level is one
-    panel launch (factor + L_Ik for every column of the level) and one update
-    launch (A_IJ -= sum_k L_Ik L_Jk^T, b_I -= sum_k L_Ik y_k per target tile),
-    and the back substitution walks the levels in reverse.  A banded window of
-    T tiles needs ~log2(T) levels instead of T sequential panel steps.
+    The 9C-row camera system is cut into tiles (tile_rows: whole cameras by
+    default, at most 64 rows each, numbered in nested-dissection order), each
+    held in a 64-row tile whose rows past its own are padding (identity
+    diagonal, no coupling); the tile-level Cholesky structure and elimination
+    tree are computed symbolically, and the columns are grouped by their height
+    in the tree: the columns of one level are mutually independent, so each
+    level is one panel launch (factor + L_Ik for every column of the level) and
+    one update launch (A_IJ -= sum_k L_Ik L_Jk^T, b_I -= sum_k L_Ik y_k per
+    target tile), and the back substitution walks the levels in reverse.  A
+    banded window of T tiles needs ~log2(T) levels instead of T sequential
+    panel steps.
 
     The same symbolic structure also drives the dataflow form of the solve
     (csrc/ba.hip k_tl3_flow: one persistent workgroup per tile column, columns
@@ -160,8 +278,12 @@ def tl_schedule(n_cams, blocks):
     boundaries), whose per-column table is appended.
 
     Returns the int32 schedule (device and host copies are the same array):
-      [0] nlev, [1] T, [2] tperm offset, [3] itperm offset, [4] level table offset,
-      [5] column table offset
+      [0] nlev, [1] T, [2] row map offset, [3] inverse row map offset,
+      [4] level table offset, [5] column table offset, [6] tile size table
+      offset, [7] reserved (0)
+      row map: row r of S -> row of the tiled system (tile * 64 + position)
+      inverse row map: row of the tiled system -> row of S, -1 on padding rows
+      tile sizes: per tile its rows of S (they come first, padding after)
       column table: per column J (rows_off, rows_cnt, rs_off, rs_cnt, upd_off)
         rows: I > J with L_IJ != 0 (ascending); rs: k < J with L_Jk != 0
         (by elimination-tree level, then index: the updates of the diagonal
@@ -170,31 +292,24 @@ def tl_schedule(n_cams, blocks):
       level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
-      back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)
-    tperm[old tile] = new tile, itperm its inverse."""
+      back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)"""
     blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
     n = 9 * int(n_cams)
-    T = (n + TB - 1) // TB
-    adj = [set() for _ in range(T)]
-    for c1, c2 in blocks:
-        t1 = range((9 * c1) // TB, (9 * c1 + 8) // TB + 1)
-        t2 = range((9 * c2) // TB, (9 * c2 + 8) // TB + 1)
-        for a in t1:
-            for b in t2:
-                if a != b:
-                    adj[a].add(b)
-                    adj[b].add(a)
-    order = _nd_order(adj, range(T))
-    tperm = np.empty(T, np.int64)
-    tperm[np.asarray(order, np.int64)] = np.arange(T)
-    itperm = np.asarray(order, np.int64)
-    # symbolic tile Cholesky in the new numbering
+    tiles = tile_rows(int(n_cams), blocks, mode)
+    T = len(tiles)
+    rowmap = np.empty(n, np.int64)
+    irow = np.full(T * TB, -1, np.int64)
+    for I, rows in enumerate(tiles):
+        rowmap[rows] = I * TB + np.arange(len(rows))
+        irow[I * TB:I * TB + len(rows)] = rows
+    tile_of = rowmap // TB
+    # symbolic tile Cholesky (tiles already in elimination order)
     struct = [set() for _ in range(T)]
-    for a in range(T):
-        for b in adj[a]:
-            A, B = tperm[a], tperm[b]
-            if A > B:
-                struct[B].add(int(A))
+    for c1, c2 in blocks:
+        for A in set(tile_of[9 * c1:9 * c1 + 9].tolist()):
+            for B in set(tile_of[9 * c2:9 * c2 + 9].tolist()):
+                if A != B:
+                    struct[min(A, B)].add(max(A, B))
     parent = [-1] * T
     level = [0] * T
     for k in range(T):
@@ -207,8 +322,8 @@ def tl_schedule(n_cams, blocks):
             level[parent[k]] = max(level[parent[k]], level[k] + 1)
     nlev = max(level) + 1 if T else 0
     cols = [[k for k in range(T) if level[k] == lv] for lv in range(nlev)]
-    head = [nlev, T, 0, 0, 0, 0]
-    table, body = [], []
+    head = [nlev, T, 0, 0, 0, 0, 0, 0]
+    table = []
     lists = []  # (k lists / struct lists) appended after the entries
 
     def list_off(vals):
@@ -232,11 +347,13 @@ def tl_schedule(n_cams, blocks):
         pan.append(p_e)
         upd.append(u_e)
         bk.append(b_e)
-    # layout: header | tperm | itperm | level table | entries | lists
+    # layout: header | row map | inverse row map | tile sizes | level table | entries | lists
     off = len(head)
     head[2] = off
-    off += T
+    off += n
     head[3] = off
+    off += T * TB
+    head[6] = off
     off += T
     head[4] = off
     off += 6 * nlev
@@ -259,7 +376,8 @@ def tl_schedule(n_cams, blocks):
         for k, li in bk[lv]:
             ents += [k, list_offs[li], len(lists[li])]
         table += [po, len(pan[lv]), uo, len(upd[lv]), bo, len(bk[lv])]
-    flat = head + tperm.tolist() + itperm.tolist() + table + ents + [v for li in lists for v in li]
+    flat = (head + rowmap.tolist() + irow.tolist() + [len(r) for r in tiles] + table + ents
+            + [v for li in lists for v in li])
     # column table of the dataflow solve.  rs(J) in the order its tiles are
     # expected to be published -- by elimination-tree level, then index -- so a
     # column accumulates the tiles of its early (low-level) children while the
@@ -705,14 +823,15 @@ class BAProblem:
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
                  block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow",
-                 fold_assembly=False):
+                 fold_assembly=False, tile_mode=None):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
         every point is seen by <= MF_CAMS cameras).  The tiled camera solve
         (9C > 120) follows the nested-dissection schedule of tl_schedule;
         tl_mode "flow" runs it as one dataflow launch (k_tl3_flow, on any
-        stream and CU mask), "levels" one launch pair per elimination-tree level.
+        stream and CU mask), "levels" one launch pair per elimination-tree level;
+        tile_mode: the tiling of that solve (tile_rows; default TILE_MODE).
         fold_assembly (lin_mode mfma): k_lin_mfma's last supergroup per camera
         block sums the block's partial rows into the system (no k_assemble
         launch).  Off by default: measured slower (the workgroup that finishes
@@ -762,13 +881,16 @@ class BAProblem:
         n_cs, n_bs = len(pl["cslot_cam"]), len(pl["bslot_blk"])
         self.sys_len = int(_lib.lib.slam_ba_sys_len(C, len(pl["blocks"])))
         self.tl_levels = C9 > LDS_MAX_N
+        if self.tl_levels:  # schedule of the tiled solve (host copy; device copy below)
+            self._sched_host = tl_schedule(C, pl["blocks"], tile_mode)
         # every float64 buffer in ONE device allocation (256-byte aligned
         # segments): the parameters (two LM copies + the initial copy) and the
         # permuted observations in one upload, the workspaces in one fill
         up = [("cams0", cams), ("pts0", pts), ("cams1", cams), ("pts1", pts), ("init_c", cams),
               ("init_p", pts), ("obs_q", qs[pl["order"]] if self.O else np.zeros((1, 2)))]
         zero = [("camrec0", C * 32), ("camrec1", C * 32), ("cpart", n_cs * 112), ("bpart", n_bs * 81),
-                ("sys", self.sys_len), ("chol", _lib.lib.slam_ba_chol_len(C) if self.tl_levels else 1),
+                ("sys", self.sys_len), ("chol", _lib.lib.slam_ba_chol_len(C, int(self._sched_host[1]))
+                                   if self.tl_levels else 1),
                 ("delta_c", C9), ("red_part", _lib.lib.slam_ba_red_slots(G)), ("small", 4),
                 ("state", N_STATE)]
         al = lambda n: (max(int(n), 1) + 31) // 32 * 32  # noqa: E731
@@ -791,8 +913,7 @@ class BAProblem:
             t[k] = arena[offs[k]:offs[k] + np.size(a)].view(np.shape(a))
         for k, n in zero:
             t[k] = arena[offs[k]:offs[k] + max(int(n), 1)]
-        if self.tl_levels:  # level schedule of the tiled solve (host + device copies)
-            self._sched_host = tl_schedule(C, pl["blocks"])
+        if self.tl_levels:
             t["tl_sched"] = T(self._sched_host)
         t["ticket"] = torch.zeros(1, dtype=torch.int32, device=dev)
         if stream is not None:  # the uploads and fills above ran on the current stream

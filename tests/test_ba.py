@@ -282,13 +282,15 @@ def test_gpu_local_ba_config3_converges(C, P, k):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["flow", "levels"])
+@pytest.mark.parametrize("mode", ["flow", "levels", "flow/cams:5", "levels/cams:7:2"])
 @pytest.mark.parametrize("C,P,k", [(14, 400, 4), (40, 1500, 5), (130, 3000, 6)])
 def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
     """9C > 120: the reduced camera system goes through the tiled Cholesky
-    (k_tl3_flow or k_tl2_*; 2, 6 and 19 tiles of 64).  The 130-camera trajectory window is
-    block-banded (points seen by 6 consecutive keyframes), so most tiles stay
-    structurally zero and are skipped.  LM iterates equal the oracle's Schur LM."""
+    (k_tl3_flow or k_tl2_*; 2, 6 and 19 tiles of 64 rows, or tiles of whole
+    cameras with padding rows, whose blocks the factor skips).  The
+    130-camera trajectory window is block-banded (points seen by 6
+    consecutive keyframes), so most tiles stay structurally zero and are
+    skipped.  LM iterates equal the oracle's Schur LM."""
     from slam355 import ba
 
     cams, pts, ci, pi, qs = make_problem(11 + C, C, P, k)
@@ -297,7 +299,8 @@ def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
     cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
     cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
     pts0 = pts + rng.normal(0, 0.05, pts.shape)
-    prob = ba.BAProblem(cams0, pts0, ci, pi, qs, tl_mode=mode)
+    tl, _, tiles = mode.partition("/")
+    prob = ba.BAProblem(cams0, pts0, ci, pi, qs, tl_mode=tl, tile_mode=tiles or None)
     st = oba.LMState(1e-4)
     oc, op = cams0.copy(), pts0.copy()
     pairs = oba._obs_pairs(ci, pi)
@@ -670,24 +673,34 @@ def test_union_plan_assembles_the_reduced_system(case):
     assert np.abs(b - br).max() <= 1e-9 * max(1.0, np.abs(br).max())
 
 
+def _tiled_system(S, b, sched):
+    """S, b laid out in the schedule's tiles (row map: row of S -> row of the
+    tiled system; the rows past a tile's cameras are padding with a unit
+    diagonal): (A [N, N], b [N], row map [n])."""
+    T, n, TB = int(sched[1]), len(b), 64
+    N = T * TB
+    rn = sched[sched[2]:sched[2] + n].astype(np.int64)
+    irow = sched[sched[3]:sched[3] + N]
+    A = np.zeros((N, N))
+    A[np.ix_(rn, rn)] = S
+    pad = np.nonzero(irow < 0)[0]
+    A[pad, pad] = 1.0
+    bb = np.zeros(N)
+    bb[rn] = b
+    return A, bb, rn
+
+
 def _emulate_tl_levels(S, b, sched):
     """The level-scheduled tiled solve (csrc/ba.hip k_tl2_*) restated in NumPy,
-    launch by launch: tiles renumbered by the schedule's tperm, each level's
+    launch by launch: S laid out in the schedule's tiles of whole cameras, each level's
     panels (diagonal factor + inverse, y_k; L_Ik = A_Ik L_kk^-T), then its
     updates (A_IJ -= sum_k L_Ik L_Jk^T, b_I -= sum_k L_Ik y_k), then the back
     substitution by levels in reverse, x un-permuted."""
     nlev, T = int(sched[0]), int(sched[1])
-    tperm = sched[sched[2]:sched[2] + T]
     tab = sched[sched[4]:sched[4] + 6 * nlev].reshape(-1, 6)
     n, TB = len(b), 64
     N = T * TB
-    new = lambda r: tperm[r // TB] * TB + r % TB  # noqa: E731
-    rn = new(np.arange(N))
-    A = np.zeros((N, N))
-    A[np.ix_(rn[:n], rn[:n])] = S
-    A[rn[n:], rn[n:]] = 1.0
-    bb = np.zeros(N)
-    bb[rn[:n]] = b
+    A, bb, rn = _tiled_system(S, b, sched)
     t = lambda I: slice(I * TB, (I + 1) * TB)  # noqa: E731
     dinv, y, x = {}, np.zeros(N), np.zeros(N)
     for lv in range(nlev):
@@ -711,14 +724,17 @@ def _emulate_tl_levels(S, b, sched):
             for I in sched[so:so + sc]:
                 r -= A[t(I), t(k)].T @ x[t(I)]
             x[t(k)] = dinv[k].T @ r
-    return x[rn[:n]]
+    return x[rn]
 
 
+@pytest.mark.parametrize("mode", ["rows64", "cams:5", "cams:7:2"])
 @pytest.mark.parametrize("C,loop", [(30, False), (64, False), (120, True)])
-def test_tl_level_schedule_solves_the_camera_system(C, loop):
-    """Nested-dissection level schedule of the tiled solver: every level's
-    columns are independent (no L between them), a banded window needs
-    ~log2(T) levels, and executing the schedule tile by tile solves S x = b."""
+def test_tl_level_schedule_solves_the_camera_system(C, loop, mode):
+    """Nested-dissection level schedule of the tiled solver: row map and
+    inverse consistent, each tile's rows first and its padding after them
+    (whole cameras in the "cams" tilings), every level's columns independent
+    (no L between them), a banded window in ~log2(T) levels (C4's 64
+    keyframes: 4), and executing the schedule tile by tile solves S x = b."""
     from slam355.ba import tl_schedule, upper_blocks
     from slam355.synthetic import ba_problem, ba_problem_loop
 
@@ -727,11 +743,23 @@ def test_tl_level_schedule_solves_the_camera_system(C, loop):
     ub = upper_blocks(C, ci, pi)
     iu, ju = np.triu_indices(C)
     blocks = np.stack([iu[ub], ju[ub]], 1)
-    sched = tl_schedule(C, blocks)
+    sched = tl_schedule(C, blocks, mode)
     nlev, T = int(sched[0]), int(sched[1])
-    assert T == -(-9 * C // 64) and nlev <= 2 + 2 * int(np.ceil(np.log2(T)))
-    tperm = sched[sched[2]:sched[2] + T]
-    assert sorted(tperm.tolist()) == list(range(T))
+    assert T >= -(-9 * C // 64) and nlev <= 2 + 2 * int(np.ceil(np.log2(T)))
+    if C == 64:
+        assert nlev == 4
+    rn = sched[sched[2]:sched[2] + 9 * C].astype(np.int64)
+    irow = sched[sched[3]:sched[3] + 64 * T]
+    nrow = sched[sched[6]:sched[6] + T]
+    assert nrow.sum() == 9 * C and nrow.min() >= 1 and nrow.max() <= 64
+    assert np.array_equal(irow[rn], np.arange(9 * C)) and (irow >= 0).sum() == 9 * C
+    if mode == "rows64":
+        assert T == -(-9 * C // 64)
+    for I in range(T):  # the tile's rows first, padding after
+        tr = irow[64 * I:64 * I + 64]
+        assert (tr[:nrow[I]] >= 0).all() and (tr[nrow[I]:] < 0).all()
+        if mode != "rows64":  # whole cameras
+            assert nrow[I] % 9 == 0 and (tr[:nrow[I]:9] % 9 == 0).all()
     # S: random SPD with exactly the camera-block pattern
     n = 9 * C
     M = np.zeros((n, n))
@@ -749,17 +777,11 @@ def _emulate_tl_flow(S, b, sched):
     updates over rs(J), its factor and inverse, y_J; each row tile's updates
     over its k list and L_IJ = A_IJ L_JJ^-T; then x_J from the rows' x_I."""
     T = int(sched[1])
-    tperm = sched[sched[2]:sched[2] + T]
     fo = int(sched[5])
     rec = sched[fo:fo + 5 * T].reshape(-1, 5)
     n, TB = len(b), 64
     N = T * TB
-    rn = tperm[np.arange(N) // TB] * TB + np.arange(N) % TB
-    A = np.zeros((N, N))
-    A[np.ix_(rn[:n], rn[:n])] = S
-    A[rn[n:], rn[n:]] = 1.0
-    bb = np.zeros(N)
-    bb[rn[:n]] = b
+    A, bb, rn = _tiled_system(S, b, sched)
     t = lambda I: slice(I * TB, (I + 1) * TB)  # noqa: E731
     dinv, y, x = {}, np.zeros(N), np.zeros(N)
     for J in range(T):
@@ -782,11 +804,12 @@ def _emulate_tl_flow(S, b, sched):
             assert I > J
             r -= A[t(I), t(J)].T @ x[t(I)]
         x[t(J)] = dinv[J].T @ r
-    return x[rn[:n]]
+    return x[rn]
 
 
+@pytest.mark.parametrize("mode", ["cams:5", "cams:7:2", "rows64"])
 @pytest.mark.parametrize("C,loop", [(30, False), (64, False), (120, True), (500, True)])
-def test_tl_flow_table_solves_the_camera_system(C, loop):
+def test_tl_flow_table_solves_the_camera_system(C, loop, mode):
     """Column table of the dataflow tiled solve: every dependency of column J
     is an earlier column (no waits on later workgroups before the back
     substitution), and executing it column by column solves S x = b."""
@@ -798,7 +821,7 @@ def test_tl_flow_table_solves_the_camera_system(C, loop):
     ub = upper_blocks(C, ci, pi)
     iu, ju = np.triu_indices(C)
     blocks = np.stack([iu[ub], ju[ub]], 1)
-    sched = tl_schedule(C, blocks)
+    sched = tl_schedule(C, blocks, mode)
     T = int(sched[1])
     rec = sched[sched[5]:sched[5] + 5 * T].reshape(-1, 5)
     for J, (ro, rc, so, sc, uo) in enumerate(rec):
