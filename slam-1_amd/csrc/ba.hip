@@ -1901,11 +1901,12 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
 #endif
 constexpr int kTB = 64;        // tile edge
 constexpr int kTlHdr = 8;      // ints of the tile schedule's header
+constexpr int kEpiCams = 16;   // cameras per tile in k_tl3_flow's spread epilogue (ba.EPI_CAMS_MAX)
 constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
 
 struct TlLayout {  // doubles inside p.chol; T = the schedule's tile count (ba.tl_schedule)
   int T, N;
-  long long a, dinv, b, y, x, nz, fail, xo, fc, flow, total;
+  long long a, dinv, b, y, x, nz, fail, xo, fc, epi, flow, total;
   __host__ __device__ TlLayout(int n, int n_tiles) {
     T = n_tiles;
     N = T * kTB;
@@ -1918,7 +1919,8 @@ struct TlLayout {  // doubles inside p.chol; T = the schedule's tile count (ba.t
     fail = nz + ((long long)T * T + 7) / 8;
     xo = fail + 8;                       // fail flag + 7 profiling slots (SLAM_TL_PROFILE)
     fc = xo + N;                         // k_tl3_flow: x in camera order; [T][T][64] L_Ik y_k
-    flow = fc + (long long)T * T * kTB;  // (forward-substitution terms), then ints: flags
+    epi = fc + (long long)T * T * kTB;   // (forward-substitution terms); [T][2] epilogue partials
+    flow = epi + 2 * T;                  // (pc, cost per tile), then ints: flags
     // tile[T][T], y[T], x[T]; ticket, epoch, start ticket (+5 spare); retired row
     // tiles + waiter mark cnt[T]; L_JJ^-1 / y_J published dv[T]
     total = flow + ((long long)T * T + 4 * T + 8 + 1) / 2;
@@ -2955,6 +2957,12 @@ __device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int
   return ok;
 }
 
+// one flag, the same contract as flow_wait (its definition follows below)
+__device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh);
+__device__ __forceinline__ bool flow_wait_one(const int* flag, int epoch, int* fail, int* sh) {
+  return flow_wait(flag, epoch, fail, sh);
+}
+
 // Thread 0 polls the parent counter of column J until its low half (retired row
 // tiles) reaches rc -- the retirers' x stores drained before their adds (the
 // counter is the acquire for those bytes); false (uniform) when the solve failed
@@ -2980,12 +2988,6 @@ __device__ bool flow_wait_count(const int* cnt, int rc, int* fail, int* sh) {
   const bool ok = *sh != 0;
   __syncthreads();
   return ok;
-}
-
-// one flag, the same contract as flow_wait (its definition follows below)
-__device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh);
-__device__ __forceinline__ bool flow_wait_one(const int* flag, int epoch, int* fail, int* sh) {
-  return flow_wait(flag, epoch, fail, sh);
 }
 
 // every thread's (sc1) stores drained, then thread 0 raises the flag
@@ -3089,6 +3091,24 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   const int32_t* trows = tl_tile_rows(S, n, T);
   auto nblk = [&](int k) { return (trows[k] + 15) >> 4; };
   const int nbJ = nblk(J);
+  // (4b)'s inputs for the cameras this column owns, loaded before any wait:
+  // thread t < 9 e_cnt takes row t % 9 of owned camera t / 9
+  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);  // b | g | diag U | cost
+  const int cur = cur_of(p.state);
+  const double lam = p.state[SLAM_BA_ST_LAMBDA];
+  const int32_t* erJ = S + S[7] + 2 * J;
+  const int e_off = erJ[0], e_cnt = erJ[1];
+  int e_row = 0, e_rn = 0;
+  double e_cam = 0.0, e_du = 0.0, e_g = 0.0, e_cost = 0.0;
+  if (threadIdx.x < 9 * e_cnt) {
+    e_row = 9 * S[e_off + threadIdx.x / 9] + threadIdx.x % 9;
+    e_rn = tl_new_row(S, e_row);
+    e_cam = p.cams[cur][e_row];
+    e_g = bvec[n + e_row];
+    e_du = bvec[2 * n + e_row];
+  }
+  if (threadIdx.x < e_cnt) e_cost = bvec[3 * n + S[e_off + threadIdx.x]];
+  const int own_orow = threadIdx.x < kTB ? tl_old_row(S, n, J * kTB + threadIdx.x) : -1;
   int* fail = reinterpret_cast<int*>(p.chol + L.fail);
   const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
   double* A = p.chol + L.a;
@@ -3417,6 +3437,18 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     if (t < kTB) st_sc1(p.chol + L.y + J * kTB + t, yv[t]);
     flow_publish(F.dv + J, epoch);
   }
+  // the own column's first two L_IJ in flight before its wait (they are this
+  // workgroup's own stores of (2)): only x_I is loaded after the counter
+  double la_pre[2][16];
+  if (own_sh == 2) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (q < rc) {
+        const double* LIk = A + (size_t)(S[ro + q] * kTB + 16 * w) * L.N + J * kTB + lane;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) la_pre[q][m] = ld_sc1(LIk + (size_t)m * L.N);
+      }
+  }
   for (int it = 0;; ++it) {
     int k;
     bool okk;
@@ -3434,6 +3466,8 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     const bool own = k == J;
     const int32_t* rk = S + S[5] + 5 * k;
     const int kro = rk[0], krc = rk[1], kso = rk[2], ksc = rk[3];
+    // x_k's rows in camera order: loaded before the waits below, off the chain
+    const int orow = own ? own_orow : (t < kTB ? tl_old_row(S, n, k * kTB + t) : -1);
     if (okk) {
       if (!own && t < kTB) yv[t] = ld_sc1(p.chol + L.y + k * kTB + t);
       double s2 = 0.0;
@@ -3442,9 +3476,10 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
         const double* LIk = A + (size_t)(I * kTB + 16 * w) * L.N + k * kTB + lane;
         const double* xI = p.chol + L.x + I * kTB + 16 * w;
         double la[16], xa[16];
+        const bool pre = it == 0 && own_sh == 2 && q < 2;  // (uniform)
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-          la[m] = ld_sc1(LIk + (size_t)m * L.N);
+          la[m] = pre ? (q == 0 ? la_pre[0][m] : la_pre[1][m]) : ld_sc1(LIk + (size_t)m * L.N);
           xa[m] = ld_sc1(xI + m);
         }
 #pragma unroll
@@ -3467,69 +3502,128 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
       __syncthreads();
       if (t < kTB) {
         const double xv = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
+        Xf[t] = xv;  // (4b) (Xf is free after (2))
         st_sc1(p.chol + L.x + k * kTB + t, xv);
-        const int orow = tl_old_row(S, n, k * kTB + t);  // camera order (padding rows dropped)
-        if (orow >= 0) st_sc1(p.chol + L.xo + orow, xv);
+        if (orow >= 0) st_sc1(p.chol + L.xo + orow, xv);  // camera order (padding rows dropped)
       }
     }
     // retire column k even when the solve failed (the counters and the ticket
     // still complete; the epilogue sees the fail code)
     flow_publish(F.xf + k, epoch);
     FLOW_TC(k, 6);
-    // the parent counters (one lane each) and the retire ticket in flight
-    // together -- they are independent, and a chain of returning atomics cost
-    // a device round trip each on the back substitution's critical path; the
-    // columns this retire completes go on the stack in u order as before
+    // the parent counters (one lane each) in flight together -- independent,
+    // and a chain of returning atomics cost a device round trip each on the
+    // back substitution's critical path; the columns this retire completes go
+    // on the stack in u order
     if (t < 64) {
       for (int u0 = 0; u0 == 0 || u0 < ksc; u0 += 64) {
         const int u = u0 + t;
         int c = 0, rcc = 0;
-        unsigned old = 0, oldt = 0;
+        unsigned old = 0;
         if (u < ksc) {
           c = S[kso + u];  // k is a row tile of column c
           rcc = S[S[5] + 5 * c + 1];
           old = ticket_add(reinterpret_cast<uint32_t*>(F.cnt + c));
         }
-        if (u0 == 0 && t == 0) oldt = ticket_add(reinterpret_cast<uint32_t*>(F.ticket));
         const bool push = u < ksc && (int)(old & 0xffffu) == rcc - 1 && (old >> 16) == 0;
         const unsigned long long m = __ballot(push);
         const int base = sp_sh;
         if (push) stk[base + __popcll(m & ((1ull << t) - 1ull))] = c;
         wave_lds_fence();
-        if (t == 0) {
-          sp_sh = base + __popcll(m);
-          if (u0 == 0 && oldt == (unsigned)(T - 1)) last_sh = 1;
-        }
+        if (t == 0) sp_sh = base + __popcll(m);
         wave_lds_fence();
       }
+    }
+    // (4b) the epilogue of the cameras tile k owns (ba.tl_schedule: those whose
+    // lowest tile is k -- every other tile of a camera is a row tile of k, so
+    // its x is already out), after the retire so that no child waits on it:
+    // delta_c, the trial parameters cams[1-cur] and their projection records,
+    // this tile's share of the camera part of the predicted reduction and of
+    // the cost (fixed order) into epi[k]; the same operations whichever
+    // workgroup forms x_k.  Written through (sc1) and drained before the retire
+    // ticket, so that the last retirer's failure path overwrites them safely.
+    {
+      const bool mine = own && own_sh != 0;
+      const int32_t* er = S + S[7] + 2 * k;
+      const int eo = mine ? e_off : er[0], ec = mine ? e_cnt : er[1];
+      double* ct = Xf + kTB;                  // trial parameters [ec][9]
+      double* pv = ct + 9 * kEpiCams;         // pc terms [9 ec]
+      double* cv = pv + 9 * kEpiCams;         // cost terms [ec]
+      if (t < 9 * ec) {
+        int row = e_row, rn = e_rn;
+        double cam = e_cam, du = e_du, g = e_g;
+        if (!mine) {
+          row = 9 * S[eo + t / 9] + t % 9;
+          rn = tl_new_row(S, row);
+          cam = p.cams[cur][row];
+          g = bvec[n + row];
+          du = bvec[2 * n + row];
+        }
+        const double d = (rn >> 6) == k ? Xf[rn & 63] : ld_sc1(p.chol + L.xo + row);
+        st_sc1(p.delta_c + row, d);
+        const double tr = cam + d;
+        st_sc1(p.cams[1 - cur] + row, tr);
+        ct[t] = tr;
+        pv[t] = d * (lam * clampd(du) * d + g);
+      }
+      if (t < ec) cv[t] = mine ? e_cost : bvec[3 * n + S[eo + t]];
+      __syncthreads();
+      if (t < ec) {
+        double rec[kCamRec];
+        cam_prep(ct + 9 * t, rec);
+        double* o = p.camrec[1 - cur] + kCamRec * S[eo + t];
+#pragma unroll
+        for (int i = 0; i < kCamRec; ++i) st_sc1(o + i, rec[i]);
+      }
+      if (t == 0) {
+        double pc = 0.0, cs = 0.0;
+        for (int i = 0; i < 9 * ec; ++i) pc += pv[i];
+        for (int q = 0; q < ec; ++q) cs += cv[q];
+        st_sc1(p.chol + L.epi + 2 * k, pc);
+        st_sc1(p.chol + L.epi + 2 * k + 1, cs);
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (t == 0 && ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1)) last_sh = 1;
     }
     __syncthreads();
   }
   FLOW_FLUSH();
-  // (5) the workgroup that retired the last column runs the epilogue
+  // (5) the workgroup that retired the last column (after its epilogue share)
+  // sums the per-tile partials in tile order; after a failed solve it redoes
+  // the whole epilogue with a zero step instead (its plain stores land after
+  // the shares' drained write-through stores)
   if (!last_sh) return;
 #ifdef SLAM_FLOW_PROFILE
   if (t == 0) g_flow_epi[0] = wall_clock64();
 #endif
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
-  const bool good = fcode == 0;
-  double* xs = VX;  // n <= 2 * 64 * 64 (host-checked)
-  for (int i0 = t; i0 < n; i0 += 8 * kTlWG) {  // 8 loads in flight per thread
-    double xv[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) xv[q] = good ? ld_sc1(p.chol + L.xo + min(i0 + q * kTlWG, n - 1)) : 0.0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (i0 + q * kTlWG < n) xs[i0 + q * kTlWG] = xv[q];
+  if (fcode != 0) {
+    const double* gvec = bvec + n;
+    solve_epilogue<true>(p, p.chol + L.xo, false, &part[0][0],
+                         EpiSrc{gvec, bvec + 2 * n, p.cams[cur], gvec + 2 * n}, fcode);
+  } else if (t < 64) {
+    double pc = 0.0, cs = 0.0;  // lane t: tiles t, t + 64, ...; then a fixed shuffle tree
+    for (int k = t; k < T; k += 64) {
+      pc += ld_sc1(p.chol + L.epi + 2 * k);
+      cs += ld_sc1(p.chol + L.epi + 2 * k + 1);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      pc += __shfl_down(pc, off, 64);
+      cs += __shfl_down(cs, off, 64);
+    }
+    if (t == 0) {
+      p.state[SLAM_BA_ST_COST] = 0.5 * cs;
+      p.state[SLAM_BA_ST_PRED_CAM] = 0.5 * pc;
+      p.state[SLAM_BA_ST_CHOL_FAIL] = 0.0;
+    }
   }
-  __syncthreads();
 #ifdef SLAM_FLOW_PROFILE
-  if (t == 0) g_flow_epi[1] = wall_clock64();
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) g_flow_epi[3] = wall_clock64();
 #endif
-  const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);
-  const double* gvec = bvec + n;
-  solve_epilogue<true>(p, xs, good, &part[0][0],
-                 EpiSrc{gvec, bvec + 2 * n, p.cams[cur_of(p.state)], gvec + 2 * n}, fcode);
   FLOW_TC(J, 7);
 }
 

@@ -93,6 +93,7 @@ def upper_blocks(n_cams, cam_idx, pt_idx):
 
 
 TB = 64  # tile edge of the tiled solver (csrc/ba.hip kTB)
+EPI_CAMS_MAX = 16  # cameras per tile in the dataflow solve's spread epilogue (csrc/ba.hip kEpiCams)
 TILE_MODE = "rows64"  # default tiling of the camera solve (tl_schedule; measured best)
 
 
@@ -280,7 +281,7 @@ def tl_schedule(n_cams, blocks, mode=None):
     Returns the int32 schedule (device and host copies are the same array):
       [0] nlev, [1] T, [2] row map offset, [3] inverse row map offset,
       [4] level table offset, [5] column table offset, [6] tile size table
-      offset, [7] reserved (0)
+      offset, [7] epilogue table offset
       row map: row r of S -> row of the tiled system (tile * 64 + position)
       inverse row map: row of the tiled system -> row of S, -1 on padding rows
       tile sizes: per tile its rows of S (they come first, padding after)
@@ -292,7 +293,8 @@ def tl_schedule(n_cams, blocks, mode=None):
       level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
-      back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)"""
+      back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)
+      epilogue table: per tile (off, cnt) of the cameras it owns (list after)"""
     blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
     n = 9 * int(n_cams)
     tiles = tile_rows(int(n_cams), blocks, mode)
@@ -405,7 +407,25 @@ def tl_schedule(n_cams, blocks, mode=None):
             pairs.append((put(ks), len(ks)))
         u_off = put([v for pr in pairs for v in pr])
         recs[5 * J:5 * J + 5] = [r_off, len(rows), s_off, len(rs[J]), u_off]
-    return np.asarray(flat + recs + tail, np.int32)
+    # the cameras whose share of the solve's epilogue (trial parameters,
+    # projection record, predicted-reduction and cost terms) the workgroup that
+    # forms x of tile k runs: those whose lowest-numbered tile is k -- a camera
+    # whose rows straddle two tiles couples them, so the lower one is a
+    # descendant of the other and its x is formed last
+    own = [[] for _ in range(T)]
+    for c in range(int(n_cams)):
+        own[int(tile_of[9 * c:9 * c + 9].min())].append(c)
+    if max((len(o) for o in own), default=0) > EPI_CAMS_MAX:
+        raise ValueError(f"tl_schedule: a tile owns more than {EPI_CAMS_MAX} cameras' epilogue")
+    epi_off = flow_off + 5 * T + len(tail)
+    epi, lo = [], epi_off + 2 * T
+    for o in own:
+        epi += [lo, len(o)]
+        lo += len(o)
+    epi += [c for o in own for c in o]
+    out = np.asarray(flat + recs + tail + epi, np.int32)
+    out[7] = epi_off
+    return out
 
 
 def _pairs_by_point(cam_idx, pt_idx):
