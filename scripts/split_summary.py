@@ -1,6 +1,6 @@
 """Per-rank split of the sharded LM iteration (scripts/gpu_r5_split3.sh output):
 rocprofv3 kernel averages of each {C4|C5}_w{W}_r{r} run -> divided (k_lin_mfma +
-k_assemble + k_back_trial) and replicated (k_tl3_flow + k_tl2_load +
+k_asm_fill + k_assemble + k_back_trial) and replicated (k_tl3_flow + k_tl2_load +
 k_tl2_scatter) microseconds per LM iteration, plus the run's own wall time per
 iteration.   python scripts/split_summary.py OUTDIR > summary.json"""
 import csv
@@ -9,7 +9,7 @@ import json
 import os
 import sys
 
-DIV = ("k_lin_mfma", "k_assemble", "k_back_trial")
+DIV = ("k_lin_mfma", "k_asm_fill", "k_assemble", "k_back_trial")
 REP = ("k_tl3_flow", "k_tl2_load", "k_tl2_scatter")
 
 

@@ -54,16 +54,16 @@ constexpr int kBS = 256;   // block size of the element-wise kernels
 // Batched LM: independent problems (local-BA windows) advance through one set
 // of launches, one problem per blockIdx.y; each keeps its own buffers and LM
 // state, so the iterates of a batched problem equal its solo iterates.  The
-// problem descriptors travel by value in the kernel arguments (16 x 296 B).
+// problem descriptors travel by value in the kernel arguments (16 x 392 B).
 constexpr int kBaMaxBatch = SLAM_BA_MAX_BATCH;
 struct BaBatch {
   slam_ba_problem p[kBaMaxBatch];
 };
 #define BA_PROB(b) const slam_ba_problem& p = (b).p[blockIdx.y]
-// the batch travels by value in the kernel arguments: 16 x 376 B,
+// the batch travels by value in the kernel arguments: 16 x 392 B,
 // beyond the traditional 4 KB; ROCm 7.2 takes it (tests/test_ba.py launches 16)
-static_assert(sizeof(slam_ba_problem) <= 376, "slam_ba_problem grew: re-check the kernarg size");
-static_assert(sizeof(BaBatch) <= 16 * 376, "BaBatch kernel argument size");
+static_assert(sizeof(slam_ba_problem) <= 392, "slam_ba_problem grew: re-check the kernarg size");
+static_assert(sizeof(BaBatch) <= 16 * 392, "BaBatch kernel argument size");
 
 // The LM kernels are short and latency-bound and usually share their CUs with
 // the (throughput-bound) ORB workgroups of the concurrent tracking stream: they
@@ -1252,12 +1252,12 @@ __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, in
 // once, full 9x9, at sys + 81 * blk.
 __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
   BA_PROB(bat);
-  if ((int)blockIdx.x >= p.n_blocks) return;
+  if ((int)blockIdx.x >= (p.asm_act != nullptr ? p.n_asm_act : p.n_blocks)) return;
   lm_wave_priority();
   __shared__ double red[kAsmWG / 81][kCPart];
   __shared__ double sh[kCPart];
   __shared__ double sb[81];
-  const int blk = blockIdx.x;
+  const int blk = p.asm_act != nullptr ? p.asm_act[blockIdx.x] : (int)blockIdx.x;
   const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
   const int C9 = 9 * p.n_cams;
   double* S = p.sys;
@@ -1307,6 +1307,21 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
     diagU[9 * c1 + t] = sh[99 + t];
   }
   if (diag && t == 0) costc[c1] = sh[108];
+}
+
+// sys of a problem with an active-block list, before k_assemble writes the
+// listed blocks: what k_assemble writes for a block without partial rows --
+// S -0.0, and for a camera without rows b = g = -0.0, diag U = cost = +0.0
+// (S's diagonal block of such a camera gets -0.0 where k_assemble would write
+// +0.0: a sign of zero, which the all-reduce's sum with the rank that observes
+// the camera does not see)
+__global__ __launch_bounds__(256) void k_asm_fill(BaBatch bat) {
+  BA_PROB(bat);
+  if (p.asm_act == nullptr) return;
+  const size_t ns = (size_t)p.n_blocks * 81, c9 = 9 * (size_t)p.n_cams;
+  const size_t n = ns + 3 * c9 + p.n_cams;  // S | b | g | diag U | cost
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    p.sys[i] = i < ns + 2 * c9 ? -0.0 : 0.0;
 }
 
 // ---------------------------------------------------------------- solve
@@ -3896,6 +3911,11 @@ int check_problem(const slam_ba_problem* p) {
                "diagonal and every block with common points (packed)", kDenseMaxN);
   SLAM_REQUIRE(!p->tl_sched == !p->tl_sched_host,
                "slam_ba: tl_sched and tl_sched_host come together");
+  SLAM_REQUIRE(p->asm_act == nullptr ||
+                   (sys_packed(p->n_cams) && p->asm_tab == nullptr && p->n_asm_act >= 0 &&
+                    p->n_asm_act <= p->n_blocks),
+               "slam_ba: asm_act (n_asm_act %d of %d blocks) needs a packed system without asm_tab",
+               p->n_asm_act, p->n_blocks);
   SLAM_REQUIRE(p->tl_mode == 0 || p->tl_mode == 1, "slam_ba: tl_mode must be 0 or 1");
   SLAM_REQUIRE(!sys_packed(p->n_cams) || p->chol != nullptr,
                "slam_ba: chol workspace (slam_ba_chol_len doubles) required for 9C > %d",
@@ -3957,6 +3977,7 @@ namespace {
 struct Launch {
   BaBatch b;
   int n, max_grps, max_blocks, max_sgrps, mode;
+  int fill_blocks;  // largest n_blocks of a problem with an active-block list (0: none)
   size_t solve_lds;
   bool dense;
 };
@@ -3970,7 +3991,7 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
   SLAM_REQUIRE(n >= 1 && n <= kBaMaxBatch, "slam_ba: batch of %d problems (1..%d)", n, kBaMaxBatch);
   SLAM_REQUIRE(probs != nullptr, "slam_ba: null problem array");
   L->n = n;
-  L->max_grps = L->max_blocks = L->max_sgrps = 0;
+  L->max_grps = L->max_blocks = L->max_sgrps = L->fill_blocks = 0;
   L->mode = probs[0].lin_mode;
   L->solve_lds = 0;
   L->dense = true;
@@ -3984,7 +4005,8 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
     L->b.p[i] = probs[i];
     L->max_grps = max(L->max_grps, probs[i].n_grps);
     L->max_sgrps = max(L->max_sgrps, probs[i].n_sgrps);
-    L->max_blocks = max(L->max_blocks, probs[i].n_blocks);
+    L->max_blocks = max(L->max_blocks, probs[i].asm_act != nullptr ? probs[i].n_asm_act : probs[i].n_blocks);
+    if (probs[i].asm_act != nullptr) L->fill_blocks = max(L->fill_blocks, probs[i].n_blocks);
     L->solve_lds = std::max(L->solve_lds, sizeof(double) * BlkLds(9 * probs[i].n_cams).total);
     L->solve_lds = std::max(L->solve_lds, g_solve_lds_floor);
     L->dense = L->dense && !sys_packed(probs[i].n_cams);
@@ -4012,6 +4034,10 @@ static int launch_build(const Launch& L, hipStream_t s) {
     SLAM_LAUNCHED("k_linearize");
   }
   if (!folded) {  // k_lin_mfma skips the fold of a problem without asm_tab
+    if (L.fill_blocks > 0) {  // the unlisted blocks of active-block problems
+      k_asm_fill<<<dim3(std::min((L.fill_blocks * 81 + 255) / 256, 512), L.n), 256, 0, s>>>(L.b);
+      SLAM_LAUNCHED("k_asm_fill");
+    }
     k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
     SLAM_LAUNCHED("k_assemble");
   }

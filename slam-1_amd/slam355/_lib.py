@@ -40,6 +40,7 @@ class BAProblemStruct(ctypes.Structure):
         ("state", c_p), ("ticket", c_p),
         ("sg_ptr", c_p), ("sg_meta", c_p), ("obs_meta", c_p), ("chk_optr", c_p), ("chk_cptr", c_p),
         ("bslot_ab", c_p), ("tl_sched", c_p), ("tl_sched_host", c_p), ("asm_tab", c_p),
+        ("asm_act", c_p), ("n_asm_act", c_int), ("asm_pad", c_int),
     ]
 
 

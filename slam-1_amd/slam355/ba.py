@@ -957,6 +957,21 @@ class BAProblem:
         if pl["mode"] == 1 and fold_assembly:  # k_lin_mfma assembles sys itself
             t["asm_tab"] = T(assembly_table(C, pl))
             s.asm_tab = t["asm_tab"].data_ptr()
+        elif self.tl_levels:
+            # a landmark shard lists the global blocks but has partial rows for few
+            # of them: k_assemble runs over the blocks with rows here, one fill
+            # launch writes the zeros of the rest (C5 rank 0 of 8: 3000
+            # workgroups -> ~400)
+            blk = np.asarray(pl["blocks"]).reshape(-1, 2)
+            bp = np.asarray(pl["blk_bslot_ptr"])
+            cp = np.asarray(pl["cam_cslot_ptr"])
+            rows = bp[1:] > bp[:-1]
+            diag = blk[:, 0] == blk[:, 1]
+            rows[diag] |= cp[blk[diag, 0] + 1] > cp[blk[diag, 0]]
+            act = np.nonzero(rows)[0].astype(np.int32)
+            if len(act) < len(blk):
+                t["asm_act"] = T(act)
+                s.asm_act, s.n_asm_act = t["asm_act"].data_ptr(), len(act)
         self._s = s
         self.reset(lam0)
 
