@@ -602,7 +602,13 @@ def run_tracking(args, world, rank):
                    "last_set_cost_mean": float(np.mean([s_["COST"] for s_ in sts])) if sts else None,
                    "last_set_accepted_mean": float(np.mean([s_["NACCEPT"] for s_ in sts])) if sts else None,
                    "note": ("local BA on windows built from the bench's own tracked frames (lag 2: "
-                            "host build of step k-2's windows overlaps step k's tracking); not the headline")}
+                            "host build of step k-2's windows overlaps step k's tracking); not the headline. "
+                            "The windows hold ~1/30 of C3's observations (8 cameras x ~830 points x ~1000 "
+                            "observations vs 10 x 5000 x 30000); the reference's export conventions "
+                            "(camera-to-world poses fed to the world-to-camera BAL projection, KITTI's "
+                            "613/185 principal point on 1280x720 frames: XXXport_files.py:51-60, "
+                            "BundleAdjustment.py:317-328) make each window ill-posed (cost ~1e8, <= 3 of 10 "
+                            "steps accepted), so this leg times LM throughput, not convergence")}
         torch.cuda.synchronize()
         tleg["wms"], tleg["last"] = None, None
     frames = reduce_scalar(float(B * args.steps), world, "sum")
