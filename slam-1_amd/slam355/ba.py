@@ -843,7 +843,7 @@ class BAProblem:
 
     def __init__(self, cams, pts, cam_idx, pt_idx, qs, *, lam0=1e-4, stream=None,
                  block_list=None, lin_mode="auto", chunks_per_wg=None, tl_mode="flow",
-                 fold_assembly=False, tile_mode=None):
+                 fold_assembly=False, tile_mode=None, active_blocks=True):
         """lin_mode: "mfma" (camera-union linearisation, k_lin_mfma: Schur
         contraction on the f64 matrix cores; points renumbered internally),
         "slot" (k_linearize, any observation structure) or "auto" (mfma when
@@ -852,6 +852,8 @@ class BAProblem:
         tl_mode "flow" runs it as one dataflow launch (k_tl3_flow, on any
         stream and CU mask), "levels" one launch pair per elimination-tree level;
         tile_mode: the tiling of that solve (tile_rows; default TILE_MODE).
+        active_blocks (packed systems): k_assemble only over the blocks with
+        partial rows here (a landmark shard), a fill launch for the rest.
         fold_assembly (lin_mode mfma): k_lin_mfma's last supergroup per camera
         block sums the block's partial rows into the system (no k_assemble
         launch).  Off by default: measured slower (the workgroup that finishes
@@ -957,7 +959,7 @@ class BAProblem:
         if pl["mode"] == 1 and fold_assembly:  # k_lin_mfma assembles sys itself
             t["asm_tab"] = T(assembly_table(C, pl))
             s.asm_tab = t["asm_tab"].data_ptr()
-        elif self.tl_levels:
+        elif self.tl_levels and active_blocks:
             # a landmark shard lists the global blocks but has partial rows for few
             # of them: k_assemble runs over the blocks with rows here, one fill
             # launch writes the zeros of the rest (C5 rank 0 of 8: 3000

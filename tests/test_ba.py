@@ -317,6 +317,33 @@ def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
         assert np.allclose(gp, op, rtol=1e-6, atol=1e-9), it
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["flow", "levels"])
+def test_gpu_tiled_solve_failure_leaves_a_zero_step(mode):
+    """A damping that makes the camera system indefinite (lambda = -1e6): the
+    tiled factor fails (CHOL_FAIL 1, not a timed-out wait), the step is
+    rejected and the parameters stay; the solve's epilogue writes a zero camera
+    step and trial cameras equal to the live ones -- in the dataflow form after
+    the per-tile epilogue shares have written theirs (the last retirer's
+    failure path overwrites them)."""
+    import torch
+    from slam355 import ba
+
+    cams, pts, ci, pi, qs = make_problem(44, 40, 1500, 5)
+    prob = ba.BAProblem(cams, pts, ci, pi, qs, tl_mode=mode)
+    c_before, p_before = prob.params()
+    prob.reset(-1e6)
+    prob.iterate(1)
+    torch.cuda.synchronize()
+    st = prob.state()
+    assert st["CHOL_FAIL"] == 1.0 and st["ACCEPTED"] == 0.0 and st["SOLVE_FAULT"] == 0.0
+    c_after, p_after = prob.params()
+    assert np.array_equal(c_after, c_before) and np.array_equal(p_after, p_before)
+    cur = int(st["CUR"] != 0)
+    assert not prob.t["delta_c"].cpu().numpy().any()
+    assert np.array_equal(prob.t[f"cams{1 - cur}"].cpu().numpy(), prob.t[f"cams{cur}"].cpu().numpy())
+
+
 def test_planner_packed_block_list():
     """9C > 120: the plan lists only the diagonal and the camera pairs with a
     common point (the packed sys layout); an explicit global list is honoured

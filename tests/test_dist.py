@@ -153,6 +153,46 @@ def test_gpu_step_distributed_matches_single_rank(tmp_path, C, P, k, iters, loop
     assert np.allclose(d["cams"], cams, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("r", [0, 5])
+def test_gpu_shard_active_block_assembly_equals_full_launch(r):
+    """A landmark shard's system (rank r of 8 of a 120-keyframe loop) assembled
+    over its blocks with partial rows only (asm_act + the fill launch) equals the
+    assembly over every listed block: the same values, the blocks without rows
+    -0.0 bit for bit (the diagonal of a camera the shard does not observe may
+    differ in the sign of its zero), and the LM iterates on it bit for bit."""
+    import torch
+    from slam355.ba import BAProblem, upper_blocks
+    from slam355.dist import shard_by_anchor
+
+    C, P = 120, 24000
+    c0, p0, ci, pi, qs = _problem(C, P, 6, True)
+    mine, keep, lpi = shard_by_anchor(C, P, ci, pi, r, 8)
+    blocks = upper_blocks(C, ci, pi)
+    args = (c0, p0[mine], ci[keep], lpi, qs[keep])
+    act = BAProblem(*args, block_list=blocks)
+    full = BAProblem(*args, block_list=blocks, active_blocks=False)
+    assert act._s.asm_act != 0 and 0 < act._s.n_asm_act < act._s.n_blocks and full._s.asm_act is None
+    for pr in (act, full):
+        pr.build_system()
+    torch.cuda.synchronize()
+    a, f = act.t["sys"].cpu().numpy(), full.t["sys"].cpu().numpy()
+    assert np.array_equal(a, f)  # (+0 == -0)
+    nb = act._s.n_blocks
+    blk = np.asarray(act.plan["blocks"]).reshape(-1, 2)
+    listed = np.zeros(nb, bool)
+    listed[act.t["asm_act"].cpu().numpy()] = True
+    off = ~listed & (blk[:, 0] != blk[:, 1])
+    sa, sf = a[:81 * nb].reshape(nb, 81), f[:81 * nb].reshape(nb, 81)
+    assert np.array_equal(sa[off].view(np.uint64), sf[off].view(np.uint64))
+    assert (sa[off].view(np.uint64) == np.uint64(1 << 63)).all()  # -0.0
+    for pr in (act, full):
+        pr.iterate(2)
+    assert act.state() == full.state()
+    for x, y in zip(act.params(), full.params()):
+        assert np.array_equal(x, y)
+
+
 # ---------------------------------------------------------------- pose chain of frame-pair shards
 def _pose_results(n, seed=5):
     """PnP results of n frame pairs: small motions, a few stale (-1) pairs."""
