@@ -392,13 +392,15 @@ typedef struct slam_ba_problem {
    * row_blk[n_bslots] (block of each bpart row), n_empty, empty[n_empty]
    * (blocks with no partial row here: zeroed every build). */
   int32_t* asm_tab;
-  /* Optional (null: all n_blocks): the listed blocks this problem's assembly
-   * writes -- those with partial rows here (a landmark shard touches few of the
-   * global list).  One fill launch writes the zeros of the others first (S
-   * -0.0, and b, g -0.0 / diag U, cost +0.0 for a camera without rows: what the
-   * assembly writes for them, up to the sign of a zero on the diagonal of a
-   * camera this rank does not observe).  Packed systems (9C > 120) without
-   * asm_tab only; ascending. */
+  /* Optional (null: all n_blocks): the blocks this problem's assembly runs
+   * over -- those with partial rows here (a landmark shard touches few of the
+   * global list): asm_act[n_asm_act] ascending block indices, then a 0/1 flag
+   * per block (listed or not) and a 0/1 flag per camera (its diagonal block
+   * listed).  Those workgroups also write the zeros of the unlisted blocks (S
+   * -0.0, and b, g -0.0 / diag U, cost +0.0 for a camera without rows: what
+   * the assembly writes for them, up to the sign of a zero on the diagonal of
+   * a camera this rank does not observe).  Packed systems (9C > 120) without
+   * asm_tab only; n_asm_act >= 1. */
   const int32_t* asm_act;
   int32_t n_asm_act;
   int32_t asm_pad;

@@ -1258,6 +1258,24 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
   __shared__ double sh[kCPart];
   __shared__ double sb[81];
   const int blk = p.asm_act != nullptr ? p.asm_act[blockIdx.x] : (int)blockIdx.x;
+  if (p.asm_act != nullptr) {
+    // this workgroup's share of the zeros of the unlisted blocks and of the
+    // vector entries of the cameras without rows (what the assembly writes for
+    // them: S -0.0, b and g -0.0, diag U and cost +0.0), beside the listed
+    // blocks that the workgroups write (disjoint addresses, no ordering needed)
+    const int32_t* listed = p.asm_act + p.n_asm_act;  // [n_blocks] 0/1
+    const int32_t* camrows = listed + p.n_blocks;      // [n_cams] 0/1
+    const size_t ns = (size_t)p.n_blocks * 81, c9 = 9 * (size_t)p.n_cams, nv = ns + 3 * c9 + p.n_cams;
+    for (size_t i = (size_t)blockIdx.x * kAsmWG + threadIdx.x; i < nv; i += (size_t)p.n_asm_act * kAsmWG) {
+      if (i < ns) {
+        if (!listed[i / 81]) p.sys[i] = -0.0;
+      } else {
+        const size_t j = i - ns;
+        const int cam = j < 3 * c9 ? (int)((j % c9) / 9) : (int)(j - 3 * c9);
+        if (!camrows[cam]) p.sys[i] = j < 2 * c9 ? -0.0 : 0.0;
+      }
+    }
+  }
   const int c1 = p.blocks[2 * blk], c2 = p.blocks[2 * blk + 1];
   const int C9 = 9 * p.n_cams;
   double* S = p.sys;
@@ -1307,21 +1325,6 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
     diagU[9 * c1 + t] = sh[99 + t];
   }
   if (diag && t == 0) costc[c1] = sh[108];
-}
-
-// sys of a problem with an active-block list, before k_assemble writes the
-// listed blocks: what k_assemble writes for a block without partial rows --
-// S -0.0, and for a camera without rows b = g = -0.0, diag U = cost = +0.0
-// (S's diagonal block of such a camera gets -0.0 where k_assemble would write
-// +0.0: a sign of zero, which the all-reduce's sum with the rank that observes
-// the camera does not see)
-__global__ __launch_bounds__(256) void k_asm_fill(BaBatch bat) {
-  BA_PROB(bat);
-  if (p.asm_act == nullptr) return;
-  const size_t ns = (size_t)p.n_blocks * 81, c9 = 9 * (size_t)p.n_cams;
-  const size_t n = ns + 3 * c9 + p.n_cams;  // S | b | g | diag U | cost
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-    p.sys[i] = i < ns + 2 * c9 ? -0.0 : 0.0;
 }
 
 // ---------------------------------------------------------------- solve
@@ -1795,7 +1798,7 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
     // registers (317 per lane: one wave per SIMD, so a solve workgroup waited
     // for a whole idle CU beside ORB); at 210 (two waves per SIMD) the batched
     // local-BA stage in the tracking bench drops 3.1 -> 2.75 ms per step
-    // (profiles/r4/solve_lowreg_ab/)
+    // (profiles/r4/solve_lowreg_ab/ at git f26058c)
     const int tr = c0 + kPanelW;
 #pragma unroll
     for (int s = 0; s < kTileMax; ++s) {
@@ -1915,7 +1918,7 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
 #define SLAM_TL_PADSKIP 1  // the tile factor skips the pivot chain of padding blocks
 #endif
 constexpr int kTB = 64;        // tile edge
-constexpr int kTlHdr = 8;      // ints of the tile schedule's header
+constexpr int kTlHdr = 10;     // ints of the tile schedule's header
 constexpr int kEpiCams = 16;   // cameras per tile in k_tl3_flow's spread epilogue (ba.EPI_CAMS_MAX)
 constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
 
@@ -2894,7 +2897,7 @@ __device__ unsigned long long g_flow_sub[SLAM_TL_FLOW_MAX_T][8];
 #endif
 
 struct FlowPtrs {
-  int *tile, *yf, *xf, *ticket, *epoch, *start, *cnt, *dv;
+  int *tile, *yf, *xf, *ticket, *epoch, *start, *fail, *cnt, *dv;
   __device__ FlowPtrs(const slam_ba_problem& p, const TlLayout& L) {
     int* base = reinterpret_cast<int*>(p.chol + L.flow);
     tile = base;
@@ -2903,6 +2906,7 @@ struct FlowPtrs {
     ticket = xf + L.T;
     epoch = ticket + 1;
     start = ticket + 2;
+    fail = ticket + 3;  // k_tl3_flow's epoch-tagged fail word
     cnt = ticket + 8;
     dv = cnt + L.T;
   }
@@ -2914,6 +2918,13 @@ __device__ __forceinline__ int ld_flag(const int* f) {
 __device__ __forceinline__ void st_flag(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The dataflow solve's fail word carries its solve: (epoch << 2) | code, code
+// 1 a non-SPD tile, 2 a timed-out wait -- so no launch has to clear it
+__device__ __forceinline__ int flow_fcode(const int* fail, int epoch) {
+  const int v = ld_flag(fail);
+  return (v >> 2) == epoch ? (v & 3) : 0;
+}
+__device__ __forceinline__ void flow_fail(int* fail, int epoch, int code) { st_flag(fail, (epoch << 2) | code); }
 
 // Thread 0 polls until *flag == epoch; false (uniform) when the solve failed or
 // the wait timed out (which marks it failed).
@@ -2921,12 +2932,12 @@ __device__ bool flow_wait(const int* flag, int epoch, int* fail, int* sh) {
   if (threadIdx.x == 0) {
     int ok = 1;
     for (int spins = 0; ld_flag(flag) != epoch; ++spins) {
-      if (ld_flag(fail) != 0) {
+      if (flow_fcode(fail, epoch) != 0) {
         ok = 0;
         break;
       }
       if (spins > kFlowSpinMax) {
-        st_flag(fail, 2);
+        flow_fail(fail, epoch, 2);
         ok = 0;
         break;
       }
@@ -2952,12 +2963,12 @@ __device__ bool flow_wait_many(const int* base, const int32_t* idx, int cnt, int
       for (int spins = 0;; ++spins) {
         const bool up = f == nullptr || ld_flag(f) == epoch;
         if (__all(up)) break;
-        if (ld_flag(fail) != 0) {
+        if (flow_fcode(fail, epoch) != 0) {
           ok = 0;
           break;
         }
         if (spins > kFlowSpinMax) {
-          if (lane == 0) st_flag(fail, 2);
+          if (lane == 0) flow_fail(fail, epoch, 2);
           ok = 0;
           break;
         }
@@ -2982,16 +2993,16 @@ __device__ __forceinline__ bool flow_wait_one(const int* flag, int epoch, int* f
 // tiles) reaches rc -- the retirers' x stores drained before their adds (the
 // counter is the acquire for those bytes); false (uniform) when the solve failed
 // or the wait timed out.
-__device__ bool flow_wait_count(const int* cnt, int rc, int* fail, int* sh) {
+__device__ bool flow_wait_count(const int* cnt, int rc, int epoch, int* fail, int* sh) {
   if (threadIdx.x == 0) {
     int ok = 1;
     for (int spins = 0; (ld_flag(cnt) & 0xffff) < rc; ++spins) {
-      if (ld_flag(fail) != 0) {
+      if (flow_fcode(fail, epoch) != 0) {
         ok = 0;
         break;
       }
       if (spins > kFlowSpinMax) {
-        st_flag(fail, 2);
+        flow_fail(fail, epoch, 2);
         ok = 0;
         break;
       }
@@ -3071,6 +3082,37 @@ __device__ __forceinline__ void gemm_xyT_acc(const double* Xf, const double* Yf,
   }
 }
 
+// Elements of the damped tiled system gathered straight from the packed S
+// (what k_tl2_load + k_tl2_scatter lay out for the level-scheduled solve),
+// through the schedule's per-column gather tables (ba.tl_schedule): gt = the
+// tile's [64][64] packed-S offsets (-1 zero, -2 a padding row's unit
+// diagonal).  Two rounds of independent loads for all N elements (offsets,
+// then values); dg: the diagonal tile's rows of S, for lambda clamp(diag U) on
+// its diagonal (null for a row tile).
+template <int N>
+__device__ __forceinline__ void tl_gather(const double* __restrict__ sys, const int32_t* gt,
+                                          const int32_t* dg, const double* dU, double lam,
+                                          const int (&ri)[N], const int (&ci)[N], double* out) {
+  int g[N], r[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    g[i] = gt[ri[i] * kTB + ci[i]];
+    r[i] = dg != nullptr && ri[i] == ci[i] ? dg[ri[i]] : -1;
+  }
+  double v[N], d[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    v[i] = sys[max(g[i], 0)];
+    d[i] = r[i] >= 0 ? dU[r[i]] : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double x = g[i] >= 0 ? v[i] : (g[i] == -2 ? 1.0 : 0.0);
+    if (r[i] >= 0) x += lam * clampd(d[i]);
+    out[i] = x;
+  }
+}
+
 // lower 16x16 blocks (row, column) of the diagonal update per wave of k_tl3_flow
 __constant__ int kDiagBlk[4][3][2] = {{{0, 0}, {3, 0}, {3, 1}}, {{1, 0}, {1, 1}, {3, 2}},
                                       {{2, 0}, {2, 1}, {2, 0}}, {{2, 2}, {3, 3}, {2, 2}}};
@@ -3088,17 +3130,24 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   __shared__ double part[4][kTB];
   __shared__ double yv[kTB];
   __shared__ double rv[kTB];
-  __shared__ int shf, okf, col_sh;
+  __shared__ int shf, okf, col_sh, ep_sh;
   __shared__ double VR[kTB * kVR];        // L_JJ^-1 row-major (stride 65): (3), this column's x
   __shared__ int stk[SLAM_TL_FLOW_MAX_T], sp_sh, cur_sh, last_sh, own_sh;
 #ifdef SLAM_FLOW_PROFILE
   __shared__ unsigned long long flow_lds[16];
 #endif
-  // the column: the start ticket hands them out in the order the workgroups start
-  if (threadIdx.x == 0)
-    col_sh = (int)ticket_add(reinterpret_cast<uint32_t*>(F.start));
+  // the column: the start ticket hands them out in the order the workgroups
+  // start.  The ticket is never reset: every solve takes exactly T tickets, so
+  // ticket v is column v mod T of solve v / T, whose number is the epoch that
+  // every flag of this solve carries (no clearing launch before the solve)
+  if (threadIdx.x == 0) {
+    const unsigned v = ticket_add(reinterpret_cast<uint32_t*>(F.start));
+    col_sh = (int)(v % (unsigned)T);
+    ep_sh = (int)(v / (unsigned)T) + 1;
+  }
   __syncthreads();
   const int J = col_sh;
+  const int epoch = ep_sh;
   const int32_t* rec = S + S[5] + 5 * J;
   const int ro = rec[0], rc = rec[1], so = rec[2], sc = rec[3], uo = rec[4];
   // rows of a tile (its rows of S first, padding after them): the 16-row
@@ -3124,8 +3173,16 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   }
   if (threadIdx.x < e_cnt) e_cost = bvec[3 * n + S[e_off + threadIdx.x]];
   const int own_orow = threadIdx.x < kTB ? tl_old_row(S, n, J * kTB + threadIdx.x) : -1;
-  int* fail = reinterpret_cast<int*>(p.chol + L.fail);
-  const int epoch = *F.epoch;  // bumped by k_tl2_load (the previous launch)
+  const double b_own = own_orow >= 0 ? bvec[own_orow] : 0.0;  // b_J in the tiled order (3)
+  int* fail = F.fail;
+  // this column's parent counter, re-armed before any tile of J is published:
+  // no row tile of J can retire before J's tiles exist (x_I needs L_IJ)
+  if (threadIdx.x == 0) st_flag(F.cnt + J, 0);
+  // this column's gather tables: its diagonal tile, row tile q at 1 + q, the
+  // diagonal tile's rows of S after them
+  const int32_t* gtJ = S + S[S[9] + J];
+  const int32_t* dgJ = gtJ + (1 + rc) * kTB * kTB;
+  const double* dU = bvec + 2 * n;
   double* A = p.chol + L.a;
   double* Vf = VX;
   double* Yf = VX + kTB * kTB;
@@ -3143,27 +3200,33 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     dC[b] = kDiagBlk[w][b][1];
   }
   const int dnb = w < 2 ? 3 : 2;
-  // A_JJ's blocks (scattered by the previous launch) in registers before any wait
+  // A_JJ's blocks, gathered from the packed system into registers before any
+  // wait (no load / scatter launch before the solve)
   double ajj[12];
+  {
+    int gi[12], gj[12];
 #pragma unroll
-  for (int b = 0; b < 3; ++b)
+    for (int b = 0; b < 3; ++b)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = dR[b] * 16 + (lane >> 4) + 4 * r, col = dC[b] * 16 + (lane & 15);
-      ajj[4 * b + r] = A[(size_t)(J * kTB + row) * L.N + J * kTB + col];
-    }
+      for (int r = 0; r < 4; ++r) {
+        gi[4 * b + r] = dR[b] * 16 + (lane >> 4) + 4 * r;
+        gj[4 * b + r] = dC[b] * 16 + (lane & 15);
+      }
+    tl_gather<12>(p.sys, gtJ, dgJ, dU, lam, gi, gj, ajj);
+  }
   // ... and the first two row tiles' A_IJ
   double air[2][16];
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int I = q < rc ? S[ro + q] : J;
+    int gi[16], gj[16];
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
-        air[q][4 * s2 + r] = A[(size_t)(I * kTB + row) * L.N + J * kTB + col];
+        gi[4 * s2 + r] = w * 16 + (lane >> 4) + 4 * r;
+        gj[4 * s2 + r] = s2 * 16 + (lane & 15);
       }
+    tl_gather<16>(p.sys, gtJ + (q < rc ? 1 + q : 0) * kTB * kTB, nullptr, dU, lam, gi, gj, air[q]);
   }
   // (1) diagonal tile, child tiles k in rs order: L_Jk operands double-buffered
   // (Xf / VX[4096:]); the next child's tile is fetched before this one's MFMAs
@@ -3270,7 +3333,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     }
     __syncthreads();  // VX is reused below
     if (!ok) {
-      if (t == 0) st_flag(fail, 1);
+      if (t == 0) flow_fail(fail, epoch, 1);
     } else {
 #pragma unroll
       for (int m = 0; m < 16; ++m) {
@@ -3333,11 +3396,15 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) a[e] = air[qc][e];
     } else {
+      int gi[16], gj[16];
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          a[4 * s2 + r] = AIJ[(size_t)(w * 16 + (lane >> 4) + 4 * r) * L.N + s2 * 16 + (lane & 15)];
+        for (int r = 0; r < 4; ++r) {
+          gi[4 * s2 + r] = w * 16 + (lane >> 4) + 4 * r;
+          gj[4 * s2 + r] = s2 * 16 + (lane & 15);
+        }
+      tl_gather<16>(p.sys, gtJ + (1 + q) * kTB * kTB, nullptr, dU, lam, gi, gj, a);
     }
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2)
@@ -3379,7 +3446,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   if (ok) ok = flow_wait_many(F.yf, S + so, sc, epoch, fail, &shf);
   if (ok) {
     if (t < kTB) {
-      double r = p.chol[L.b + J * kTB + t];
+      double r = b_own;
       for (int q0 = 0; q0 < sc; q0 += 16) {
         double v[16];
 #pragma unroll
@@ -3438,7 +3505,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     own_sh = 0;
     if (rc == 0) {
       own_sh = 1;
-    } else if (ld_flag(F.start) >= T) {
+    } else if (ld_flag(F.start) >= epoch * T) {  // every workgroup of this solve has started
       const unsigned old = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(F.cnt + J), 1u << 16,
                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       own_sh = (int)(old & 0xffffu) < rc ? 2 : 0;
@@ -3470,7 +3537,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
     if (it == 0) {  // this workgroup's own column, when it forms it
       if (!own_sh) continue;
       k = J;
-      okk = ok && (own_sh == 1 || flow_wait_count(F.cnt + J, rc, fail, &shf));
+      okk = ok && (own_sh == 1 || flow_wait_count(F.cnt + J, rc, epoch, fail, &shf));
     } else {
       if (t == 0) cur_sh = sp_sh > 0 ? stk[--sp_sh] : -1;
       __syncthreads();
@@ -3599,7 +3666,9 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
       }
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      if (t == 0 && ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) == (unsigned)(T - 1)) last_sh = 1;
+      // (never reset: T retires per solve, the last of each solve is T - 1 mod T)
+      if (t == 0 && ticket_add(reinterpret_cast<uint32_t*>(F.ticket)) % (unsigned)T == (unsigned)(T - 1))
+        last_sh = 1;
     }
     __syncthreads();
   }
@@ -3613,7 +3682,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   if (t == 0) g_flow_epi[0] = wall_clock64();
 #endif
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int fcode = ld_flag(fail);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
+  const int fcode = flow_fcode(fail, epoch);  // 0 ok, 1 non-SPD tile, 2 a wait timed out
   if (fcode != 0) {
     const double* gvec = bvec + n;
     solve_epilogue<true>(p, p.chol + L.xo, false, &part[0][0],
@@ -3672,7 +3741,7 @@ static int tl_check_sched(const slam_ba_problem& p) {
   const int32_t* h = p.tl_sched_host;
   const int n = 9 * p.n_cams, T = h[1];
   SLAM_REQUIRE(T >= (n + kTB - 1) / kTB && h[2] == kTlHdr && h[3] == kTlHdr + n &&
-                   h[6] == kTlHdr + n + T * kTB,
+                   h[6] == kTlHdr + n + T * kTB && h[8] > 0 && h[9] > 0,
                "slam_ba: tl_sched layout is not ba.tl_schedule's (T %d, offsets %d %d %d for n %d)", T,
                h[2], h[3], h[6], n);
   return SLAM_OK;
@@ -3681,9 +3750,7 @@ static int tl_check_sched(const slam_ba_problem& p) {
 static int tl_solve_flow(const slam_ba_problem& p, hipStream_t s) {
   const TlLayout L(9 * p.n_cams, p.tl_sched_host[1]);
   if (int rc = tl_check_sched(p)) return rc;
-  tl_load(p, s);
-  k_tl2_scatter<<<p.n_blocks, 128, 0, s>>>(p, L.T);
-  k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p, L.T);
+  k_tl3_flow<<<L.T, kTlWG, 0, s>>>(p, L.T);  // gathers its tiles from the packed system itself
   SLAM_LAUNCHED("k_tl3_flow");
   return SLAM_OK;
 }
@@ -3912,7 +3979,7 @@ int check_problem(const slam_ba_problem* p) {
   SLAM_REQUIRE(!p->tl_sched == !p->tl_sched_host,
                "slam_ba: tl_sched and tl_sched_host come together");
   SLAM_REQUIRE(p->asm_act == nullptr ||
-                   (sys_packed(p->n_cams) && p->asm_tab == nullptr && p->n_asm_act >= 0 &&
+                   (sys_packed(p->n_cams) && p->asm_tab == nullptr && p->n_asm_act >= 1 &&
                     p->n_asm_act <= p->n_blocks),
                "slam_ba: asm_act (n_asm_act %d of %d blocks) needs a packed system without asm_tab",
                p->n_asm_act, p->n_blocks);
@@ -3977,7 +4044,6 @@ namespace {
 struct Launch {
   BaBatch b;
   int n, max_grps, max_blocks, max_sgrps, mode;
-  int fill_blocks;  // largest n_blocks of a problem with an active-block list (0: none)
   size_t solve_lds;
   bool dense;
 };
@@ -3991,7 +4057,7 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
   SLAM_REQUIRE(n >= 1 && n <= kBaMaxBatch, "slam_ba: batch of %d problems (1..%d)", n, kBaMaxBatch);
   SLAM_REQUIRE(probs != nullptr, "slam_ba: null problem array");
   L->n = n;
-  L->max_grps = L->max_blocks = L->max_sgrps = L->fill_blocks = 0;
+  L->max_grps = L->max_blocks = L->max_sgrps = 0;
   L->mode = probs[0].lin_mode;
   L->solve_lds = 0;
   L->dense = true;
@@ -4006,7 +4072,6 @@ static int make_launch(const slam_ba_problem* probs, int n, Launch* L) {
     L->max_grps = max(L->max_grps, probs[i].n_grps);
     L->max_sgrps = max(L->max_sgrps, probs[i].n_sgrps);
     L->max_blocks = max(L->max_blocks, probs[i].asm_act != nullptr ? probs[i].n_asm_act : probs[i].n_blocks);
-    if (probs[i].asm_act != nullptr) L->fill_blocks = max(L->fill_blocks, probs[i].n_blocks);
     L->solve_lds = std::max(L->solve_lds, sizeof(double) * BlkLds(9 * probs[i].n_cams).total);
     L->solve_lds = std::max(L->solve_lds, g_solve_lds_floor);
     L->dense = L->dense && !sys_packed(probs[i].n_cams);
@@ -4034,10 +4099,6 @@ static int launch_build(const Launch& L, hipStream_t s) {
     SLAM_LAUNCHED("k_linearize");
   }
   if (!folded) {  // k_lin_mfma skips the fold of a problem without asm_tab
-    if (L.fill_blocks > 0) {  // the unlisted blocks of active-block problems
-      k_asm_fill<<<dim3(std::min((L.fill_blocks * 81 + 255) / 256, 512), L.n), 256, 0, s>>>(L.b);
-      SLAM_LAUNCHED("k_asm_fill");
-    }
     k_assemble<<<dim3(L.max_blocks, L.n), kAsmWG, 0, s>>>(L.b);
     SLAM_LAUNCHED("k_assemble");
   }

@@ -204,7 +204,7 @@ constexpr int kMxWaves = kMxWG / kWave;
 // 2897 vs 2429 Gpairs/s at batch 32), 6 inside the tracking pipeline (192
 // instead of 248 VGPRs, so its waves find room beside the local-BA and tail
 // kernels on the CUs ORB leaves: 19.4-19.7k vs 19.0-19.1k frames/s in
-// alternating runs, profiles/r3_sweeps/mxqb_pipe_v1/) -- the pipeline wins.
+// alternating runs, profiles/r3_sweeps/mxqb_pipe_v1/ in git history before 1bfa753) -- the pipeline wins.
 #ifndef SLAM_MX_QB
 #define SLAM_MX_QB 6
 #endif

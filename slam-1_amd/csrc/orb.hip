@@ -228,7 +228,7 @@ __device__ unsigned long long g_orb_prof[96];
 // -DSLAM_ORB_CUT=k (profiling builds only, scripts/build_variant.sh + scripts/gpu_profile.sh): every
 // level stops after phase k (1 resize, 2 FAST, 3 NMS, 6 rank, 7 IC angle,
 // 8 blur), so the SQ counters of successive cuts split the LDS instructions /
-// bank conflicts by phase (profiles/r3_orb_lds_phases_v1.json).
+// bank conflicts by phase (profiles/r3_orb_lds_phases_v1.json, git history before 1bfa753).
 #ifdef SLAM_ORB_CUT
 #define ORB_CUT(ph) \
   if ((ph) == SLAM_ORB_CUT) continue

@@ -281,7 +281,8 @@ def tl_schedule(n_cams, blocks, mode=None):
     Returns the int32 schedule (device and host copies are the same array):
       [0] nlev, [1] T, [2] row map offset, [3] inverse row map offset,
       [4] level table offset, [5] column table offset, [6] tile size table
-      offset, [7] epilogue table offset
+      offset, [7] epilogue table offset, [8] block index table offset,
+      [9] gather table offset
       row map: row r of S -> row of the tiled system (tile * 64 + position)
       inverse row map: row of the tiled system -> row of S, -1 on padding rows
       tile sizes: per tile its rows of S (they come first, padding after)
@@ -294,7 +295,11 @@ def tl_schedule(n_cams, blocks, mode=None):
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
       back entries (k, soff, scnt) -- the rows I of L_Ik (ancestors)
-      epilogue table: per tile (off, cnt) of the cameras it owns (list after)"""
+      epilogue table: per tile (off, cnt) of the cameras it owns (list after)
+      block index table: [C][C], the packed block of cameras (c1 <= c2), -1 if none
+      gather table: per column its offset (T), then per column the packed-S
+        offsets of its diagonal and row tiles' elements [1 + rows][64][64]
+        (-1 zero, -2 unit diagonal) and its diagonal tile's rows of S [64]"""
     blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
     n = 9 * int(n_cams)
     tiles = tile_rows(int(n_cams), blocks, mode)
@@ -324,7 +329,7 @@ def tl_schedule(n_cams, blocks, mode=None):
             level[parent[k]] = max(level[parent[k]], level[k] + 1)
     nlev = max(level) + 1 if T else 0
     cols = [[k for k in range(T) if level[k] == lv] for lv in range(nlev)]
-    head = [nlev, T, 0, 0, 0, 0, 0, 0]
+    head = [nlev, T, 0, 0, 0, 0, 0, 0, 0, 0]
     table = []
     lists = []  # (k lists / struct lists) appended after the entries
 
@@ -423,8 +428,42 @@ def tl_schedule(n_cams, blocks, mode=None):
         epi += [lo, len(o)]
         lo += len(o)
     epi += [c for o in own for c in o]
-    out = np.asarray(flat + recs + tail + epi, np.int32)
+    # dense camera-pair -> packed block index (-1: no block): the dataflow
+    # solve gathers its tiles straight from the packed system through it
+    bix = np.full((int(n_cams), int(n_cams)), -1, np.int64)
+    bix[blocks[:, 0], blocks[:, 1]] = np.arange(len(blocks))
+    bix_off = epi_off + len(epi)
+    # per column J: for its diagonal tile and each row tile (rows order), the
+    # packed-S offset of every element (i, j) of the 64 x 64 tile (-1: zero;
+    # -2: a padding row's unit diagonal), then the row of S of each of the
+    # diagonal tile's 64 rows (-1: padding) for the damping: the dataflow solve
+    # gathers its tiles in two rounds of loads (offsets, then values)
+    gt_base = bix_off + bix.size
+    gofs, gtab, o = [], [], gt_base + T
+    ii, jj = np.meshgrid(np.arange(TB), np.arange(TB), indexing="ij")
+    for J in range(T):
+        gofs.append(o)
+        for I in [J] + sorted(struct[J]):
+            r, c = irow[I * TB + ii], irow[J * TB + jj]
+            valid = (r >= 0) & (c >= 0)
+            a, b = np.maximum(r, 0) // 9, np.maximum(c, 0) // 9
+            sw = a > b
+            blk = np.where(sw, bix[b, a], bix[a, b])
+            e = np.where(sw, 9 * (np.maximum(c, 0) % 9) + np.maximum(r, 0) % 9,
+                         9 * (np.maximum(r, 0) % 9) + np.maximum(c, 0) % 9)
+            g = np.where(valid & (blk >= 0), 81 * blk + e, -1)
+            g = np.where(~valid & (I * TB + ii == J * TB + jj), -2, g)
+            gtab.append(g.ravel())
+            o += TB * TB
+        gtab.append(irow[J * TB:J * TB + TB])
+        o += TB
+    gt = np.concatenate(gtab) if gtab else np.zeros(0, np.int64)
+    if o >= 2 ** 31:
+        raise ValueError("tl_schedule: the gather tables exceed int32 offsets")
+    out = np.asarray(flat + recs + tail + epi + bix.ravel().tolist() + gofs + gt.tolist(), np.int32)
     out[7] = epi_off
+    out[8] = bix_off
+    out[9] = gt_base
     return out
 
 
@@ -859,7 +898,8 @@ class BAProblem:
         launch).  Off by default: measured slower (the workgroup that finishes
         last assembles every block it touched, a serial tail; 16 C3 windows
         326 vs 225 us per iteration, C4 406 vs 324 us, tracking 19.0k vs 19.9k
-        frames/s, profiles/r4/fold_ab/)."""
+        frames/s, profiles/r4/fold_ab/ at f26058c; landmark shards at W = 8 too: C4
+        296 vs 155 us, C5 903 vs 387 us per iteration, profiles/r6/asm_fold/)."""
         if tl_mode not in ("flow", "levels"):
             raise ValueError(f"tl_mode must be 'flow' or 'levels', not {tl_mode!r}")
         dev = require_gpu()
@@ -961,9 +1001,9 @@ class BAProblem:
             s.asm_tab = t["asm_tab"].data_ptr()
         elif self.tl_levels and active_blocks:
             # a landmark shard lists the global blocks but has partial rows for few
-            # of them: k_assemble runs over the blocks with rows here, one fill
-            # launch writes the zeros of the rest (C5 rank 0 of 8: 3000
-            # workgroups -> ~400)
+            # of them: k_assemble runs over the blocks with rows here (C5 rank 0
+            # of 8: 3000 workgroups -> ~400), which also write the zeros of the
+            # rest (table: the listed blocks, a flag per block, a flag per camera)
             blk = np.asarray(pl["blocks"]).reshape(-1, 2)
             bp = np.asarray(pl["blk_bslot_ptr"])
             cp = np.asarray(pl["cam_cslot_ptr"])
@@ -971,8 +1011,10 @@ class BAProblem:
             diag = blk[:, 0] == blk[:, 1]
             rows[diag] |= cp[blk[diag, 0] + 1] > cp[blk[diag, 0]]
             act = np.nonzero(rows)[0].astype(np.int32)
-            if len(act) < len(blk):
-                t["asm_act"] = T(act)
+            if 0 < len(act) < len(blk):
+                camrows = np.zeros(C, np.int32)
+                camrows[blk[diag & rows, 0]] = 1
+                t["asm_act"] = T(np.concatenate([act, rows.astype(np.int32), camrows]))
                 s.asm_act, s.n_asm_act = t["asm_act"].data_ptr(), len(act)
         self._s = s
         self.reset(lam0)

@@ -798,6 +798,48 @@ def test_tl_level_schedule_solves_the_camera_system(C, loop, mode):
     assert np.allclose(x, np.linalg.solve(S, b), rtol=0, atol=1e-10 * np.abs(x).max())
 
 
+@pytest.mark.parametrize("mode", ["rows64", "cams:5"])
+@pytest.mark.parametrize("C,loop", [(30, False), (120, True)])
+def test_tl_gather_tables_lay_out_the_system(C, loop, mode):
+    """The dataflow solve's gather tables (k_tl3_flow reads its diagonal and
+    row tiles straight from the packed system): every element of every
+    structural tile, looked up in a packed S with the damping on the diagonal,
+    equals the tiled layout of S (unit diagonal on padding rows, zeros off the
+    blocks)."""
+    from slam355.ba import tl_schedule, upper_blocks
+    from slam355.synthetic import ba_problem, ba_problem_loop
+
+    rng = np.random.default_rng(C + 7)
+    cams, pts, ci, pi, qs = (ba_problem_loop if loop else ba_problem)(rng, C, 20 * C, 5)
+    ub = upper_blocks(C, ci, pi)
+    iu, ju = np.triu_indices(C)
+    blocks = np.stack([iu[ub], ju[ub]], 1)
+    sched = tl_schedule(C, blocks, mode)
+    n, T = 9 * C, int(sched[1])
+    packed = rng.normal(size=(len(blocks), 9, 9))
+    dU, lam = rng.uniform(1.0, 2.0, n), 0.37
+    Sd = np.zeros((n, n))
+    for k, (c1, c2) in enumerate(blocks):
+        Sd[9 * c1:9 * c1 + 9, 9 * c2:9 * c2 + 9] = packed[k]
+        if c1 != c2:
+            Sd[9 * c2:9 * c2 + 9, 9 * c1:9 * c1 + 9] = packed[k].T
+    Sd[np.arange(n), np.arange(n)] += lam * dU
+    A, _, _ = _tiled_system(Sd, np.zeros(n), sched)
+    flat = packed.ravel()
+    rec = sched[sched[5]:sched[5] + 5 * T].reshape(-1, 5)
+    for J in range(T):
+        ro, rc = rec[J][:2]
+        base = int(sched[sched[9] + J])
+        dg = sched[base + (1 + rc) * 4096:base + (1 + rc) * 4096 + 64]
+        for q, I in enumerate([J] + list(sched[ro:ro + rc])):
+            g = sched[base + q * 4096:base + (q + 1) * 4096].reshape(64, 64).astype(np.int64)
+            got = np.where(g >= 0, flat[np.maximum(g, 0)], np.where(g == -2, 1.0, 0.0))
+            if q == 0:
+                d = np.arange(64)
+                got[d[dg >= 0], d[dg >= 0]] += lam * dU[dg[dg >= 0]]
+            assert np.array_equal(got, A[64 * I:64 * I + 64, 64 * J:64 * J + 64]), (J, q)
+
+
 def _emulate_tl_flow(S, b, sched):
     """The dataflow tiled solve (csrc/ba.hip k_tl3_flow) restated in NumPy,
     column by column from the schedule's column table: the diagonal tile's
