@@ -184,28 +184,64 @@ def _nd_tiles(adj, comp, cap, chain):
     return out + _chunk(adj, order[i:r + 1], cap)
 
 
-def _nd_order(adj, nodes):
+def _dist_from(adj, comp, srcs):
+    """BFS distance inside comp from the nodes srcs (multi-source)."""
+    dist = {v: 0 for v in srcs}
+    frontier = list(srcs)
+    while frontier:
+        nxt = []
+        for u in frontier:
+            for v in adj[u]:
+                if v in comp and v not in dist:
+                    dist[v] = dist[u] + 1
+                    nxt.append(v)
+        frontier = nxt
+    return dist
+
+
+def _nd_order(adj, nodes, bound=frozenset()):
     """Nested-dissection order of `nodes` in the 64-row tile graph (the
     "rows64" tiling): each connected component separately; a component whose
     BFS level structure has >= 3 levels is split by its middle level, the
-    separator numbered last."""
+    separator numbered last.  `bound`: the separators already numbered after
+    these nodes (their ancestors).  A component next to them is levelled from
+    its node furthest from them, so that its own separator sits nearer to them:
+    the part between the two separators is the smaller one (a single tile on a
+    band), and the larger part -- a chain of tiles on a band, eliminated from
+    its far end -- shares no row with the ancestors.  Otherwise the top of that
+    chain would carry a row to an ancestor, and its parent's update with it
+    would wait until after the parent's factor (a deferred row fold on the
+    critical path: C4's right half, 6.5 us)."""
     out = []
     for comp in _components(adj, nodes):
+        near = {u for u in comp if adj[u] & bound}
+        dist = _dist_from(adj, comp, near) if near else None
         if len(comp) <= 2:
-            out += sorted(comp)
+            # a chain of <= 2 tiles: its far end first (it then shares no row with
+            # the ancestors), otherwise ascending
+            out += sorted(comp, key=(lambda v: (-dist.get(v, 0), v)) if dist else None)
             continue
         levels = _bfs_levels(adj, comp, min(comp))
-        for _ in range(2):
+        for _ in range(2):  # pseudo-peripheral
             far = min(levels[-1])
             lv2 = _bfs_levels(adj, comp, far)
             if len(lv2) <= len(levels):
                 break
             levels = lv2
+        if dist:
+            # from the node furthest from the ancestors, when that levels the
+            # component as deeply as a pseudo-peripheral node does (a band
+            # touching them at one end; not a path they bound at both ends,
+            # whose middle would give levels of two tiles)
+            root = min(comp, key=lambda v: (-dist.get(v, 0), v))
+            lvb = _bfs_levels(adj, comp, root)
+            if len(lvb) >= len(levels):
+                levels = lvb
         if len(levels) < 3:
             out += sorted(comp)
             continue
         sep = set(levels[len(levels) // 2])
-        out += _nd_order(adj, comp - sep) + sorted(sep)
+        out += _nd_order(adj, comp - sep, bound | sep) + sorted(sep)
     return out
 
 
