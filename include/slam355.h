@@ -485,10 +485,12 @@ int slam_ba_stage_windows(int n_win, int n, int cap, const double* rows, const i
 /* Number of doubles red_part needs for a problem with n_grps point groups. */
 int slam_ba_red_slots(int n_grps);
 /* Doubles of the tiled-Cholesky workspace `chol` (needed only when 9C > 120)
- * for a tile schedule of n_tiles tiles (tl_sched[1]; slam355/ba.py
- * tl_schedule cuts the system into tiles of whole cameras, so a schedule may
- * have more tiles than 9C / 64); n_tiles <= 0: ceil(9C / 64). */
-long long slam_ba_chol_len(int n_cams, int n_tiles);
+ * for a tile schedule (the host copy tl_sched_host, slam355/ba.py
+ * tl_schedule): its tile count tl_sched_host[1] (a schedule of whole-camera
+ * tiles may have more tiles than 9C / 64) and its product slots
+ * tl_sched_host[11] (the 64x64 terms L_Ik L_Jk^T that column k forms for
+ * column J's first two row tiles).  NULL: ceil(9C / 64) tiles, no slots. */
+long long slam_ba_chol_len(int n_cams, const int32_t* tl_sched_host);
 /* Doubles in the all-reduced system buffer `sys`: dense (9C <= 120) (9C)^2,
  * packed (9C > 120) 81 * n_blocks (the listed upper camera blocks), then
  * b, g, diag U (9C each) and the per-camera cost (C). */

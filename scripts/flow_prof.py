@@ -31,15 +31,14 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
     st = runs[-1]
     t0 = st[:, 0].min()
     rel = (st - t0) * 10 / 1000.0  # us
+    dump = {"config": name, "T": T, "stamps_us": rel.round(2).tolist()}
     print(f"{name}: T={T} span {rel[:, 6].max():.1f} us (to last x), epilogue end {rel[:, 7].max():.1f}")
     sched = prob._sched_host
     rec = sched[sched[5]:sched[5] + 5 * T].reshape(-1, 5)
-    for J in range(T):
+    for J in range(min(T, 26)):
         d = np.diff(rel[J, :7])
         print(f"  col {J:3d} rows {rec[J,1]} rs {rec[J,3]}: start {rel[J,0]:7.1f} " +
               " ".join(f"{PH[i]} {d[i]:6.1f}" for i in range(6)) + f" | x at {rel[J,6]:7.1f}")
-        if J > 24:
-            break
     fs = getattr(_lib.lib, "slam_flow_sub_stamps", None)
     if fs is not None:
         fs.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -47,6 +46,15 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
         fs(ctypes.cast(sb, ctypes.c_void_p), T)
         raw = np.array(sb[:], np.uint64).reshape(T, 8).astype(np.float64)
         sub = np.where((raw > t0) & (raw < t0 + 1e8), (raw - t0) * 10 / 1000.0, np.nan)
+        dump["sub_us"] = np.nan_to_num(sub, nan=-1.0).round(2).tolist()
+        rec_ = prob._sched_host[prob._sched_host[5]:prob._sched_host[5] + 5 * T].reshape(-1, 5)
+        sh_ = prob._sched_host
+        dump["rows"] = [sh_[r[0]:r[0] + r[1]].tolist() for r in rec_]
+        dump["rs"] = [sh_[r[2]:r[2] + r[3]].tolist() for r in rec_]
+        if len(sys.argv) > 1:
+            import json as _json
+            with open(f"{sys.argv[1]}_{name}.json", "w") as fo:
+                _json.dump(dump, fo)
         rs = sched  # rs(J) list at rec[J, 2], count rec[J, 3]; rows at rec[J, 0], count rec[J, 1]
         print("  row 0 of each column (us, absolute): first child in / last child in / factor end /"
               " folds done / staged / product / published | parent's last child in")
@@ -59,7 +67,7 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
                     last_in = f"{sub[P, 1]:7.1f} (+{sub[P, 1] - sub[J, 5]:.1f})"
             print(f"  col {J:3d}: " + " ".join(f"{sub[J, i]:7.1f}" for i in (0, 1)) + f" {rel[J, 2]:7.1f} " +
                   " ".join(f"{sub[J, i]:7.1f}" for i in (2, 3, 4, 5)) + " | " + last_in +
-                  f" | staging at the barrier: wave 0 {sub[J, 6]:7.1f}, waves 1-3 {sub[J, 7]:7.1f}")
+                  f" | deferred fold: tile in view {sub[J, 6]:7.1f}, loaded {sub[J, 7]:7.1f}")
     fe = getattr(_lib.lib, "slam_flow_epi_stamps", None)
     if fe is not None:
         fe.argtypes = [ctypes.c_void_p]

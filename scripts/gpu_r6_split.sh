@@ -22,6 +22,6 @@ import json;d=json.load(open('$OUT/split/summary.json'))
 for k,v in d.items(): print(k, 'div', v['divided'], 'rep', v['replicated'], 'wall', v.get('wall_us_per_iter'))"
 cd "$ROOT"
 if [ -f slam-1_amd/prof/libslam355_fp.so ]; then
-  SLAM355_LIB=$ROOT/slam-1_amd/prof/libslam355_fp.so timeout -k 10 200 python3 scripts/flow_prof.py > $OUT/flow_phases.log 2>&1 || exit 1
+  SLAM355_LIB=$ROOT/slam-1_amd/prof/libslam355_fp.so timeout -k 10 200 python3 scripts/flow_prof.py $OUT/flow > $OUT/flow_phases.log 2>&1 || exit 1
   grep "^C4\|^C5" $OUT/flow_phases.log
 fi

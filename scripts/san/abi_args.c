@@ -121,7 +121,8 @@ int main(void) {
     expect_arg(slam_ba_reset_batch(&pr, -1, 1e-3, NULL), "ba reset n<0");
     expect_arg(slam_ba_residual(P, P, P, P, P, -1, P, NULL), "ba residual n_obs<0");
     expect_arg(slam_ba_jacobian(P, P, P, P, P, 4, P, NULL, NULL), "ba jacobian null jac");
-    expect(slam_ba_chol_len(100, 0) > 0 && slam_ba_chol_len(100, 40) > slam_ba_chol_len(100, 0) && slam_ba_sys_len(100, 300) > 0, "ba sizes");
+    int32_t sched40[12] = {1, 40, 0, 0, 0, 0, 0, 0, 0, 0, 0, 3};  /* header only: 40 tiles, 3 slots */
+    expect(slam_ba_chol_len(100, NULL) > 0 && slam_ba_chol_len(100, sched40) > slam_ba_chol_len(100, NULL) && slam_ba_sys_len(100, 300) > 0, "ba sizes");
     expect(slam_ba_red_slots(7) >= 1, "ba red slots");
   }
   /* pose graph / BoW */

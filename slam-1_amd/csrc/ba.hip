@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(kBlkWG) __attribute__((amdgpu_waves_per_eu(2))) voi
 #define SLAM_TL_PADSKIP 1  // the tile factor skips the pivot chain of padding blocks
 #endif
 constexpr int kTB = 64;        // tile edge
-constexpr int kTlHdr = 10;     // ints of the tile schedule's header
+constexpr int kTlHdr = 12;     // ints of the tile schedule's header
 constexpr int kEpiCams = 16;   // cameras per tile in k_tl3_flow's spread epilogue (ba.EPI_CAMS_MAX)
 constexpr int kTlWG = 256;     // 4 waves: wave w owns rows 16w..16w+15 of a tile
 
@@ -1942,6 +1942,12 @@ struct TlLayout {  // doubles inside p.chol; T = the schedule's tile count (ba.t
     // tile[T][T], y[T], x[T]; ticket, epoch, start ticket (+5 spare); retired row
     // tiles + waiter mark cnt[T]; L_JJ^-1 / y_J published dv[T]
     total = flow + ((long long)T * T + 4 * T + 8 + 1) / 2;
+    // then k_tl3_flow's product slots (tl_sched[11] of them, slam_ba_chol_len):
+    // [slots][64][64] terms L_Ik L_Jk^T, then one epoch flag (int) per slot
+  }
+  __host__ __device__ long long prod(int slot) const { return total + (long long)slot * kTB * kTB; }
+  __host__ __device__ long long with_slots(int n_slots) const {
+    return prod(n_slots) + ((long long)n_slots + 1) / 2;
   }
 };
 
@@ -2571,7 +2577,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
 // k_tl2_unperm moves x back to the camera order (into the y region, which the
 // epilogue reads).  A banded window of T tiles runs ~log2 T levels instead of
 // T panel steps (C4: 4 levels for 9 tiles; C5: 8 for 71).
-// The schedule's row maps sit at fixed offsets after its 8-int header (ba.tl_schedule;
+// The schedule's row maps sit at fixed offsets after its kTlHdr-int header (ba.tl_schedule;
 // checked on the host in tl_check_sched), so no lookup waits on a header load:
 // row r of S (camera order) -> its row in the tiled system
 __device__ __forceinline__ int tl_new_row(const int32_t* sched, int r) { return sched[kTlHdr + r]; }
@@ -2886,7 +2892,7 @@ __device__ unsigned long long g_flow_sub[SLAM_TL_FLOW_MAX_T][8];
       for (int i_ = 0; i_ < 5; ++i_) g_flow_stamp[J][i_] = flow_lds[i_];         \
       for (int i_ = 0; i_ < 6; ++i_) g_flow_sub[J][i_] = flow_lds[8 + i_];       \
       g_flow_sub[J][6] = flow_lds[5];                                            \
-      g_flow_sub[J][7] = max(flow_lds[6], max(flow_lds[7], flow_lds[14]));         \
+      g_flow_sub[J][7] = flow_lds[6];                                            \
     }                                                                            \
   } while (0)
 #else
@@ -2897,7 +2903,7 @@ __device__ unsigned long long g_flow_sub[SLAM_TL_FLOW_MAX_T][8];
 #endif
 
 struct FlowPtrs {
-  int *tile, *yf, *xf, *ticket, *epoch, *start, *fail, *cnt, *dv;
+  int *tile, *yf, *xf, *ticket, *epoch, *start, *fail, *cnt, *dv, *pf;
   __device__ FlowPtrs(const slam_ba_problem& p, const TlLayout& L) {
     int* base = reinterpret_cast<int*>(p.chol + L.flow);
     tile = base;
@@ -2909,6 +2915,7 @@ struct FlowPtrs {
     fail = ticket + 3;  // k_tl3_flow's epoch-tagged fail word
     cnt = ticket + 8;
     dv = cnt + L.T;
+    pf = reinterpret_cast<int*>(p.chol + L.prod(p.tl_sched[11]));  // product slot flags
   }
 };
 
@@ -3155,6 +3162,14 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   const int32_t* trows = tl_tile_rows(S, n, T);
   auto nblk = [&](int k) { return (trows[k] + 15) >> 4; };
   const int nbJ = nblk(J);
+  // Product tasks (ba.tl_schedule): the terms L_Ik L_Jk^T of a column J's rows
+  // 0 and 1 are formed by column k itself, as soon as both of its tiles exist,
+  // into slots that J sums after its factor -- J's diagonal phase never waits
+  // for a child's later row tiles, which its children publish after the L_Jk
+  // that phase needs.  This column's tasks (a, b, slot), ordered by b.
+  const int32_t* tkJ = S + S[S[10] + 2 * J];
+  const int n_tk = S[S[10] + 2 * J + 1];
+  double* prod = p.chol + L.prod(0);
   // (4b)'s inputs for the cameras this column owns, loaded before any wait:
   // thread t < 9 e_cnt takes row t % 9 of owned camera t / 9
   const double* bvec = p.sys + sys_vec_off(p.n_cams, p.n_blocks);  // b | g | diag U | cost
@@ -3232,22 +3247,12 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   // (Xf / VX[4096:]); the next child's tile is fetched before this one's MFMAs
   // when its flag is already up (loads in flight under the MFMAs), after them
   // otherwise (a child that is not ready yet never holds up the MFMAs of the
-  // ones that are).  Row tiles 0 and 1 take their updates sum_k L_Ik L_Jk^T
-  // here too, child by child as it arrives (L_Ik staged in VR, free until the
-  // factor), for every child but the last: the last child's row tiles are
-  // published after its L_Jk, so they are folded in after the factor (2).
-  // The sums run over k in the same order as before: bit-identical.
+  // ones that are).  Row tiles 0 and 1 take their updates from the product
+  // slots after the factor (2).
   d4 acc[4];
 #pragma unroll
   for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
-  d4 racc[2][4];
-#pragma unroll
-  for (int q2 = 0; q2 < 2; ++q2)
-#pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) racc[q2][s2] = d4{0.0, 0.0, 0.0, 0.0};
-  int rptr[2] = {0, 0};  // next entry of row tile q2's k list (uniform)
-  // The buffers alternate so that the LAST child's L_Jk lands in Xf, which the
-  // factor leaves alone: (2) reuses it for that child's deferred row updates.
+  // The buffers alternate so that the LAST child's L_Jk lands in Xf.
   if (sc > 0) {
     ok = flow_wait(F.tile + J * T + S[so], epoch, fail, &shf);
     if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so] * kTB, L.N, ((sc - 1) & 1) ? Yf : Xf);
@@ -3256,7 +3261,6 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   for (int q = 0; q < sc && ok; ++q) {
     double* cur = ((sc - 1 - q) & 1) ? Yf : Xf;
     double* nxt = ((sc - 1 - q) & 1) ? Xf : Yf;
-    const int k = S[so + q];
     __syncthreads();  // cur filled; the previous MFMAs' reads of nxt done
     if (q == sc - 1) FLOW_S(1);
     bool pre = false;
@@ -3267,8 +3271,8 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
       __syncthreads();
       if (pre) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
     }
-    const int kmk = nblk(k);  // child k's column blocks past its rows: zeros
 #if SLAM_TL_KSKIP
+    const int kmk = nblk(S[so + q]);  // child k's column blocks past its rows: zeros
     for (int kb = 0; kb < kmk; ++kb)
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4)
@@ -3287,21 +3291,7 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
                                                       cur[((dC[b] * 16 + kk) << 6) + lane], acc[b], 0, 0, 0);
 #endif
     if (q + 1 < sc) {
-#pragma unroll
-      for (int q2 = 0; q2 < 2; ++q2) {
-        if (q2 >= rc) break;
-        const int ko = S[uo + 2 * q2], kc = S[uo + 2 * q2 + 1];
-        if (rptr[q2] >= kc || S[ko + rptr[q2]] != k) continue;  // (uniform)
-        ++rptr[q2];
-        const int I = S[ro + q2];
-        ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);
-        if (!ok) break;
-        tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, VR);
-        __syncthreads();  // VR filled
-        gemm_xyT_acc(VR, cur, racc[q2], kmk);
-        __syncthreads();  // VR reads done
-      }
-      if (ok && !pre) {
+      if (!pre) {
         ok = flow_wait(F.tile + J * T + S[so + q + 1], epoch, fail, &shf);
         if (ok) tile_to_frag_sc1(A + (size_t)J * kTB * L.N + S[so + q + 1] * kTB, L.N, nxt);
       }
@@ -3349,44 +3339,54 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
   // one uniform branch per row tile, not one per element (this code runs once
   // per solve on a CU whose instruction cache the LM kernels have refilled, so
   // every taken branch into cold code costs an L2 fetch).
+  double l0[16];  // L_{rows[0]} J, kept for this column's product tasks with a = 0
   auto row_tile = [&](auto QC, int q) {
     constexpr int qc = decltype(QC)::value;  // 0, 1: rows 0 / 1; 2: any later row
     const int I = S[ro + q];
     const int ko = S[uo + 2 * q], kc = S[uo + 2 * q + 1];
 #pragma unroll
-    for (int s2 = 0; s2 < 4; ++s2) {
-      if constexpr (qc < 2) acc[s2] = racc[qc][s2];
-      else acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
-    }
-    // Rows 0 and 1 have at most the last child left (its L_Jk still in Xf from
-    // (1): only L_Ik is loaded, into Yf); the staged A_IJ goes to Yf so that Xf
-    // keeps L_Jk for row 1.  Later rows load both tiles (loads in flight together)
-    // and stage into Xf.
+    for (int s2 = 0; s2 < 4; ++s2) acc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+    // Rows 0 and 1: the k list's product slots (after the list), summed in list
+    // order, each a 64x64 term in the accumulator layout; the staged A_IJ goes
+    // to Yf.  Later rows load both tiles (loads in flight together), MFMA the
+    // term here and stage into Xf.
     double* stg = qc < 2 ? Yf : Xf;
-    int u0 = 0;
-    if constexpr (qc < 2) u0 = rptr[qc];
-    for (int u = u0; u < kc && ok; ++u) {
-      const int k = S[ko + u];
-      ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);  // (J, k) was waited for in (1)
-      if (!ok) break;
-      if (qc < 2 && k == S[so + sc - 1]) {
-        tile_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, L.N, Yf);
-        __syncthreads();
-        gemm_xyT_acc(Yf, Xf, acc, nblk(k));
-      } else {
-        // (cannot happen for rows 0 and 1 with the schedule's ordered k lists;
-        // kept general: Xf's L_Jk of the last child is then reloaded below)
+    if constexpr (qc < 2) {
+      if (kc > 0) ok = flow_wait_many(F.pf, S + ko + kc, kc, epoch, fail, &shf);
+#ifdef SLAM_FLOW_PROFILE
+      if (q == 0) FLOW_LDS(5);
+#endif
+      for (int u0 = 0; u0 < kc && ok; u0 += 2) {
+        double cv[2][16];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const double* Cp = prod + (size_t)S[ko + kc + min(u0 + h, kc - 1)] * kTB * kTB;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) cv[h][e] = ld_sc1(Cp + ((4 * w + (e >> 2)) * 4 + (e & 3)) * 64 + lane);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          if (u0 + h < kc) {
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[s2][r] += cv[h][4 * s2 + r];
+          }
+      }
+#ifdef SLAM_FLOW_PROFILE
+      if (q == 0) FLOW_LDS(6);
+#endif
+    } else {
+      for (int u = 0; u < kc && ok; ++u) {
+        const int k = S[ko + u];
+        ok = flow_wait(F.tile + I * T + k, epoch, fail, &shf);  // (J, k) was waited for in (1)
+        if (!ok) break;
         tiles2_to_frag_sc1(A + (size_t)I * kTB * L.N + k * kTB, A + (size_t)J * kTB * L.N + k * kTB, L.N,
                            Yf, Xf);
         __syncthreads();
         gemm_xyT_acc(Yf, Xf, acc, nblk(k));
-        if (qc < 2 && sc > 0) {
-          __syncthreads();
-          const int kl = S[so + sc - 1];
-          tile_to_frag_sc1(A + (size_t)J * kTB * L.N + kl * kTB, L.N, Xf);
-        }
+        __syncthreads();
       }
-      __syncthreads();
     }
     if (!ok) return;
     if (q == 0) FLOW_S(2);
@@ -3413,9 +3413,6 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
         const int row = w * 16 + (lane >> 4) + 4 * r, col = s2 * 16 + (lane & 15);
         stg[frag_swz(row, col)] = a[4 * s2 + r] - acc[s2][r];
       }
-#ifdef SLAM_FLOW_PROFILE
-    if (q == 0 && lane == 0) flow_lds[w < 3 ? 5 + w : 14] = wall_clock64();
-#endif
     __syncthreads();
     if (q == 0) FLOW_S(3);
     d4 lacc[4];
@@ -3435,6 +3432,48 @@ void k_tl3_flow(slam_ba_problem p, int T_) {
       }
     flow_publish(F.tile + I * T + J, epoch);
     if (q == 0) FLOW_S(5);
+    if (q == 0) {
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) l0[4 * s2 + r] = lacc[s2][r];
+    }
+    // this column's product tasks with b = q: L_IJ (this row tile, X operand)
+    // times L_{rows[a]} J^T (row 0 from registers, others reloaded), into the
+    // slot; the publish's barrier ended every read of Xf / Yf
+    bool xs = false;
+    for (int e = 0; e < n_tk; ++e) {
+      if (tkJ[3 * e + 1] != q) continue;  // (uniform)
+      const int ta = tkJ[3 * e], slot = tkJ[3 * e + 2];
+      if (!xs) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Xf[frag_idx(w * 16 + (lane >> 4) + 4 * r, s2 * 16 + (lane & 15))] = lacc[s2][r];
+        xs = true;
+      }
+      if (ta == 0) {
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            Yf[frag_idx(w * 16 + (lane >> 4) + 4 * r, s2 * 16 + (lane & 15))] = l0[4 * s2 + r];
+      } else {
+        tile_to_frag_sc1(A + (size_t)S[ro + ta] * kTB * L.N + J * kTB, L.N, Yf);
+      }
+      __syncthreads();
+      d4 pacc[4];
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) pacc[s2] = d4{0.0, 0.0, 0.0, 0.0};
+      gemm_xyT_acc(Xf, Yf, pacc, nbJ);
+      double* Cp = prod + (size_t)slot * kTB * kTB;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_sc1(Cp + ((4 * w + s2) * 4 + r) * 64 + lane, pacc[s2][r]);
+      flow_publish(F.pf + slot, epoch);  // (its barrier also ends this task's Yf reads)
+    }
   };
   if (ok && rc > 0) row_tile(std::integral_constant<int, 0>{}, 0);
   if (ok && rc > 1) row_tile(std::integral_constant<int, 1>{}, 1);
@@ -3741,7 +3780,7 @@ static int tl_check_sched(const slam_ba_problem& p) {
   const int32_t* h = p.tl_sched_host;
   const int n = 9 * p.n_cams, T = h[1];
   SLAM_REQUIRE(T >= (n + kTB - 1) / kTB && h[2] == kTlHdr && h[3] == kTlHdr + n &&
-                   h[6] == kTlHdr + n + T * kTB && h[8] > 0 && h[9] > 0,
+                   h[6] == kTlHdr + n + T * kTB && h[8] > 0 && h[9] > 0 && h[10] > h[9] && h[11] >= 0,
                "slam_ba: tl_sched layout is not ba.tl_schedule's (T %d, offsets %d %d %d for n %d)", T,
                h[2], h[3], h[6], n);
   return SLAM_OK;
@@ -3997,12 +4036,14 @@ int check_problem(const slam_ba_problem* p) {
 
 extern "C" int slam_ba_red_slots(int n_grps) { return 2 * n_grps; }
 
-extern "C" long long slam_ba_chol_len(int n_cams, int n_tiles) {
-  // tiled factor workspace (9C > kLdsMaxN) for a schedule of n_tiles tiles
-  // (tl_sched[1]); n_tiles <= 0: the fewest 64-row tiles that hold 9C rows
+extern "C" long long slam_ba_chol_len(int n_cams, const int32_t* tl_sched_host) {
+  // tiled factor workspace (9C > kLdsMaxN) for a schedule of tl_sched_host[1]
+  // tiles and tl_sched_host[11] product slots; no schedule: the fewest 64-row
+  // tiles that hold 9C rows, no slots
   if (n_cams <= 0) return 0;
   const int n = 9 * n_cams;
-  return TlLayout(n, n_tiles > 0 ? n_tiles : (n + kTB - 1) / kTB).total;
+  if (tl_sched_host == nullptr) return TlLayout(n, (n + kTB - 1) / kTB).total;
+  return TlLayout(n, tl_sched_host[1]).with_slots(tl_sched_host[11]);
 }
 
 extern "C" long long slam_ba_sys_len(int n_cams, int n_blocks) {

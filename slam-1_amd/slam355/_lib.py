@@ -98,7 +98,7 @@ SIGNATURES = {
     "slam_ba_jacobian": [c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p],
     "slam_ba_red_slots": [c_int],
     "slam_ba_sys_len": [c_int, c_int],
-    "slam_ba_chol_len": [c_int, c_int],
+    "slam_ba_chol_len": [c_int, c_p],
     "slam_ba_build_system": [_PROB, c_p],
     "slam_ba_solve_step": [_PROB, c_p],
     "slam_ba_decide": [_PROB, c_p],

@@ -318,7 +318,7 @@ def tl_schedule(n_cams, blocks, mode=None):
       [0] nlev, [1] T, [2] row map offset, [3] inverse row map offset,
       [4] level table offset, [5] column table offset, [6] tile size table
       offset, [7] epilogue table offset, [8] block index table offset,
-      [9] gather table offset
+      [9] gather table offset, [10] product task table offset, [11] product slots
       row map: row r of S -> row of the tiled system (tile * 64 + position)
       inverse row map: row of the tiled system -> row of S, -1 on padding rows
       tile sizes: per tile its rows of S (they come first, padding after)
@@ -326,7 +326,8 @@ def tl_schedule(n_cams, blocks, mode=None):
         rows: I > J with L_IJ != 0 (ascending); rs: k < J with L_Jk != 0
         (by elimination-tree level, then index: the updates of the diagonal
         tile and the forward substitution); upd: per row I, (koff, kcnt) -- the
-        k < J with L_Ik and L_Jk both nonzero (in rs order)
+        k < J with L_Ik and L_Jk both nonzero (in rs order), followed by their
+        product slots (rows 0 and 1; -1 for later rows)
       level table: per level (pan_off, pan_cnt, upd_off, upd_cnt, bk_off, bk_cnt)
       panel entries (k, I)         -- I == k: the diagonal tile
       update entries (I, J, koff, kcnt), I >= J, k list in `koff`
@@ -335,7 +336,9 @@ def tl_schedule(n_cams, blocks, mode=None):
       block index table: [C][C], the packed block of cameras (c1 <= c2), -1 if none
       gather table: per column its offset (T), then per column the packed-S
         offsets of its diagonal and row tiles' elements [1 + rows][64][64]
-        (-1 zero, -2 unit diagonal) and its diagonal tile's rows of S [64]"""
+        (-1 zero, -2 unit diagonal) and its diagonal tile's rows of S [64]
+      product task table: per column k (off, cnt), then its tasks (a, b, slot):
+        form L_{rows[b]} k L_{rows[a]} k^T into the slot (ordered by b)"""
     blocks = np.asarray(blocks, np.int64).reshape(-1, 2)
     n = 9 * int(n_cams)
     tiles = tile_rows(int(n_cams), blocks, mode)
@@ -365,7 +368,7 @@ def tl_schedule(n_cams, blocks, mode=None):
             level[parent[k]] = max(level[parent[k]], level[k] + 1)
     nlev = max(level) + 1 if T else 0
     cols = [[k for k in range(T) if level[k] == lv] for lv in range(nlev)]
-    head = [nlev, T, 0, 0, 0, 0, 0, 0, 0, 0]
+    head = [nlev, T, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]
     table = []
     lists = []  # (k lists / struct lists) appended after the entries
 
@@ -438,14 +441,27 @@ def tl_schedule(n_cams, blocks, mode=None):
         tail.extend(vals)
         return base + len(tail) - len(vals)
 
+    # product slots: every term L_Ik L_Jk^T of column J's rows 0 and 1 is formed
+    # by column k itself once both of its tiles exist (k's task (a, b, slot):
+    # its row tiles a = J and b = I), and column J sums the slots of a row's k
+    # list (stored after the list) in list order
+    n_slot = 0
+    tasks = [[] for _ in range(T)]
     for J in range(T):
         rows = sorted(struct[J])
         r_off = put(rows)
         s_off = put(rs[J])
         pairs = []
-        for I in rows:
+        for qi, I in enumerate(rows):
             ks = [k for k in rs[J] if I in struct[k]]
-            pairs.append((put(ks), len(ks)))
+            sl = [-1] * len(ks)
+            if qi < 2:
+                sl = list(range(n_slot, n_slot + len(ks)))
+                n_slot += len(ks)
+                for k, sk in zip(ks, sl):
+                    rk = sorted(struct[k])
+                    tasks[k].append((rk.index(J), rk.index(I), sk))
+            pairs.append((put(ks + sl), len(ks)))
         u_off = put([v for pr in pairs for v in pr])
         recs[5 * J:5 * J + 5] = [r_off, len(rows), s_off, len(rs[J]), u_off]
     # the cameras whose share of the solve's epilogue (trial parameters,
@@ -496,10 +512,21 @@ def tl_schedule(n_cams, blocks, mode=None):
     gt = np.concatenate(gtab) if gtab else np.zeros(0, np.int64)
     if o >= 2 ** 31:
         raise ValueError("tl_schedule: the gather tables exceed int32 offsets")
-    out = np.asarray(flat + recs + tail + epi + bix.ravel().tolist() + gofs + gt.tolist(), np.int32)
+    # product task table: per column (off, cnt), then its tasks (a, b, slot) by b
+    pt_base = gt_base + T + len(gt)
+    ptab, lo = [], pt_base + 2 * T
+    for tk in tasks:
+        ptab += [lo, len(tk)]
+        lo += 3 * len(tk)
+    ptab += [v for tk in tasks for e in sorted(tk, key=lambda e: (e[1], e[0])) for v in e]
+    if lo >= 2 ** 31:
+        raise ValueError("tl_schedule: the schedule exceeds int32 offsets")
+    out = np.asarray(flat + recs + tail + epi + bix.ravel().tolist() + gofs + gt.tolist() + ptab, np.int32)
     out[7] = epi_off
     out[8] = bix_off
     out[9] = gt_base
+    out[10] = pt_base
+    out[11] = n_slot
     return out
 
 
@@ -987,7 +1014,7 @@ class BAProblem:
         up = [("cams0", cams), ("pts0", pts), ("cams1", cams), ("pts1", pts), ("init_c", cams),
               ("init_p", pts), ("obs_q", qs[pl["order"]] if self.O else np.zeros((1, 2)))]
         zero = [("camrec0", C * 32), ("camrec1", C * 32), ("cpart", n_cs * 112), ("bpart", n_bs * 81),
-                ("sys", self.sys_len), ("chol", _lib.lib.slam_ba_chol_len(C, int(self._sched_host[1]))
+                ("sys", self.sys_len), ("chol", _lib.lib.slam_ba_chol_len(C, self._sched_host.ctypes.data)
                                    if self.tl_levels else 1),
                 ("delta_c", C9), ("red_part", _lib.lib.slam_ba_red_slots(G)), ("small", 4),
                 ("state", N_STATE)]

@@ -844,7 +844,9 @@ def _emulate_tl_flow(S, b, sched):
     """The dataflow tiled solve (csrc/ba.hip k_tl3_flow) restated in NumPy,
     column by column from the schedule's column table: the diagonal tile's
     updates over rs(J), its factor and inverse, y_J; each row tile's updates
-    over its k list and L_IJ = A_IJ L_JJ^-T; then x_J from the rows' x_I."""
+    over its k list (rows 0 and 1: the product slots that the k formed
+    themselves, through the product task table) and L_IJ = A_IJ L_JJ^-T; then
+    x_J from the rows' x_I."""
     T = int(sched[1])
     fo = int(sched[5])
     rec = sched[fo:fo + 5 * T].reshape(-1, 5)
@@ -853,19 +855,40 @@ def _emulate_tl_flow(S, b, sched):
     A, bb, rn = _tiled_system(S, b, sched)
     t = lambda I: slice(I * TB, (I + 1) * TB)  # noqa: E731
     dinv, y, x = {}, np.zeros(N), np.zeros(N)
+    pt = int(sched[10])
+    prod, seen = {}, set()
     for J in range(T):
         ro, rc, so, sc, uo = rec[J]
         rs = sched[so:so + sc]
+        rows = sched[ro:ro + rc]
         for k in rs:
             A[t(J), t(J)] -= A[t(J), t(k)] @ A[t(J), t(k)].T
         dinv[J] = np.linalg.inv(np.linalg.cholesky(A[t(J), t(J)]))
         r = bb[t(J)] - sum((A[t(J), t(k)] @ y[t(k)] for k in rs), np.zeros(TB))
         y[t(J)] = dinv[J] @ r
-        for q, I in enumerate(sched[ro:ro + rc]):
+        for q, I in enumerate(rows):
             ko, kc = sched[uo + 2 * q], sched[uo + 2 * q + 1]
-            for k in sched[ko:ko + kc]:
-                A[t(I), t(J)] -= A[t(I), t(k)] @ A[t(J), t(k)].T
+            if q < 2:
+                for k, sl in zip(sched[ko:ko + kc], sched[ko + kc:ko + 2 * kc]):
+                    assert k < J and sl in prod  # formed by column k, earlier
+                    A[t(I), t(J)] -= prod[sl]
+            else:
+                assert (sched[ko + kc:ko + 2 * kc] == -1).all()
+                for k in sched[ko:ko + kc]:
+                    A[t(I), t(J)] -= A[t(I), t(k)] @ A[t(J), t(k)].T
             A[t(I), t(J)] = A[t(I), t(J)] @ dinv[J].T
+        # this column's product tasks (a, b, slot), ordered by b: rows[b]'s
+        # L times rows[a]'s L^T, with rows[b] among rows[a]'s first two rows
+        off, cnt = sched[pt + 2 * J], sched[pt + 2 * J + 1]
+        tk = sched[off:off + 3 * cnt].reshape(-1, 3)
+        assert (np.diff(tk[:, 1]) >= 0).all()
+        for a, b_, sl in tk:
+            assert a < b_ < rc and sl not in seen
+            seen.add(sl)
+            Ja, Ib = rows[a], rows[b_]
+            assert Ib in sched[rec[Ja][0]:rec[Ja][0] + min(2, rec[Ja][1])]
+            prod[sl] = A[t(Ib), t(J)] @ A[t(Ja), t(J)].T
+    assert seen == set(range(int(sched[11])))
     for J in reversed(range(T)):
         ro, rc = rec[J][:2]
         r = y[t(J)].copy()
