@@ -294,6 +294,52 @@ def tile_rows(n_cams, blocks, mode=None):
     return [[9 * c + i for c in cams for i in range(9)] for cams in out]
 
 
+# k_tl3_flow's phase costs in us (profiles/r6/prod_slots, C4 / C5 per-column
+# stamps): tile hand-off, one child's diagonal update, the tile factor, a row
+# tile's staging + product + publish, a product slot's wait + load, a product
+# task, a later row tile's update per k
+_FLOW_COST = dict(start=4.0, hand=2.6, child=1.5, factor=10.6, row=2.6, slot=2.1, task=2.0, fold=3.0)
+
+
+def _flow_rs_order(T, struct, level):
+    """rs(J) of the dataflow solve (every k < J with L_Jk != 0) ordered by the
+    predicted time its tile (J, k) is published: columns are simulated in index
+    order (children first) with _FLOW_COST, each column taking its rs tiles in
+    the order chosen for it, its row tiles after its factor (rows 0 and 1 once
+    their product slots are in) and its product tasks after the row tile they
+    need.  Ties: elimination-tree level, then index."""
+    c = _FLOW_COST
+    pub, prod_t, out = {}, {}, []
+    for J in range(T):
+        ks = [k for k in range(J) if J in struct[k]]
+        t_in = {k: pub[(k, J)] + c["hand"] for k in ks}
+        order = sorted(ks, key=lambda k: (round(t_in[k], 6), level[k], k))
+        out.append(order)
+        t = c["start"]
+        for k in order:
+            t = max(t, t_in[k]) + c["child"]
+        t += c["factor"]
+        rows = sorted(struct[J])
+        tasks = {}  # b -> [(a, b)]: J forms L_{rows[b]} J L_{rows[a]} J^T after row b
+        for a, Ja in enumerate(rows):
+            first2 = sorted(struct[Ja])[:2]
+            for b in range(a + 1, len(rows)):
+                if rows[b] in first2:
+                    tasks.setdefault(b, []).append(a)
+        for q, I in enumerate(rows):
+            kl = [k for k in order if I in struct[k]]
+            if q < 2 and kl:
+                t = max(t, max(prod_t[(k, J, I)] for k in kl)) + c["slot"]
+            else:
+                t += c["fold"] * len(kl)
+            t += c["row"]
+            pub[(J, I)] = t
+            for a in tasks.get(q, []):
+                t += c["task"]
+                prod_t[(J, rows[a], I)] = t
+    return out
+
+
 def tl_schedule(n_cams, blocks, mode=None):
     """Level schedule of the tiled camera solve (csrc/ba.hip tl_solve_levels).
 
@@ -425,12 +471,11 @@ def tl_schedule(n_cams, blocks, mode=None):
     flat = (head + rowmap.tolist() + irow.tolist() + [len(r) for r in tiles] + table + ents
             + [v for li in lists for v in li])
     # column table of the dataflow solve.  rs(J) in the order its tiles are
-    # expected to be published -- by elimination-tree level, then index -- so a
-    # column accumulates the tiles of its early (low-level) children while the
-    # late ones are still being factored, instead of waiting on the first
+    # expected to be published (_flow_rs_order: a cost model of k_tl3_flow's
+    # phases), so a column accumulates the tiles of its early children while
+    # the late ones are still being factored, instead of waiting on the first
     # listed tile (the sums keep this fixed order: deterministic)
-    rs = [sorted((k for k in range(J) if J in struct[k]), key=lambda k: (level[k], k))
-          for J in range(T)]
+    rs = _flow_rs_order(T, struct, level)
     flow_off = len(flat)
     flat[5] = flow_off
     recs = [0] * (5 * T)
