@@ -60,6 +60,28 @@ struct BaBatch {
   slam_ba_problem p[kBaMaxBatch];
 };
 #define BA_PROB(b) const slam_ba_problem& p = (b).p[blockIdx.y]
+// The batched per-observation / per-block launches (grid x = the problem's
+// workgroups, y = problem) with 8k problems: workgroups are dealt round-robin
+// over the 8 XCDs (for speed only; nothing depends on it), so the linear
+// workgroup id is remapped to keep each problem's workgroups on one XCD --
+// problem w's observations, points and partial rows stay in that XCD's L2
+// from k_lin_mfma through k_assemble to k_back_trial.  The same (x, problem)
+// pairs run either way, so results do not change.
+#ifndef SLAM_BA_XCD
+#define SLAM_BA_XCD 1
+#endif
+__device__ __forceinline__ int2 ba_xcd_map() {
+  const int gx = (int)gridDim.x, n = (int)gridDim.y;
+  if (!SLAM_BA_XCD || n < 8 || (n & 7)) return int2{(int)blockIdx.x, (int)blockIdx.y};
+  const int lin = (int)blockIdx.y * gx + (int)blockIdx.x;
+  const int xcd = lin & 7, slot = lin >> 3;  // n gx / 8 slots per XCD: its n / 8 problems
+  const int wi = slot / gx;
+  return int2{slot - wi * gx, xcd + 8 * wi};
+}
+#define BA_PROB_X(b)                 \
+  const int2 bw_ = ba_xcd_map();     \
+  const int bx = bw_.x;              \
+  const slam_ba_problem& p = (b).p[bw_.y]
 // the batch travels by value in the kernel arguments: 16 x 392 B,
 // beyond the traditional 4 KB; ROCm 7.2 takes it (tests/test_ba.py launches 16)
 static_assert(sizeof(slam_ba_problem) <= 392, "slam_ba_problem grew: re-check the kernarg size");
@@ -531,8 +553,8 @@ __device__ __forceinline__ void lin_slots(const slam_ba_problem& p, LinLds& L, i
 #define LIN_T(i) (void)0
 #endif
 __global__ __launch_bounds__(kLinWG) void k_linearize(BaBatch bat) {
-  BA_PROB(bat);
-  const int g = blockIdx.x;
+  BA_PROB_X(bat);
+  const int g = bx;
   if (g >= p.n_grps) return;  // batch: grid.x covers the largest problem
   lm_wave_priority();
   __shared__ LinLds L;
@@ -844,8 +866,8 @@ __device__ void lin_fold_assemble(const slam_ba_problem& p, const int* cams, int
 }
 
 __global__ __launch_bounds__(kMWG) void k_lin_mfma(BaBatch bat) {
-  BA_PROB(bat);
-  const int sg = blockIdx.x;
+  BA_PROB_X(bat);
+  const int sg = bx;
   if (sg >= p.n_sgrps) return;  // batch: grid.x covers the largest problem
   LINM_DECL();
   lm_wave_priority();
@@ -1251,13 +1273,13 @@ __device__ void rows_sum(const double* __restrict__ part, int stride, int rb, in
 // needs no separate clearing.  Packed layout: each listed block is written
 // once, full 9x9, at sys + 81 * blk.
 __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
-  BA_PROB(bat);
-  if ((int)blockIdx.x >= (p.asm_act != nullptr ? p.n_asm_act : p.n_blocks)) return;
+  BA_PROB_X(bat);
+  if (bx >= (p.asm_act != nullptr ? p.n_asm_act : p.n_blocks)) return;
   lm_wave_priority();
   __shared__ double red[kAsmWG / 81][kCPart];
   __shared__ double sh[kCPart];
   __shared__ double sb[81];
-  const int blk = p.asm_act != nullptr ? p.asm_act[blockIdx.x] : (int)blockIdx.x;
+  const int blk = p.asm_act != nullptr ? p.asm_act[bx] : bx;
   if (p.asm_act != nullptr) {
     // this workgroup's share of the zeros of the unlisted blocks and of the
     // vector entries of the cameras without rows (what the assembly writes for
@@ -1266,7 +1288,7 @@ __global__ __launch_bounds__(kAsmWG) void k_assemble(BaBatch bat) {
     const int32_t* listed = p.asm_act + p.n_asm_act;  // [n_blocks] 0/1
     const int32_t* camrows = listed + p.n_blocks;      // [n_cams] 0/1
     const size_t ns = (size_t)p.n_blocks * 81, c9 = 9 * (size_t)p.n_cams, nv = ns + 3 * c9 + p.n_cams;
-    for (size_t i = (size_t)blockIdx.x * kAsmWG + threadIdx.x; i < nv; i += (size_t)p.n_asm_act * kAsmWG) {
+    for (size_t i = (size_t)bx * kAsmWG + threadIdx.x; i < nv; i += (size_t)p.n_asm_act * kAsmWG) {
       if (i < ns) {
         if (!listed[i / 81]) p.sys[i] = -0.0;
       } else {
@@ -3833,8 +3855,8 @@ __device__ void lm_decide(double* __restrict__ state, const double* __restrict__
 // decision.
 template <bool DECIDE>
 __global__ __launch_bounds__(kGrp) void k_back_trial(BaBatch bat) {
-  BA_PROB(bat);
-  const int g = blockIdx.x, G = p.n_grps;
+  BA_PROB_X(bat);
+  const int g = bx, G = p.n_grps;
   if (g >= G) return;  // batch: grid.x covers the largest problem (not in the ticket count)
   double* __restrict__ part = p.red_part;
   lm_wave_priority();
