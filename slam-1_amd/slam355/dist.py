@@ -16,17 +16,59 @@ from __future__ import annotations
 import numpy as np
 
 
-def shard_by_anchor(n_cams, n_pts, cam_idx, pt_idx, rank, world):
+# Per-rank cost of a landmark shard's linearisation, assembly and back
+# substitution (k_lin_mfma + k_assemble + k_back_trial), fitted to four C5
+# W = 8 shards measured alone (scripts/shard_split.py; profiles/r6/split and
+# profiles/r6/shard_balance: 150k / 150k / 93k / 158k observations in 1782 /
+# 782 / 1486 / 824 camera-union supergroups, 139.7 / 97.6 / 112.6 / 99.7 us):
+# 25.8 us + 0.25 ns per observation + 43 ns per supergroup, within 0.9 us --
+# a supergroup costs as much as SHARD_SG_OBS observations.
+SHARD_SG_OBS = 172.0
+
+
+def point_costs(n_cams, n_pts, cam_idx, pt_idx, world):
+    """Estimated cost of each point in a landmark shard, in observation units:
+    its observations plus its share of the camera-union supergroup it falls in
+    (ba.plan_mfma_native of the whole problem, chunks per workgroup as a shard of
+    1 / world of it would use).  A loop-closure point whose cameras span the
+    sequence's two ends shares its supergroup with few others (C5: 1947 such
+    points make 1000 of 7251 supergroups).  Observation counts alone when the
+    problem has no camera-union plan."""
+    from .ba import plan_mfma_native
+
+    cam_idx = np.asarray(cam_idx, np.int64)
+    pt_idx = np.asarray(pt_idx, np.int64)
+    w = np.bincount(pt_idx, minlength=n_pts).astype(np.float64)
+    pl = plan_mfma_native(n_cams, n_pts, cam_idx, pt_idx, chunks_per_wg=shard_chunks_per_wg(len(cam_idx) // world))
+    if pl is None:
+        return w
+    pt_of_chunk = pl["grp_ptr"].astype(np.int64)
+    sg = pl["sg_ptr"].astype(np.int64)
+    lo, hi = pt_of_chunk[sg[:-1]], pt_of_chunk[sg[1:]]  # supergroup -> new point range
+    share = np.repeat(SHARD_SG_OBS / np.maximum(hi - lo, 1), hi - lo)
+    w[pl["perm"][:len(share)].astype(np.int64)] += share
+    return w
+
+
+def shard_by_anchor(n_cams, n_pts, cam_idx, pt_idx, rank, world, balance=True):
     """-> (point mask [P] bool, observation mask [O] bool, local point index of
     every observation kept).  Points are sorted by anchor (first observing
-    camera, then index) and cut into `world` contiguous ranges."""
+    camera, then index) and cut into `world` contiguous ranges -- of equal
+    estimated cost (point_costs) with `balance`, of equal point counts without.
+    Every rank computes the same cuts (deterministic host code)."""
     cam_idx = np.asarray(cam_idx, np.int64)
     pt_idx = np.asarray(pt_idx, np.int64)
     first = np.full(n_pts, n_cams, np.int64)
     np.minimum.at(first, pt_idx, cam_idx)
     order = np.lexsort((np.arange(n_pts), first))
+    if balance and world > 1:
+        cw = np.cumsum(point_costs(n_cams, n_pts, cam_idx, pt_idx, world)[order])
+        cuts = np.searchsorted(cw, cw[-1] * np.arange(1, world) / world, side="right")
+        bounds = np.concatenate([[0], cuts, [n_pts]])
+    else:
+        bounds = np.arange(world + 1) * n_pts // world
     mine = np.zeros(n_pts, bool)
-    mine[order[rank * n_pts // world:(rank + 1) * n_pts // world]] = True
+    mine[order[bounds[rank]:bounds[rank + 1]]] = True
     keep = mine[pt_idx]
     remap = -np.ones(n_pts, np.int64)
     remap[mine] = np.arange(int(mine.sum()))

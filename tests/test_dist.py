@@ -98,6 +98,31 @@ def test_shards_partition_points_and_observations():
     assert (sum(m[1].astype(int) for m in masks) == 1).all()
 
 
+def test_shards_balance_estimated_cost_on_a_loop():
+    """Landmark shards of a closed loop (its loop-closure points anchored at
+    keyframe 0 share their camera-union supergroups with few others): the
+    cost-balanced cuts give every rank the same estimated cost (point_costs,
+    within one point's), where equal point counts leave rank 0 heavier; both
+    partition the points, and every rank computes the same cuts."""
+    from slam355.dist import point_costs, shard_by_anchor
+    from slam355.synthetic import ba_problem_loop
+
+    rng = np.random.default_rng(3)
+    C, P, W = 120, 24000, 4
+    _, _, ci, pi, _ = ba_problem_loop(rng, C, P, 6)
+    w = point_costs(C, P, ci, pi, W)
+    for balance in (True, False):
+        masks = [shard_by_anchor(C, P, ci, pi, r, W, balance=balance)[0] for r in range(W)]
+        assert (sum(m.astype(int) for m in masks) == 1).all()
+        cost = np.array([w[m].sum() for m in masks])
+        if balance:
+            assert cost.max() - cost.min() <= 2 * w.max()
+        else:
+            assert cost[0] > 1.05 * cost[1:].max()
+    again = shard_by_anchor(C, P, ci, pi, 1, W)[0]
+    assert np.array_equal(again, shard_by_anchor(C, P, ci, pi, 1, W)[0])
+
+
 def _gpu_worker(rank, world, port, out, C=8, P=600, k=4, iters=6, loop=False):
     import sys
 
