@@ -269,7 +269,10 @@ struct KP {  // one kept keypoint of the current level (LDS)
 };
 
 template <bool kGlob>
-__global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(4))) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
+#ifndef SLAM_ORB_WPE
+#define SLAM_ORB_WPE 4  // waves per SIMD the register budget is cut for (4: 128 VGPRs)
+#endif
+__global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(SLAM_ORB_WPE))) void k_orb_tile(const uint8_t* __restrict__ img, OrbGeom g,
                                                      float* __restrict__ ws_kp,
                                                      int32_t* __restrict__ ws_oct,
                                                      uint8_t* __restrict__ ws_desc,
