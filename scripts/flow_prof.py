@@ -83,6 +83,8 @@ for name, C, P, gen in (("C4", 64, 50000, ba_problem), ("C5", 500, 200000, ba_pr
         ff(ctypes.cast(fb, ctypes.c_void_p))
         v = np.array(fb[:14], np.int64) * 10 / 1000.0
         d = np.diff(v)
+        # slots: 3p + 1 wave 0's look-ahead done, 3p + 2 its pivots done,
+        # 3p + 3 the block's barrier passed (p = 3: after the loop)
         print("  factor of column 0 (us): " + " ".join(
-            f"p{p}: w0 {d[3 * p]:.2f} panel {d[3 * p + 1]:.2f} trail {d[3 * p + 2]:.2f}" for p in range(4))
-            + f" | inverse assembly {d[12]:.2f} | total {v[13] - v[0]:.2f}")
+            f"p{p}: look-ahead {d[3 * p]:.2f} pivots {d[3 * p + 1]:.2f} inverse+barrier {d[3 * p + 2]:.2f}"
+            for p in range(4)) + f" | inverse assembly {d[12]:.2f} | total {v[13] - v[0]:.2f}")

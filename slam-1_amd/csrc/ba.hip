@@ -2399,6 +2399,7 @@ __device__ __forceinline__ void blk_factor_w0(double* M, double* Xb, int p, bool
     v[j] = lij;
     FacRest<j>::run(v, -pj, lij);
   });
+  FAC_T(2 + 3 * p);  // (profiling build: wave 0's pivots of block p done)
   // column c = lane of L_pp^-1: x_c = 1 / l_cc, x_i = -(sum_{k<i} l_ik x_k) / l_ii
   // (column-oriented: once x_k is known, every later row's sum takes its
   // term -- the same k order per sum as the row form, a 16-step chain
@@ -2526,6 +2527,7 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
           put(p == 1 ? 0 : (p == 2 ? 3 : 5));
           trail(p, p, p - 1);
         }
+        FAC_T(1 + 3 * p);  // (profiling build: block p's look-ahead done)
         blk_factor_w0(M, Xb, p, ok);
       }
     } else if (p == 1) {  // block column 0's other panel and trailing blocks
@@ -2568,13 +2570,9 @@ __device__ __forceinline__ bool tile_chol_inv_blk(const double* __restrict__ Akk
     }
     if (p < 3) {
       __syncthreads();  // X_pp and block column p-1's blocks published
-      FAC_T(1 + 3 * p);
-      FAC_T(2 + 3 * p);
       FAC_T(3 + 3 * p);
     }
   }
-  FAC_T(10);
-  FAC_T(11);
   FAC_T(12);
   __syncthreads();  // X_33 published
   if (w > 0) X_from(3, w == 1 ? 1 : (w == 2 ? 0 : 2), T3);
