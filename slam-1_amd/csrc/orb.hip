@@ -110,9 +110,23 @@ __device__ __forceinline__ uint32_t quick4(uint32_t v, uint32_t dn, uint32_t rt,
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(d, b));
 }
 
+// -DSLAM_ORB_KO=mask (timing knock-outs, wrong keypoints; never a product
+// build): 1 -- the full FAST test reads only its centre byte; 2 -- the
+// resize reads one source byte per destination pixel instead of four; 4 --
+// the full FAST test reads its 16 circle bytes but scores them trivially
+#ifndef SLAM_ORB_KO
+#define SLAM_ORB_KO 0
+#endif
 // Full segment test + OpenCV cornerScore<16> at c (past the quick reject).
 __device__ __forceinline__ int fast_full(const uint8_t* c, int st) {
   const int v = c[0];
+  if (SLAM_ORB_KO & 1) return v > 128 ? v - 100 : 0;
+  if (SLAM_ORB_KO & 4) {  // the 16 reads kept, the arc minima dropped
+    const int sum = c[3 * st] + c[3 * st + 1] + c[2 * st + 2] + c[st + 3] + c[3] + c[-st + 3] + c[-2 * st + 2] +
+                    c[-3 * st + 1] + c[-3 * st] + c[-3 * st - 1] + c[-2 * st - 2] + c[-st - 3] + c[-3] +
+                    c[st - 3] + c[2 * st - 2] + c[3 * st - 1];
+    return (sum >> 4) > v + 20 ? 30 : 0;
+  }
   int cc[16];  // the circle pixels, d[k] = v - cc[k]
   cc[0] = c[3 * st];
   cc[1] = c[3 * st + 1];
@@ -378,6 +392,8 @@ __global__ __launch_bounds__(kOrbWG) __attribute__((amdgpu_waves_per_eu(SLAM_ORB
           p01[q] = (cx[q] & 511) ? rp[1] : 0;
           p10[q] = d1 ? rp[SP] : 0;
           p11[q] = ((cx[q] & 511) && d1) ? rp[SP + 1] : 0;
+        } else if (SLAM_ORB_KO & 2) {
+          p01[q] = p10[q] = p11[q] = p00[q];
         } else {
           // LDS: past the last source row / column lies more of the LDS
           // allocation (U follows A), and a neighbour outside the source has
