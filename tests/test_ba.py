@@ -318,6 +318,53 @@ def test_gpu_tiled_solver_iterates_match_oracle(C, P, k, mode):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("C,P,k,tiles", [(60, 3000, 8, "rows64"), (40, 2000, 7, "cams:3"),
+                                         (60, 3000, 8, "cams:5")])
+def test_gpu_flow_product_tasks_of_deeper_rows_equal_level_solve(C, P, k, tiles):
+    """Closed loops seen 7-8 keyframes per point: their tile columns have three
+    and more row tiles, so some product tasks form L_Ik L_Jk^T for a column J
+    that is not the task owner's first row tile (the owner reloads that tile
+    instead of keeping it in registers).  Four LM iterates of the dataflow
+    solve equal those of the level-scheduled solve, which forms every such
+    term itself (k_tl2_update): accept flags, costs to 1e-8, cameras to the
+    oracle tests' 1e-6 / 1e-9, points to 1e-6 of their largest coordinate
+    (the sums run in other orders, and these loops amplify rounding over the
+    iterations; a wrong term would show at O(1)); both solve forms are checked
+    against the oracle's Schur LM above."""
+    from slam355 import ba
+    from slam355.synthetic import ba_problem_loop
+
+    rng = np.random.default_rng(5)
+    cams, pts, ci, pi, qs = ba_problem_loop(rng, C, P, k)
+    cams0 = cams.copy()
+    cams0[:, :3] += rng.normal(0, 1e-3, (C, 3))
+    cams0[:, 3:6] += rng.normal(0, 1e-2, (C, 3))
+    pts0 = pts + rng.normal(0, 0.05, pts.shape)
+    runs = {}
+    for mode in ("flow", "levels"):
+        prob = ba.BAProblem(cams0, pts0, ci, pi, qs, tl_mode=mode, tile_mode=tiles)
+        if mode == "flow":
+            S = prob._sched_host
+            T, pt = int(S[1]), int(S[10])
+            tasks = np.concatenate([S[S[pt + 2 * J]:S[pt + 2 * J] + 3 * S[pt + 2 * J + 1]]
+                                    for J in range(T)]).reshape(-1, 3)
+            assert (tasks[:, 0] > 0).any()  # the reload path is taken
+        out = []
+        for _ in range(4):
+            prob.iterate(1)
+            s = prob.state()
+            assert s["CHOL_FAIL"] == 0.0
+            out.append((s["COST_NEW"], s["ACCEPTED"], *prob.params()))
+        runs[mode] = out
+        del prob
+    for a, b in zip(runs["flow"], runs["levels"]):
+        assert a[1] == b[1] and abs(a[0] - b[0]) <= 1e-8 * abs(b[0])
+        assert np.allclose(a[2], b[2], rtol=1e-6, atol=1e-9)
+        # points as a whole (a few low-parallax loop points are ill-determined)
+        assert np.abs(a[3] - b[3]).max() <= 1e-6 * np.abs(b[3]).max()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["flow", "levels"])
 def test_gpu_tiled_solve_failure_leaves_a_zero_step(mode):
     """A damping that makes the camera system indefinite (lambda = -1e6): the
