@@ -379,9 +379,12 @@ typedef struct slam_ba_problem {
    * slam355/ba.py tl_schedule: tiles of whole cameras (64-row tiles, the rows
    * past a tile's cameras padding) in nested-dissection order, with the row
    * maps between S and the tiled system, columns grouped by elimination-tree
-   * level and the dataflow solve's column table.
+   * level, the dataflow solve's column table, epilogue and gather tables and
+   * its product task table (12-int header; the layout is tl_schedule's and is
+   * checked by the launcher).
    * tl_sched is the device copy, tl_sched_host the same array in host memory
-   * (the launcher reads the level counts from it); both or neither. */
+   * (the launcher reads the level counts from it); both or neither. The
+   * workspace `chol` is sized from it: slam_ba_chol_len(n_cams, tl_sched_host). */
   const int32_t* tl_sched;
   const int32_t* tl_sched_host;
   /* lin_mode 1, optional (null: the separate k_assemble launch): the assembly
